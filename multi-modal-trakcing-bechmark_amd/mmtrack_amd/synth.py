@@ -1,0 +1,244 @@
+"""Seeded synthetic weights and frames for the ViPT / OSTrack tracking path.
+
+No checkpoint of the reference ships (``*.pth`` is git-ignored, reference
+``.gitignore:19-20``; ViPT expects ``models/ViPT_<yaml>.pth``,
+``ViPT/lib/test/parameter/vipt.py:25``), so every test, the bench and the
+golden-fixture generator build weights from the same portable law:
+
+* the key / shape list is the reference ``state_dict`` layout
+  (``ViPT/lib/models/vipt/ostrack_prompt.py:94-145`` for ViPT,
+  ``ViPT/lib/models/vipt/ostrack.py:95-144`` for OSTrack),
+* every tensor is drawn from ``torch.Generator`` (CPU mt19937, identical on
+  every host running this image) seeded with ``seed ^ crc32(key)``.
+
+The law is chosen so the random network behaves like a trained one in the
+ways the parity tests care about: peaked attention (so candidate elimination
+is decided by clear margins), a score map with a distinct peak, and sizes
+away from the sigmoid's saturation.
+
+Frames are H x W x C uint8 (RGB + aux), smooth backgrounds plus a bright
+moving target, from numpy's PCG64 (portable across hosts).
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+EMBED = 768
+DEPTH = 12
+HEADS = 12
+MLP = 3072
+PATCH = 16
+
+
+def model_shapes(kind: str = "vipt", prompt_type: str = "vipt_deep", search_size: int = 256,
+                 template_size: int = 128, head_channels: int = 256, in_chans: int = 3) -> "OrderedDict[str, tuple]":
+    """Reference ``state_dict`` keys and shapes.
+
+    kind == "vipt": ``VisionTransformerCE`` of ``vit_ce_prompt.py:84-182`` (+ the
+    leftover ``cls_token`` / 197-row ``pos_embed`` of ``vit.py:137-139``).
+    kind == "ostrack": ``VisionTransformerCE`` of ``vit_ce.py:21-100`` with the
+    ``pos_embed_z/x`` parameters that ``finetune_track`` adds
+    (``base_backbone.py:92-93``).
+    """
+    s = OrderedDict()
+    lz = (template_size // PATCH) ** 2
+    lx = (search_size // PATCH) ** 2
+    s["backbone.cls_token"] = (1, 1, EMBED)
+    s["backbone.pos_embed"] = (1, 197, EMBED)
+    if kind == "vipt":
+        s["backbone.pos_embed_z"] = (1, lz, EMBED)
+        s["backbone.pos_embed_x"] = (1, lx, EMBED)
+    s["backbone.patch_embed.proj.weight"] = (EMBED, in_chans, PATCH, PATCH)
+    s["backbone.patch_embed.proj.bias"] = (EMBED,)
+    if kind == "vipt":
+        s["backbone.patch_embed_prompt.proj.weight"] = (EMBED, in_chans, PATCH, PATCH)
+        s["backbone.patch_embed_prompt.proj.bias"] = (EMBED,)
+        nprompt = DEPTH if prompt_type == "vipt_deep" else 1
+        for i in range(nprompt):
+            p = f"backbone.prompt_blocks.{i}."
+            s[p + "conv0_0.weight"] = (8, EMBED, 1, 1)
+            s[p + "conv0_0.bias"] = (8,)
+            s[p + "conv0_1.weight"] = (8, EMBED, 1, 1)
+            s[p + "conv0_1.bias"] = (8,)
+            s[p + "conv1x1.weight"] = (EMBED, 8, 1, 1)
+            s[p + "conv1x1.bias"] = (EMBED,)
+            s[p + "fovea.smooth"] = (1,)
+        for i in range(nprompt):
+            s[f"backbone.prompt_norms.{i}.weight"] = (EMBED,)
+            s[f"backbone.prompt_norms.{i}.bias"] = (EMBED,)
+    for i in range(DEPTH):
+        p = f"backbone.blocks.{i}."
+        s[p + "norm1.weight"] = (EMBED,)
+        s[p + "norm1.bias"] = (EMBED,)
+        s[p + "attn.qkv.weight"] = (3 * EMBED, EMBED)
+        s[p + "attn.qkv.bias"] = (3 * EMBED,)
+        s[p + "attn.proj.weight"] = (EMBED, EMBED)
+        s[p + "attn.proj.bias"] = (EMBED,)
+        s[p + "norm2.weight"] = (EMBED,)
+        s[p + "norm2.bias"] = (EMBED,)
+        s[p + "mlp.fc1.weight"] = (MLP, EMBED)
+        s[p + "mlp.fc1.bias"] = (MLP,)
+        s[p + "mlp.fc2.weight"] = (EMBED, MLP)
+        s[p + "mlp.fc2.bias"] = (EMBED,)
+    s["backbone.norm.weight"] = (EMBED,)
+    s["backbone.norm.bias"] = (EMBED,)
+    if kind == "ostrack":
+        s["backbone.pos_embed_z"] = (1, lz, EMBED)
+        s["backbone.pos_embed_x"] = (1, lx, EMBED)
+    ch = [EMBED, head_channels, head_channels // 2, head_channels // 4, head_channels // 8]
+    for br in ("ctr", "offset", "size"):
+        for j in range(1, 5):
+            p = f"box_head.conv{j}_{br}."
+            s[p + "0.weight"] = (ch[j], ch[j - 1], 3, 3)
+            s[p + "0.bias"] = (ch[j],)
+            s[p + "1.weight"] = (ch[j],)
+            s[p + "1.bias"] = (ch[j],)
+            s[p + "1.running_mean"] = (ch[j],)
+            s[p + "1.running_var"] = (ch[j],)
+            s[p + "1.num_batches_tracked"] = ()
+    # conv5 comes after all conv1..4 of a branch in the module order of head.py:106-124
+    out = OrderedDict()
+    for k, v in s.items():
+        out[k] = v
+    ordered = OrderedDict()
+    for k, v in out.items():
+        if not k.startswith("box_head"):
+            ordered[k] = v
+    for br, n5 in (("ctr", 1), ("offset", 2), ("size", 2)):
+        for j in range(1, 5):
+            for k, v in out.items():
+                if k.startswith(f"box_head.conv{j}_{br}."):
+                    ordered[k] = v
+        ordered[f"box_head.conv5_{br}.weight"] = (n5, ch[4], 1, 1)
+        ordered[f"box_head.conv5_{br}.bias"] = (n5,)
+    return ordered
+
+
+def _gen(seed: int, key: str) -> torch.Generator:
+    g = torch.Generator()
+    g.manual_seed((int(seed) ^ zlib.crc32(key.encode())) & 0x7FFFFFFFFFFF)
+    return g
+
+
+def _law(key: str, shape: tuple, g: torch.Generator) -> torch.Tensor:
+    if key.endswith("num_batches_tracked"):
+        return torch.tensor(0, dtype=torch.int64)
+
+    def normal(std, mean=0.0):
+        return torch.randn(shape, generator=g) * std + mean
+
+    def uniform(lo, hi):
+        return torch.rand(shape, generator=g) * (hi - lo) + lo
+
+    if key.endswith("fovea.smooth"):
+        return uniform(8.0, 12.0)
+    if "pos_embed" in key or key.endswith("cls_token"):
+        return normal(0.5)
+    if "patch_embed" in key:
+        return normal(0.05) if key.endswith("weight") else normal(0.05)
+    if "prompt_blocks" in key:
+        if key.endswith("weight"):
+            fan_in, fan_out = shape[1], shape[0]
+            bound = math.sqrt(6.0 / (fan_in + fan_out))  # xavier_uniform_, vit_ce_prompt.py:58-60
+            return uniform(-bound, bound)
+        return normal(0.02)
+    if "norm" in key and key.startswith("backbone"):
+        return normal(0.1, 1.0) if key.endswith("weight") else normal(0.05)
+    if ".attn.qkv." in key:
+        return normal(0.07) if key.endswith("weight") else normal(0.05)
+    if ".attn.proj." in key:
+        return normal(0.025) if key.endswith("weight") else normal(0.02)
+    if ".mlp.fc1." in key:
+        return normal(0.03) if key.endswith("weight") else normal(0.02)
+    if ".mlp.fc2." in key:
+        return normal(0.02) if key.endswith("weight") else normal(0.02)
+    if key.startswith("box_head"):
+        if "conv5_size" in key:   # sizes near 0.25 of the search region keep the box scale stable
+            return normal(0.05) if key.endswith("weight") else normal(0.05, -1.1)
+        if "conv5_offset" in key:
+            return normal(0.05) if key.endswith("weight") else normal(0.05, 0.5)
+        if "conv5" in key:
+            return normal(0.3)
+        if key.endswith(".1.weight"):
+            return uniform(0.8, 1.2)
+        if key.endswith(".1.bias"):
+            return normal(0.1)
+        if key.endswith("running_mean"):
+            return normal(0.1)
+        if key.endswith("running_var"):
+            return uniform(0.5, 1.5)
+        if key.endswith("weight"):
+            fan_in = shape[1] * shape[2] * shape[3]
+            return normal(math.sqrt(2.0 / fan_in))  # He-normal keeps ReLU stacks alive
+        return normal(0.05)
+    raise KeyError(key)
+
+
+def make_state_dict(seed: int = 0, **shape_kw) -> "OrderedDict[str, torch.Tensor]":
+    """Seeded fp32 ``state_dict`` in the reference key layout."""
+    sd = OrderedDict()
+    for k, shp in model_shapes(**shape_kw).items():
+        sd[k] = _law(k, shp, _gen(seed, k)).contiguous()
+    return sd
+
+
+# ----------------------------------------------------------------------------- frames
+def make_frames(seed: int, n: int, H: int = 480, W: int = 640, C: int = 6,
+                box=(300.0, 200.0, 40.0, 30.0), drift=(1.5, 0.75)):
+    """Synthetic RGB+aux video: smooth textured background + bright target.
+
+    Returns (frames uint8 [n,H,W,C], gt boxes float64 [n,4] in x,y,w,h)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    # low-frequency background: upsampled coarse noise per channel
+    coarse = rng.integers(0, 256, size=(H // 32 + 2, W // 32 + 2, C)).astype(np.float32)
+    ys = np.linspace(0, coarse.shape[0] - 1.001, H)
+    xs = np.linspace(0, coarse.shape[1] - 1.001, W)
+    y0 = np.floor(ys).astype(int)
+    x0 = np.floor(xs).astype(int)
+    wy = (ys - y0)[:, None, None]
+    wx = (xs - x0)[None, :, None]
+    bg = (coarse[y0][:, x0] * (1 - wy) * (1 - wx) + coarse[y0 + 1][:, x0] * wy * (1 - wx)
+          + coarse[y0][:, x0 + 1] * (1 - wy) * wx + coarse[y0 + 1][:, x0 + 1] * wy * wx)
+    tex = rng.integers(-12, 13, size=(H, W, C)).astype(np.float32)
+    target_col = rng.integers(0, 256, size=(C,)).astype(np.float32)
+    frames = np.empty((n, H, W, C), dtype=np.uint8)
+    gts = np.empty((n, 4), dtype=np.float64)
+    yy = np.arange(H, dtype=np.float32)[:, None]
+    xx = np.arange(W, dtype=np.float32)[None, :]
+    x, y, w, h = box
+    for t in range(n):
+        cx = x + 0.5 * w + drift[0] * t + 6.0 * math.sin(0.21 * t)
+        cy = y + 0.5 * h + drift[1] * t + 4.0 * math.cos(0.17 * t)
+        cx = min(max(cx, w), W - w)
+        cy = min(max(cy, h), H - h)
+        m = np.exp(-(((xx - cx) / (0.5 * w)) ** 4 + ((yy - cy) / (0.5 * h)) ** 4))[..., None]
+        noise = rng.integers(-6, 7, size=(H, W, C)).astype(np.float32)
+        img = bg * (1 - m) + target_col * m + tex + noise
+        frames[t] = np.clip(img, 0, 255).astype(np.uint8)
+        gts[t] = (cx - 0.5 * w, cy - 0.5 * h, w, h)
+    return frames, gts
+
+
+def make_patch(seed: int, size: int, C: int = 6) -> np.ndarray:
+    """A single synthetic crop (size x size x C uint8) with a centred target."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    coarse = rng.integers(0, 256, size=(size // 16 + 2, size // 16 + 2, C)).astype(np.float32)
+    idx = np.linspace(0, coarse.shape[0] - 1.001, size)
+    i0 = np.floor(idx).astype(int)
+    w = (idx - i0)
+    bg = (coarse[i0][:, i0] * ((1 - w)[:, None, None] * (1 - w)[None, :, None])
+          + coarse[i0 + 1][:, i0] * (w[:, None, None] * (1 - w)[None, :, None])
+          + coarse[i0][:, i0 + 1] * ((1 - w)[:, None, None] * w[None, :, None])
+          + coarse[i0 + 1][:, i0 + 1] * (w[:, None, None] * w[None, :, None]))
+    yy = np.arange(size, dtype=np.float32)[:, None]
+    c = size / 2 + rng.uniform(-size / 8, size / 8, size=2)
+    r = size / 8
+    m = np.exp(-(((yy - c[1]) / r) ** 2 + ((yy.T - c[0]) / r) ** 2))[..., None]
+    col = rng.integers(0, 256, size=(C,)).astype(np.float32)
+    img = bg * (1 - m) + col * m + rng.integers(-10, 11, size=(size, size, C))
+    return np.clip(img, 0, 255).astype(np.uint8)

@@ -1,0 +1,339 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+Run in the build container only (needs /root/reference; the GPU box never runs
+this).  It imports the reference's own Python (``/root/reference/ViPT`` and
+``/root/reference/RGBD/models/DeT``) and records its outputs on seeded
+synthetic weights / inputs (``mmtrack_amd.synth``), so both the CPU oracle and
+the HIP engine are checked against numbers the reference produced.
+
+Third-party packages the reference imports but the image lacks are provided as
+minimal in-process modules that restate the *pinned* dependency's published
+behaviour:
+
+* ``timm`` 0.5.4 (``install_vipt.sh:59``): ``to_2tuple``, ``Mlp`` (fc1 -> act ->
+  drop -> fc2 -> drop, the parameter names the state_dict keys depend on),
+  ``DropPath`` (identity in eval), ``trunc_normal_`` (torch's), registry /
+  helper no-ops used only at import time;
+* ``easydict`` (attribute dict, nested dicts converted);
+* ``torchvision.ops.boxes.box_area`` 0.13.1 (``install_vipt.sh:8``);
+* ``cv2``: ``copyMakeBorder`` (constant zero pad) and ``resize`` (the
+  INTER_LINEAR restatement of ``oracle/crop.py`` -- the one unpinned piece);
+* ``vot`` / ``visdom``: empty (debug-only imports).
+
+No reference source is copied; outputs are written as .npz / .json data.
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "multi-modal-trakcing-bechmark_amd"))
+
+from mmtrack_amd import synth  # noqa: E402
+from oracle import crop as ocrop  # noqa: E402
+
+
+# ----------------------------------------------------------------------------- shims
+def _mod(name, **attrs):
+    m = types.ModuleType(name)
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    sys.modules[name] = m
+    return m
+
+
+def install_shims():
+    import collections.abc
+    import torch.nn.functional as F
+
+    def to_2tuple(x):
+        if isinstance(x, collections.abc.Iterable):
+            return tuple(x)
+        return (x, x)
+
+    class Mlp(nn.Module):  # timm 0.5.4 timm/models/layers/mlp.py
+        def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.):
+            super().__init__()
+            out_features = out_features or in_features
+            hidden_features = hidden_features or in_features
+            drop_probs = to_2tuple(drop)
+            self.fc1 = nn.Linear(in_features, hidden_features)
+            self.act = act_layer()
+            self.drop1 = nn.Dropout(drop_probs[0])
+            self.fc2 = nn.Linear(hidden_features, out_features)
+            self.drop2 = nn.Dropout(drop_probs[1])
+
+        def forward(self, x):
+            return self.drop2(self.fc2(self.drop1(self.act(self.fc1(x)))))
+
+    class DropPath(nn.Module):
+        def __init__(self, drop_prob=None):
+            super().__init__()
+            self.drop_prob = drop_prob
+
+        def forward(self, x):
+            assert not self.training or not self.drop_prob
+            return x
+
+    def trunc_normal_(t, mean=0., std=1., a=-2., b=2.):
+        return nn.init.trunc_normal_(t, mean, std, a, b)
+
+    def lecun_normal_(t):
+        return nn.init.normal_(t, std=1.0 / math.sqrt(t.shape[1]))
+
+    def named_apply(fn, module, name='', depth_first=True, include_root=False):
+        for child_name, child in module.named_children():
+            named_apply(fn, child, '.'.join((name, child_name)) if name else child_name, depth_first, True)
+        if include_root:
+            fn(module=module, name=name)
+        return module
+
+    def _unused(*a, **k):
+        raise RuntimeError("not used on the inference path")
+
+    _mod("timm")
+    _mod("timm.models")
+    _mod("timm.models.layers", to_2tuple=to_2tuple, Mlp=Mlp, DropPath=DropPath, trunc_normal_=trunc_normal_,
+         lecun_normal_=lecun_normal_)
+    _mod("timm.models.helpers", build_model_with_cfg=_unused, named_apply=named_apply, adapt_input_conv=_unused)
+    _mod("timm.models.registry", register_model=lambda f: f)
+    _mod("timm.models.vision_transformer", resize_pos_embed=_unused)
+    _mod("timm.data", IMAGENET_DEFAULT_MEAN=(0.485, 0.456, 0.406), IMAGENET_DEFAULT_STD=(0.229, 0.224, 0.225),
+         IMAGENET_INCEPTION_MEAN=(0.5, 0.5, 0.5), IMAGENET_INCEPTION_STD=(0.5, 0.5, 0.5))
+
+    class EasyDict(dict):
+        def __init__(self, d=None, **kwargs):
+            if d is None:
+                d = {}
+            if kwargs:
+                d.update(**kwargs)
+            for k, v in d.items():
+                setattr(self, k, v)
+
+        def __setattr__(self, name, value):
+            if isinstance(value, (list, tuple)):
+                value = [self.__class__(x) if isinstance(x, dict) else x for x in value]
+            elif isinstance(value, dict) and not isinstance(value, self.__class__):
+                value = self.__class__(value)
+            super().__setattr__(name, value)
+            super().__setitem__(name, value)
+
+        __setitem__ = __setattr__
+
+    _mod("easydict", EasyDict=EasyDict)
+
+    def box_area(boxes):
+        return (boxes[:, 2] - boxes[:, 0]) * (boxes[:, 3] - boxes[:, 1])
+    _mod("torchvision")
+    _mod("torchvision.ops")
+    _mod("torchvision.ops.boxes", box_area=box_area)
+
+    def copyMakeBorder(src, top, bottom, left, right, borderType, value=None):
+        pad = [(top, bottom), (left, right)] + [(0, 0)] * (src.ndim - 2)
+        return np.pad(src, pad, mode="constant", constant_values=0)
+
+    def resize(src, dsize, interpolation=1):
+        if src.dtype == np.uint8:
+            return ocrop.cv2_resize_linear_u8(src, dsize[0], dsize[1])
+        # float inputs (att_mask): not used by the tracker's outputs
+        t = torch.tensor(np.ascontiguousarray(src), dtype=torch.float64)[None, None]
+        return F.interpolate(t, size=(dsize[1], dsize[0]), mode="bilinear", align_corners=False)[0, 0].numpy()
+
+    _mod("cv2", copyMakeBorder=copyMakeBorder, resize=resize, BORDER_CONSTANT=0, BORDER_REPLICATE=1,
+         INTER_LINEAR=1, getTickCount=lambda: 0, getTickFrequency=lambda: 1.0)
+    _mod("vot")
+    _mod("visdom", Visdom=object)
+    _mod("visdom.server")
+    _mod("tensorboardX", SummaryWriter=object)
+    for name in ("jpeg4py", "lmdb"):
+        _mod(name)
+
+
+# ----------------------------------------------------------------------------- helpers
+def load_cfg(yaml_name):
+    import importlib
+    cfgmod = importlib.import_module("lib.config.vipt.config")
+    importlib.reload(cfgmod)
+    cfgmod.update_config_from_file(os.path.join(REF, "ViPT/experiments/vipt/%s.yaml" % yaml_name))
+    return cfgmod.cfg
+
+
+def ostrack_cfg(search=384, template=192):
+    cfg = load_cfg("deep_rgbt")
+    cfg.MODEL.BACKBONE.TYPE = "vit_base_patch16_224_ce"
+    cfg.DATA.SEARCH.SIZE = search
+    cfg.DATA.TEMPLATE.SIZE = template
+    cfg.TEST.SEARCH_SIZE = search
+    cfg.TEST.TEMPLATE_SIZE = template
+    cfg.TEST.SEARCH_FACTOR = 5.0
+    return cfg
+
+
+def preprocess(patch):
+    return ocrop.preprocess(patch)
+
+
+def manifest(model):
+    return [[k, list(v.shape)] for k, v in model.state_dict().items()]
+
+
+def run_net(model, cfg, z, x, C):
+    from lib.utils.ce_utils import generate_mask_cond
+    mask = generate_mask_cond(cfg, 1, "cpu", None)
+    with torch.no_grad():
+        out = model.forward(template=z, search=x, ce_template_mask=mask)
+    return out
+
+
+def net_fixture(name, model, cfg, sd, C, tsz, ssz, seeds):
+    res = {"seeds": np.array(seeds)}
+    for j, (sz, ss) in enumerate(seeds):
+        z = preprocess(synth.make_patch(sz, tsz, C))
+        x = preprocess(synth.make_patch(ss, ssz, C))
+        out = run_net(model, cfg, z, x, C)
+        feat_sz = ssz // 16
+        resp = (synth_hann(feat_sz) * out["score_map"]).flatten()
+        top = torch.sort(resp, descending=True).values
+        res[f"score_map_{j}"] = out["score_map"].numpy()
+        res[f"size_map_{j}"] = out["size_map"].numpy()
+        res[f"offset_map_{j}"] = out["offset_map"].numpy()
+        res[f"pred_boxes_{j}"] = out["pred_boxes"].numpy()
+        res[f"removed_{j}"] = np.concatenate([r.numpy() for r in out["removed_indexes_s"]], axis=1).astype(np.int64)
+        res[f"feat_rows_{j}"] = out["backbone_feat"][0, ::8].numpy()
+        res[f"feat_sum_{j}"] = np.array([float(out["backbone_feat"].double().sum())])
+        res[f"resp_argmax_{j}"] = np.array([int(torch.argmax(resp))])
+        res[f"resp_top2gap_{j}"] = np.array([float((top[0] - top[1]) / top[0])])
+    np.savez_compressed(os.path.join(HERE, f"net_{name}.npz"), **res)
+    print("wrote net", name)
+
+
+def synth_hann(sz):
+    from lib.test.utils.hann import hann2d
+    return hann2d(torch.tensor([sz, sz]).long(), centered=True)
+
+
+def tracker_fixture(name, yaml_name, sd, n_frames, seq_seed, H, W, C, init_box):
+    """Run the reference ViPTTrack (lib/test/tracker/vipt.py) on a synthetic sequence."""
+    import lib.test.tracker.vipt as tv
+    # the reference tracker hard-codes .cuda() (vipt.py:23,30; data_utils.py:17-18,22): run it on the CPU
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    nn.Module.cuda = lambda self, *a, **k: self
+    from lib.test.utils.params import TrackerParams
+    params = TrackerParams()
+    params.cfg = load_cfg(yaml_name)
+    cfg = params.cfg
+    params.template_factor = cfg.TEST.TEMPLATE_FACTOR
+    params.template_size = cfg.TEST.TEMPLATE_SIZE
+    params.search_factor = cfg.TEST.SEARCH_FACTOR
+    params.search_size = cfg.TEST.SEARCH_SIZE
+    params.save_all_boxes = False
+    params.debug = 0
+    ckpt = "/tmp/mmtrack_golden_%s.pth" % yaml_name
+    torch.save({"net": sd}, ckpt)
+    params.checkpoint = ckpt
+    tracker = tv.ViPTTrack(params)
+    frames, gts = synth.make_frames(seq_seed, n_frames, H, W, C, box=init_box)
+    boxes = [list(init_box)]
+    scores = [1.0]
+    tracker.initialize(frames[0], {"init_bbox": list(init_box)})
+    for t in range(1, n_frames):
+        o = tracker.track(frames[t])
+        boxes.append([float(v) for v in o["target_bbox"]])
+        scores.append(float(o["best_score"]))
+    os.remove(ckpt)
+    np.savez_compressed(os.path.join(HERE, f"tracker_{name}.npz"), boxes=np.array(boxes), scores=np.array(scores),
+                        meta=np.array([seq_seed, n_frames, H, W, C]), init_box=np.array(init_box, dtype=np.float64))
+    print("wrote tracker", name, np.round(np.array(boxes), 1).tolist(), "gt", np.round(gts, 1).tolist())
+
+
+def crop_fixture():
+    """sample_target geometry from the reference (processing_utils.py) on edge boxes."""
+    from lib.train.data.processing_utils import sample_target
+    rng = np.random.Generator(np.random.PCG64(7))
+    im = rng.integers(0, 256, size=(96, 128, 6), dtype=np.uint8)
+    cases = [(40.0, 30.0, 20.0, 16.0, 4.0, 64), (0.5, 0.5, 10.0, 10.0, 4.0, 64), (100.0, 70.0, 30.0, 30.0, 2.0, 32),
+             (-5.0, -3.0, 12.0, 9.0, 4.0, 64), (110.0, 80.0, 16.0, 16.0, 4.0, 64), (32.0, 32.0, 32.0, 32.0, 2.0, 32),
+             (10.25, 20.75, 7.5, 13.5, 4.0, 48), (60.0, 40.0, 2.0, 2.0, 4.0, 64)]
+    res = {"image": im, "cases": np.array(cases)}
+    for j, (x, y, w, h, f, o) in enumerate(cases):
+        patch, rf, _ = sample_target(im, [x, y, w, h], f, output_sz=int(o))
+        res[f"patch_{j}"] = patch
+        res[f"rf_{j}"] = np.array([rf])
+    np.savez_compressed(os.path.join(HERE, "crop_geometry.npz"), **res)
+    print("wrote crop")
+
+
+def dimp_fixture():
+    """DiMP filter / steepest-descent GN iterates (DeT ltr), the in-tree stand-in for mfDiMP."""
+    sys.path.insert(0, os.path.join(REF, "RGBD/models/DeT"))
+    import ltr.models.layers.filter as filter_layer
+    from ltr.models.target_classifier.optimizer import DiMPSteepestDescentGN
+    g = torch.Generator().manual_seed(11)
+    nimg, nseq, C, H, W = 3, 2, 32, 18, 18
+    feat = torch.randn(nimg, nseq, C, H, W, generator=g)
+    filt = torch.randn(nseq, C, 4, 4, generator=g) * 0.01
+    bb = torch.tensor([[[100.0 + 3 * i, 120.0 - 2 * i, 60.0, 50.0] for _ in range(nseq)] for i in range(nimg)])
+    scores = filter_layer.apply_filter(feat, filt)
+    resid = torch.randn(scores.shape, generator=g)
+    ft = filter_layer.apply_feat_transpose(feat, resid, (4, 4), training=False)
+    opt = DiMPSteepestDescentGN(num_iter=5, feat_stride=16, init_step_length=1.0, init_filter_reg=0.05,
+                                init_gauss_sigma=1.0, num_dist_bins=10, bin_displacement=0.5, mask_init_factor=3.0,
+                                score_act='relu', mask_act='sigmoid')
+    opt.eval()
+    with torch.no_grad():
+        w, iters, losses = opt(filt, feat=feat, bb=bb)
+    sdo = {k: v.numpy() for k, v in opt.state_dict().items()}
+    np.savez_compressed(os.path.join(HERE, "dimp.npz"), feat=feat.numpy(), filt=filt.numpy(), bb=bb.numpy(),
+                        scores=scores.numpy(), resid=resid.numpy(), feat_t=ft.numpy(), final=w.numpy(),
+                        iterates=torch.stack(iters).numpy(), losses=torch.stack(losses).numpy().ravel(),
+                        **{"opt." + k: v for k, v in sdo.items()})
+    print("wrote dimp", [float(l) for l in losses])
+
+
+def main():
+    install_shims()
+    sys.path.insert(0, os.path.join(REF, "ViPT"))
+    torch.set_num_threads(8)
+    from lib.models.vipt import build_viptrack, build_ostrack
+
+    mani = {}
+    # --- ViPT deep / shaw, RGB-T and RGB-D yamls (C2, C3)
+    for yaml_name, seeds in (("deep_rgbt", [(101, 201), (102, 202)]), ("deep_rgbd", [(103, 203)]),
+                             ("shaw_rgbt", [(104, 204)])):
+        cfg = load_cfg(yaml_name)
+        model = build_viptrack(cfg, training=False).eval()
+        pt = cfg.TRAIN.PROMPT.TYPE
+        sd = synth.make_state_dict(0, kind="vipt", prompt_type=pt)
+        model.load_state_dict(sd, strict=True)
+        mani[yaml_name] = manifest(model)
+        net_fixture(yaml_name, model, cfg, sd, 6, 128, 256, seeds)
+    # --- OSTrack-384 RGB (C4)
+    cfg = ostrack_cfg()
+    model = build_ostrack(cfg, training=False).eval()
+    sd = synth.make_state_dict(0, kind="ostrack", search_size=384, template_size=192)
+    model.load_state_dict(sd, strict=True)
+    mani["ostrack384"] = manifest(model)
+    net_fixture("ostrack384", model, cfg, sd, 3, 192, 384, [(105, 205)])
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(mani, f)
+    # --- tracker-level sequences
+    sd = synth.make_state_dict(0, kind="vipt", prompt_type="vipt_deep")
+    tracker_fixture("deep_rgbt", "deep_rgbt", sd, 10, 31, 480, 640, 6, (300.0, 200.0, 40.0, 30.0))
+    crop_fixture()
+    dimp_fixture()
+
+
+if __name__ == "__main__":
+    main()

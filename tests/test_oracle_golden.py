@@ -1,0 +1,82 @@
+"""The CPU oracle against the reference's own outputs (tests/golden/, made by make_golden.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from mmtrack_amd import synth
+from oracle import crop as ocrop
+from oracle import tracker as otracker
+from oracle import vipt as ov
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+NETS = {
+    "deep_rgbt": dict(shape=dict(kind="vipt", prompt_type="vipt_deep"), cfg=ov.NetCfg(), C=6),
+    "deep_rgbd": dict(shape=dict(kind="vipt", prompt_type="vipt_deep"), cfg=ov.NetCfg(), C=6),
+    "shaw_rgbt": dict(shape=dict(kind="vipt", prompt_type="vipt_shaw"), cfg=ov.NetCfg(prompt_type="vipt_shaw"), C=6),
+    "ostrack384": dict(shape=dict(kind="ostrack", search_size=384, template_size=192),
+                       cfg=ov.NetCfg(kind="ostrack", search_size=384, template_size=192), C=3),
+}
+
+
+@pytest.mark.parametrize("name", list(NETS))
+def test_state_dict_layout_matches_reference(name):
+    mani = json.load(open(os.path.join(GOLDEN, "manifest.json")))[name]
+    ours = synth.model_shapes(**NETS[name]["shape"])
+    assert {k: list(v) for k, v in ours.items()} == {k: v for k, v in mani}
+
+
+@pytest.mark.parametrize("name", list(NETS))
+def test_oracle_network_matches_reference(name):
+    spec = NETS[name]
+    torch.set_num_threads(min(8, os.cpu_count()))
+    g = np.load(os.path.join(GOLDEN, f"net_{name}.npz"))
+    sd = synth.make_state_dict(0, **spec["shape"])
+    cfg = spec["cfg"]
+    for j, (sz, ss) in enumerate(g["seeds"]):
+        z = ocrop.preprocess(synth.make_patch(int(sz), cfg.template_size, spec["C"]))
+        x = ocrop.preprocess(synth.make_patch(int(ss), cfg.search_size, spec["C"]))
+        out = ov.forward(sd, z, x, cfg, ov.ce_template_mask(cfg))
+        removed = torch.cat(out["removed_indexes_s"], dim=1).numpy()
+        np.testing.assert_array_equal(removed, g[f"removed_{j}"])
+        for k in ("score_map", "size_map", "offset_map", "pred_boxes"):
+            np.testing.assert_allclose(out[k].numpy(), g[f"{k}_{j}"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(out["backbone_feat"][0, ::8].numpy(), g[f"feat_rows_{j}"], rtol=1e-4, atol=1e-4)
+        resp = (ov.hann2d(cfg.feat_sz) * out["score_map"]).flatten()
+        assert int(torch.argmax(resp)) == int(g[f"resp_argmax_{j}"][0])
+
+
+def test_crop_geometry_matches_reference():
+    g = np.load(os.path.join(GOLDEN, "crop_geometry.npz"))
+    im = g["image"]
+    for j, (x, y, w, h, f, o) in enumerate(g["cases"]):
+        patch, rf = ocrop.sample_target(im, [x, y, w, h], f, int(o))
+        np.testing.assert_array_equal(patch, g[f"patch_{j}"])
+        assert rf == g[f"rf_{j}"][0]
+
+
+def test_oracle_tracker_matches_reference():
+    g = np.load(os.path.join(GOLDEN, "tracker_deep_rgbt.npz"))
+    seed, n, H, W, C = [int(v) for v in g["meta"]]
+    frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
+    sd = synth.make_state_dict(0, kind="vipt", prompt_type="vipt_deep")
+    tr = otracker.OracleTracker(sd, ov.NetCfg())
+    boxes, scores = otracker.run_sequence(tr, frames, g["init_box"])
+    np.testing.assert_allclose(boxes, g["boxes"], rtol=1e-4, atol=2e-2)
+    np.testing.assert_allclose(scores, g["scores"], rtol=1e-4, atol=1e-6)
+
+
+def test_cv2_resize_restatement_properties():
+    """Unpinned piece: self-consistency of the INTER_LINEAR restatement."""
+    rng = np.random.Generator(np.random.PCG64(3))
+    im = rng.integers(0, 256, size=(70, 70, 6), dtype=np.uint8)
+    same = ocrop.cv2_resize_linear_u8(im, 70, 70)          # identity scale reproduces the input
+    np.testing.assert_array_equal(same, im)
+    const = np.full((37, 53, 3), 117, np.uint8)
+    np.testing.assert_array_equal(ocrop.cv2_resize_linear_u8(const, 256, 256), 117)
+    half = ocrop.cv2_resize_linear_u8(im[:64, :64], 32, 32)  # exact 2x -> area average
+    ref = (im[:64:2, :64:2].astype(int) + im[1:64:2, :64:2] + im[:64:2, 1:64:2] + im[1:64:2, 1:64:2] + 2) >> 2
+    np.testing.assert_array_equal(half, ref)
