@@ -66,7 +66,7 @@ def test_oracle_tracker_matches_reference():
     tr = otracker.OracleTracker(sd, ov.NetCfg())
     boxes, scores = otracker.run_sequence(tr, frames, g["init_box"])
     np.testing.assert_allclose(boxes, g["boxes"], rtol=1e-4, atol=2e-2)
-    np.testing.assert_allclose(scores, g["scores"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(scores, g["scores"], rtol=1e-3, atol=1e-5)
 
 
 def test_cv2_resize_restatement_properties():
