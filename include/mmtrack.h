@@ -1,0 +1,128 @@
+/*
+ * mmtrack.h — C ABI of the MI355X-native per-frame tracking engine.
+ *
+ * Drop-in boundary for the reference's per-frame tracker call
+ * (wxltop/Multi-Modal-Trakcing-Bechmark, ViPT):
+ *
+ *   reference                                            this ABI
+ *   ---------------------------------------------------  ---------------------------------------
+ *   ViPTTrack.__init__ + build_viptrack + strict          mmt_create + mmt_set_tensor (every key)
+ *     load_state_dict   (ViPT/lib/test/tracker/vipt.py:18-39,   + mmt_finalize (strict check)
+ *     ViPT/lib/models/vipt/ostrack_prompt.py:94-145)
+ *   ViPTTrack.initialize(image, {'init_bbox'})            mmt_initialize
+ *     (vipt.py:41-62)
+ *   ViPTTrack.track(image) -> {'target_bbox','best_score'} mmt_track   (one sequence)
+ *     (vipt.py:64-110)                                     mmt_track_batch (N independent sequences,
+ *                                                           one launch; the reference runs one
+ *                                                           tracker per Pool worker,
+ *                                                           RGBT_workspace/test_rgbt_mgpus.py:180-184)
+ *   OSTrack.track (ViPT/lib/test/tracker/ostrack.py:75-100) same entry points, cfg.model = OSTRACK
+ *   SiamFC / DiMP correlation (RGBE/models/siamfc (absent), mmt_xcorr
+ *     RGBD/models/DeT/ltr/models/layers/filter.py:5-54)
+ *   DiMPSteepestDescentGN.forward                          mmt_dimp_optimize
+ *     (RGBD/models/DeT/ltr/models/target_classifier/optimizer.py:85-170)
+ *
+ * Conventions: plain pointers and sizes; frames are H x W x C uint8, row-major, channels last
+ * (RGB first, then the aux modality), host or device memory; boxes are [x, y, w, h] doubles in
+ * frame pixels.  Every call returns MMT_OK (0) or a negative error code; mmt_last_error() gives
+ * the message (the Python mirror re-raises it with the reference's exception type and text,
+ * e.g. "Too small bounding box." from processing_utils.py:34-35).  One engine owns one HIP
+ * device + stream; engines are not shared between threads.
+ */
+#ifndef MMTRACK_H_
+#define MMTRACK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mmt_engine mmt_engine;
+
+enum {
+  MMT_OK = 0,
+  MMT_E_ARG = -1,      /* invalid argument (ValueError)                     */
+  MMT_E_STATE = -2,    /* call out of order (e.g. track before initialize)  */
+  MMT_E_HIP = -3,      /* HIP runtime failure                               */
+  MMT_E_WEIGHTS = -4,  /* missing / unexpected / mis-shaped state_dict key  */
+  MMT_E_BOX = -5       /* "Too small bounding box." (processing_utils.py:34-35) */
+};
+
+enum { MMT_MODEL_VIPT = 0, MMT_MODEL_OSTRACK = 1 };
+enum { MMT_PROMPT_NONE = 0, MMT_PROMPT_SHAW = 1, MMT_PROMPT_DEEP = 2 };
+
+typedef struct mmt_config {
+  int model;               /* MMT_MODEL_*                                           */
+  int prompt_type;         /* MMT_PROMPT_* (cfg.TRAIN.PROMPT.TYPE)                  */
+  int in_chans;            /* frame channels: 6 (RGB + aux) for ViPT, 3 for OSTrack */
+  int template_size;       /* cfg.TEST.TEMPLATE_SIZE (128)                          */
+  int search_size;         /* cfg.TEST.SEARCH_SIZE (256)                            */
+  double template_factor;  /* cfg.TEST.TEMPLATE_FACTOR (2.0)                        */
+  double search_factor;    /* cfg.TEST.SEARCH_FACTOR (4.0)                          */
+  int n_ce;                /* len(cfg.MODEL.BACKBONE.CE_LOC)                        */
+  int ce_loc[12];
+  double ce_keep_ratio[12];
+  int ce_template_index;   /* CTR_POINT template token (generate_mask_cond, ce_utils.py:22-35) */
+  int head_channels;       /* cfg.MODEL.HEAD.NUM_CHANNELS (256)                     */
+  int max_batch;           /* sequences (slots) this engine tracks concurrently    */
+  int use_graphs;          /* capture the per-frame launch sequence in a hipGraph   */
+  int debug_outputs;       /* keep crops / score maps / features for parity tests   */
+} mmt_config;
+
+/* lifecycle */
+int mmt_create(const mmt_config* cfg, int device, mmt_engine** out);
+void mmt_destroy(mmt_engine* e);
+const char* mmt_last_error(const mmt_engine* e);
+const char* mmt_version(void);
+
+/* weights: every reference state_dict key, fp32, row-major (load_state_dict(strict=True)) */
+int mmt_set_tensor(mmt_engine* e, const char* key, const float* data, const int64_t* shape, int ndim);
+int mmt_finalize(mmt_engine* e);
+int mmt_num_expected_keys(const mmt_engine* e);
+const char* mmt_expected_key(const mmt_engine* e, int i);
+
+/* tracking (vipt.py:41-110) */
+int mmt_initialize(mmt_engine* e, int slot, const uint8_t* frame, int H, int W, int C, int64_t row_stride,
+                   int is_device, const double init_xywh[4]);
+int mmt_track(mmt_engine* e, int slot, const uint8_t* frame, int H, int W, int C, int64_t row_stride,
+              int is_device, double out_xywh[4], float* out_score);
+int mmt_track_batch(mmt_engine* e, int first_slot, int n, const uint8_t* const* frames, const int* H,
+                    const int* W, int C, const int64_t* row_stride, int is_device, double* out_xywh,
+                    float* out_score);
+int mmt_get_state(const mmt_engine* e, int slot, double out_xywh[4]);
+int mmt_set_state(mmt_engine* e, int slot, const double xywh[4]);
+
+/* parity / debug read-back of the last track call (debug_outputs = 1):
+ *   "crop"   uint8 [S][S][C]  search patch         "maps"  f32 [5][fs*fs] ctr,size_w,size_h,off_x,off_y
+ *   "feat"   f32 [Lz+Lx][768] backbone output      "removed" i32 [Lx] removed slots, CE order
+ *   "result" f32 [8] cx,cy,w,h (normalised), best_score, argmax index                        */
+int mmt_debug_fetch(mmt_engine* e, const char* what, int batch_index, void* dst, size_t nbytes);
+
+/* kernel timing probe: bracket every launch of one kernel class with HIP events on the engine
+ * stream ("fc1", "fc2", "qkv", "proj", "attn", "conv1"); returns launches and summed ms */
+int mmt_timing_enable(mmt_engine* e, const char* kernel_class);
+int mmt_timing_read(mmt_engine* e, int* launches, double* total_ms, double* flops, double* bytes);
+
+/* ---- correlation trackers (device pointers, fp32, NCHW) ---------------------------------- */
+/* out[b][0][y][x] = scale * sum_c,i,j x[b][c][y+i][x+j] * z[b][c][i][j] + bias  (valid)        */
+int mmt_xcorr(const float* z, const float* x, float* out, int B, int C, int hz, int wz, int hx, int wx,
+              float scale, float bias, void* hip_stream);
+
+/* ---- operator-level entry points (device pointers; used by the parity tests and by hosts that
+ *      compose their own pipelines).  epi: 0 bias->bf16, 1 bias+GELU->bf16, 2 C(f32) = R + acc + bias,
+ *      3 bias+ReLU->bf16, 4 bias->f32, 5 bias+ReLU->f32, 6 C(f32) = acc + bias + R[m % pos_rows].
+ *      conv_hw > 0 selects the implicit 3x3 (pad 1) conv A-operand over an NHWC map.            */
+int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, void* C, int64_t ldc,
+                const float* R, int64_t ldr, int M, int N, int K, int epi, int conv_hw, int conv_cin, int pos_rows,
+                void* hip_stream);
+int mmt_op_attention(const void* qkv, void* out, int B, int N, int heads, int ce_query, int ce_lens_t,
+                     float* ce_prob, void* hip_stream);
+int mmt_op_layernorm(const float* x, const float* w, const float* b, void* out_bf16, float* out_f32, int rows,
+                     void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMTRACK_H_ */

@@ -1,0 +1,33 @@
+// Shared device helpers for the MI355X (gfx950 / CDNA4) tracking engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;                                              // storage type
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));            // MFMA A/B fragment
+typedef float f32x4 __attribute__((ext_vector_type(4)));              // 16x16 accumulator
+
+#define WAVE 64
+
+__device__ __forceinline__ bf16_t f2bf(float x) {                    // RNE (v_cvt_pk_bf16_f32)
+  return __builtin_bit_cast(bf16_t, (__bf16)x);
+}
+__device__ __forceinline__ float bf2f(bf16_t x) {
+  return __uint_as_float(((uint32_t)x) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Exact-erf GELU (nn.GELU default; vit_ce_prompt.py:122).
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}

@@ -1,0 +1,1026 @@
+// Host runtime of the MI355X tracking engine: weight packing, HBM layout, the per-frame launch
+// sequence (optionally one hipGraph per batch shape), tracker state and the C ABI of mmtrack.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/mmtrack.h"
+#include "kernels.h"
+
+using namespace mmt;
+
+namespace {
+
+constexpr int C = 768;
+constexpr int HEADS = 12;
+constexpr int DEPTH = 12;
+constexpr int MLPD = 3072;
+
+struct HostTensor {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+};
+
+// -- bf16 round-to-nearest-even on the host (finite inputs)
+inline uint16_t host_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16) | ((u & 0xffff) ? 0x40 : 0);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct LayerW {
+  bf16_t *qkv_w, *proj_w, *fc1_w, *fc2_w;
+  float *qkv_b, *proj_b, *fc1_b, *fc2_b, *n1w, *n1b, *n2w, *n2b;
+};
+struct PromptW {
+  float *w00, *b00, *w01, *b01, *w1, *b1, *nw, *nb;
+  float smooth;
+};
+
+struct TimingProbe {
+  std::string cls;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;  // pool
+  size_t used = 0;
+  long launches = 0;
+  double total_ms = 0, flops = 0, bytes = 0;
+  std::vector<std::pair<double, double>> pending_work;  // flops/bytes of each pending pair
+};
+
+}  // namespace
+
+struct mmt_engine {
+  mmt_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::map<std::string, std::vector<int64_t>> expected;
+  std::vector<std::string> expected_order;
+  std::map<std::string, HostTensor> host;
+  bool finalized = false;
+
+  // geometry
+  int Lz = 0, Lx = 0, L = 0, fs = 0, tfs = 0;
+  std::vector<int> ls_before;   // search tokens entering block i
+  std::vector<int> keep_at;     // search tokens kept after block i (== ls_before[i] if no CE)
+
+  // weights (one arena)
+  void* warena = nullptr;
+  size_t wcap = 0, wused = 0;
+  LayerW lw[DEPTH];
+  PromptW pw[DEPTH];
+  int nprompt = 0;
+  bf16_t *pe_w = nullptr, *pep_w = nullptr;
+  float *pe_b = nullptr, *pep_b = nullptr, *pos = nullptr, *norm_w = nullptr, *norm_b = nullptr;
+  bf16_t* hw1 = nullptr;
+  float* hb1 = nullptr;
+  bf16_t* hw[3] = {};   // conv2..4, [3 branches] contiguous
+  float* hb[3] = {};
+  float *w5 = nullptr, *b5 = nullptr, *hann = nullptr;
+
+  // activations (max_batch)
+  void* aarena = nullptr;
+  bf16_t *A_rgb = nullptr, *A_aux = nullptr, *Hn = nullptr, *QKV = nullptr, *O = nullptr, *Hm = nullptr,
+         *feat = nullptr, *h1 = nullptr, *h2 = nullptr, *h3 = nullptr;
+  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *P = nullptr, *a8 = nullptr,
+        *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
+        *dbg_feat = nullptr;
+  int *gidx0 = nullptr, *gidx1 = nullptr, *slot2pos = nullptr, *gather = nullptr, *removed = nullptr;
+  uint8_t* dbg_patch = nullptr;
+  CropParam* params_dev = nullptr;
+  CropParam* params_host = nullptr;   // pinned
+  float* res_host = nullptr;          // pinned
+
+  // host-frame staging (per slot)
+  std::vector<uint8_t*> frame_dev;
+  std::vector<size_t> frame_cap;
+
+  // tracker state (vipt.py:57, 88) in doubles
+  std::vector<std::array<double, 4>> state;
+  std::vector<char> active;
+  std::vector<double> last_rf;
+  int last_batch = 0;
+
+  std::map<std::pair<int, int>, hipGraphExec_t> graphs;
+  std::unique_ptr<TimingProbe> probe;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+};
+
+namespace {
+
+#define HIPCHECK(e, expr)                                                              \
+  do {                                                                                 \
+    hipError_t _st = (expr);                                                           \
+    if (_st != hipSuccess)                                                             \
+      return (e)->fail(MMT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_st)); \
+  } while (0)
+
+void add_expected(mmt_engine* e, const std::string& k, std::vector<int64_t> shape) {
+  e->expected[k] = std::move(shape);
+  e->expected_order.push_back(k);
+}
+
+// Reference state_dict layout (ostrack_prompt.py:94-145 / vit_ce_prompt.py:84-182 / ostrack.py:95-144).
+void build_expected(mmt_engine* e) {
+  const auto& c = e->cfg;
+  const bool vipt = c.model == MMT_MODEL_VIPT;
+  add_expected(e, "backbone.cls_token", {1, 1, C});
+  add_expected(e, "backbone.pos_embed", {1, 197, C});
+  add_expected(e, "backbone.pos_embed_z", {1, e->Lz, C});
+  add_expected(e, "backbone.pos_embed_x", {1, e->Lx, C});
+  add_expected(e, "backbone.patch_embed.proj.weight", {C, 3, 16, 16});
+  add_expected(e, "backbone.patch_embed.proj.bias", {C});
+  if (vipt) {
+    add_expected(e, "backbone.patch_embed_prompt.proj.weight", {C, 3, 16, 16});
+    add_expected(e, "backbone.patch_embed_prompt.proj.bias", {C});
+    for (int i = 0; i < e->nprompt; ++i) {
+      const std::string p = "backbone.prompt_blocks." + std::to_string(i) + ".";
+      add_expected(e, p + "conv0_0.weight", {8, C, 1, 1});
+      add_expected(e, p + "conv0_0.bias", {8});
+      add_expected(e, p + "conv0_1.weight", {8, C, 1, 1});
+      add_expected(e, p + "conv0_1.bias", {8});
+      add_expected(e, p + "conv1x1.weight", {C, 8, 1, 1});
+      add_expected(e, p + "conv1x1.bias", {C});
+      add_expected(e, p + "fovea.smooth", {1});
+      add_expected(e, "backbone.prompt_norms." + std::to_string(i) + ".weight", {C});
+      add_expected(e, "backbone.prompt_norms." + std::to_string(i) + ".bias", {C});
+    }
+  }
+  for (int i = 0; i < DEPTH; ++i) {
+    const std::string p = "backbone.blocks." + std::to_string(i) + ".";
+    add_expected(e, p + "norm1.weight", {C});
+    add_expected(e, p + "norm1.bias", {C});
+    add_expected(e, p + "attn.qkv.weight", {3 * C, C});
+    add_expected(e, p + "attn.qkv.bias", {3 * C});
+    add_expected(e, p + "attn.proj.weight", {C, C});
+    add_expected(e, p + "attn.proj.bias", {C});
+    add_expected(e, p + "norm2.weight", {C});
+    add_expected(e, p + "norm2.bias", {C});
+    add_expected(e, p + "mlp.fc1.weight", {MLPD, C});
+    add_expected(e, p + "mlp.fc1.bias", {MLPD});
+    add_expected(e, p + "mlp.fc2.weight", {C, MLPD});
+    add_expected(e, p + "mlp.fc2.bias", {C});
+  }
+  add_expected(e, "backbone.norm.weight", {C});
+  add_expected(e, "backbone.norm.bias", {C});
+  const int hc = c.head_channels;
+  const int ch[5] = {C, hc, hc / 2, hc / 4, hc / 8};
+  const char* br[3] = {"ctr", "offset", "size"};
+  const int n5[3] = {1, 2, 2};
+  for (int b = 0; b < 3; ++b) {
+    for (int j = 1; j <= 4; ++j) {
+      const std::string p = std::string("box_head.conv") + std::to_string(j) + "_" + br[b] + ".";
+      add_expected(e, p + "0.weight", {ch[j], ch[j - 1], 3, 3});
+      add_expected(e, p + "0.bias", {ch[j]});
+      add_expected(e, p + "1.weight", {ch[j]});
+      add_expected(e, p + "1.bias", {ch[j]});
+      add_expected(e, p + "1.running_mean", {ch[j]});
+      add_expected(e, p + "1.running_var", {ch[j]});
+      add_expected(e, p + "1.num_batches_tracked", {});
+    }
+    add_expected(e, std::string("box_head.conv5_") + br[b] + ".weight", {n5[b], ch[4], 1, 1});
+    add_expected(e, std::string("box_head.conv5_") + br[b] + ".bias", {n5[b]});
+  }
+  add_expected(e, "output_window", {1, 1, e->fs, e->fs});  // hann2d (vipt.py:30), computed by the caller
+}
+
+template <class T>
+T* walloc(mmt_engine* e, size_t n) {
+  size_t bytes = (n * sizeof(T) + 255) & ~size_t(255);
+  if (e->wused + bytes > e->wcap) return nullptr;
+  T* p = reinterpret_cast<T*>(static_cast<char*>(e->warena) + e->wused);
+  e->wused += bytes;
+  return p;
+}
+
+const std::vector<float>& H(mmt_engine* e, const std::string& k) { return e->host.at(k).data; }
+
+int upload_f32(mmt_engine* e, float** dst, const std::vector<float>& v) {
+  *dst = walloc<float>(e, v.size());
+  if (!*dst) return e->fail(MMT_E_HIP, "weight arena overflow");
+  HIPCHECK(e, hipMemcpy(*dst, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+  return MMT_OK;
+}
+int upload_bf16(mmt_engine* e, bf16_t** dst, const std::vector<float>& v) {
+  std::vector<uint16_t> t(v.size());
+  for (size_t i = 0; i < v.size(); ++i) t[i] = host_bf16(v[i]);
+  *dst = walloc<bf16_t>(e, v.size());
+  if (!*dst) return e->fail(MMT_E_HIP, "weight arena overflow");
+  HIPCHECK(e, hipMemcpy(*dst, t.data(), t.size() * 2, hipMemcpyHostToDevice));
+  return MMT_OK;
+}
+
+#define TRY(x)                  \
+  do {                          \
+    int _r = (x);               \
+    if (_r != MMT_OK) return _r; \
+  } while (0)
+
+// BN(eval) folded into the preceding conv, weights reordered [out][ky][kx][in] (implicit-GEMM K order).
+void fold_conv(mmt_engine* e, const std::string& p, int cout, int cin, std::vector<float>& w_out,
+               std::vector<float>& b_out, size_t w_off, size_t b_off) {
+  const auto& w = H(e, p + ".0.weight");
+  const auto& b = H(e, p + ".0.bias");
+  const auto& g = H(e, p + ".1.weight");
+  const auto& be = H(e, p + ".1.bias");
+  const auto& rm = H(e, p + ".1.running_mean");
+  const auto& rv = H(e, p + ".1.running_var");
+  for (int o = 0; o < cout; ++o) {
+    const double s = (double)g[o] / std::sqrt((double)rv[o] + 1e-5);  // head.py:20 BatchNorm2d eps
+    b_out[b_off + o] = (float)(((double)b[o] - (double)rm[o]) * s + (double)be[o]);
+    for (int ci = 0; ci < cin; ++ci)
+      for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx)
+          w_out[w_off + (size_t)o * 9 * cin + (size_t)(ky * 3 + kx) * cin + ci] =
+              (float)((double)w[(((size_t)o * cin + ci) * 3 + ky) * 3 + kx] * s);
+  }
+}
+
+int pack_weights(mmt_engine* e) {
+  const auto& c = e->cfg;
+  const bool vipt = c.model == MMT_MODEL_VIPT;
+  e->wcap = 200ull << 20;
+  HIPCHECK(e, hipMalloc(&e->warena, e->wcap));
+  TRY(upload_bf16(e, &e->pe_w, H(e, "backbone.patch_embed.proj.weight")));
+  TRY(upload_f32(e, &e->pe_b, H(e, "backbone.patch_embed.proj.bias")));
+  if (vipt) {
+    TRY(upload_bf16(e, &e->pep_w, H(e, "backbone.patch_embed_prompt.proj.weight")));
+    TRY(upload_f32(e, &e->pep_b, H(e, "backbone.patch_embed_prompt.proj.bias")));
+  }
+  std::vector<float> pos(H(e, "backbone.pos_embed_z"));
+  const auto& px = H(e, "backbone.pos_embed_x");
+  pos.insert(pos.end(), px.begin(), px.end());
+  TRY(upload_f32(e, &e->pos, pos));
+  for (int i = 0; i < e->nprompt; ++i) {
+    const std::string p = "backbone.prompt_blocks." + std::to_string(i) + ".";
+    PromptW& w = e->pw[i];
+    TRY(upload_f32(e, &w.w00, H(e, p + "conv0_0.weight")));
+    TRY(upload_f32(e, &w.b00, H(e, p + "conv0_0.bias")));
+    TRY(upload_f32(e, &w.w01, H(e, p + "conv0_1.weight")));
+    TRY(upload_f32(e, &w.b01, H(e, p + "conv0_1.bias")));
+    TRY(upload_f32(e, &w.w1, H(e, p + "conv1x1.weight")));
+    TRY(upload_f32(e, &w.b1, H(e, p + "conv1x1.bias")));
+    w.smooth = H(e, p + "fovea.smooth")[0];
+    TRY(upload_f32(e, &w.nw, H(e, "backbone.prompt_norms." + std::to_string(i) + ".weight")));
+    TRY(upload_f32(e, &w.nb, H(e, "backbone.prompt_norms." + std::to_string(i) + ".bias")));
+  }
+  for (int i = 0; i < DEPTH; ++i) {
+    const std::string p = "backbone.blocks." + std::to_string(i) + ".";
+    LayerW& w = e->lw[i];
+    TRY(upload_bf16(e, &w.qkv_w, H(e, p + "attn.qkv.weight")));
+    TRY(upload_f32(e, &w.qkv_b, H(e, p + "attn.qkv.bias")));
+    TRY(upload_bf16(e, &w.proj_w, H(e, p + "attn.proj.weight")));
+    TRY(upload_f32(e, &w.proj_b, H(e, p + "attn.proj.bias")));
+    TRY(upload_bf16(e, &w.fc1_w, H(e, p + "mlp.fc1.weight")));
+    TRY(upload_f32(e, &w.fc1_b, H(e, p + "mlp.fc1.bias")));
+    TRY(upload_bf16(e, &w.fc2_w, H(e, p + "mlp.fc2.weight")));
+    TRY(upload_f32(e, &w.fc2_b, H(e, p + "mlp.fc2.bias")));
+    TRY(upload_f32(e, &w.n1w, H(e, p + "norm1.weight")));
+    TRY(upload_f32(e, &w.n1b, H(e, p + "norm1.bias")));
+    TRY(upload_f32(e, &w.n2w, H(e, p + "norm2.weight")));
+    TRY(upload_f32(e, &w.n2b, H(e, p + "norm2.bias")));
+  }
+  TRY(upload_f32(e, &e->norm_w, H(e, "backbone.norm.weight")));
+  TRY(upload_f32(e, &e->norm_b, H(e, "backbone.norm.bias")));
+  // head
+  const int hc = c.head_channels;
+  const int ch[5] = {C, hc, hc / 2, hc / 4, hc / 8};
+  const char* br[3] = {"ctr", "offset", "size"};
+  {
+    std::vector<float> w((size_t)3 * hc * 9 * C), b((size_t)3 * hc);
+    for (int k = 0; k < 3; ++k)
+      fold_conv(e, std::string("box_head.conv1_") + br[k], hc, C, w, b, (size_t)k * hc * 9 * C, (size_t)k * hc);
+    TRY(upload_bf16(e, &e->hw1, w));
+    TRY(upload_f32(e, &e->hb1, b));
+  }
+  for (int j = 2; j <= 4; ++j) {
+    const int co = ch[j], ci = ch[j - 1];
+    std::vector<float> w((size_t)3 * co * 9 * ci), b((size_t)3 * co);
+    for (int k = 0; k < 3; ++k)
+      fold_conv(e, std::string("box_head.conv") + std::to_string(j) + "_" + br[k], co, ci, w, b,
+                (size_t)k * co * 9 * ci, (size_t)k * co);
+    TRY(upload_bf16(e, &e->hw[j - 2], w));
+    TRY(upload_f32(e, &e->hb[j - 2], b));
+  }
+  {
+    std::vector<float> w5, b5;
+    for (int k = 0; k < 3; ++k) {
+      const auto& w = H(e, std::string("box_head.conv5_") + br[k] + ".weight");
+      const auto& b = H(e, std::string("box_head.conv5_") + br[k] + ".bias");
+      w5.insert(w5.end(), w.begin(), w.end());
+      b5.insert(b5.end(), b.begin(), b.end());
+    }
+    TRY(upload_f32(e, &e->w5, w5));
+    TRY(upload_f32(e, &e->b5, b5));
+  }
+  TRY(upload_f32(e, &e->hann, H(e, "output_window")));
+  return MMT_OK;
+}
+
+int alloc_acts(mmt_engine* e) {
+  const int B = e->cfg.max_batch, L = e->L, Lx = e->Lx;
+  const int S = e->cfg.search_size, Cin = e->cfg.in_chans;
+  const int hc = e->cfg.head_channels;
+  struct Req { void** p; size_t bytes; };
+  std::vector<Req> reqs = {
+      {(void**)&e->A_rgb, (size_t)B * L * C * 2},      {(void**)&e->A_aux, (size_t)B * L * C * 2},
+      {(void**)&e->tok_rgb, (size_t)B * L * C * 4},    {(void**)&e->tok_aux, (size_t)B * L * C * 4},
+      {(void**)&e->X, (size_t)B * L * C * 4},          {(void**)&e->X2, (size_t)B * L * C * 4},
+      {(void**)&e->P, (size_t)B * L * C * 4},          {(void**)&e->a8, (size_t)B * L * 8 * 4},
+      {(void**)&e->c8, (size_t)B * L * 8 * 4},         {(void**)&e->Hn, (size_t)B * L * C * 2},
+      {(void**)&e->QKV, (size_t)B * L * 3 * C * 2},    {(void**)&e->O, (size_t)B * L * C * 2},
+      {(void**)&e->Hm, (size_t)B * L * MLPD * 2},      {(void**)&e->feat, (size_t)B * Lx * C * 2},
+      {(void**)&e->h1, (size_t)B * Lx * 3 * hc * 2},   {(void**)&e->h2, (size_t)B * Lx * 3 * (hc / 2) * 2},
+      {(void**)&e->h3, (size_t)B * Lx * 3 * (hc / 4) * 2}, {(void**)&e->h4, (size_t)B * Lx * 3 * 32 * 4},
+      {(void**)&e->ce_prob, (size_t)B * HEADS * Lx * 4}, {(void**)&e->res, (size_t)B * 8 * 4},
+      {(void**)&e->gidx0, (size_t)B * Lx * 4},         {(void**)&e->gidx1, (size_t)B * Lx * 4},
+      {(void**)&e->slot2pos, (size_t)B * Lx * 4},      {(void**)&e->gather, (size_t)B * L * 4},
+      {(void**)&e->removed, (size_t)B * Lx * 4},       {(void**)&e->params_dev, (size_t)B * sizeof(CropParam)},
+  };
+  if (e->cfg.debug_outputs) {
+    reqs.push_back({(void**)&e->dbg_patch, (size_t)B * S * S * Cin});
+    reqs.push_back({(void**)&e->dbg_maps, (size_t)B * 5 * Lx * 4});
+    reqs.push_back({(void**)&e->dbg_feat, (size_t)B * L * C * 4});
+  }
+  size_t total = 0;
+  for (auto& r : reqs) total += (r.bytes + 255) & ~size_t(255);
+  HIPCHECK(e, hipMalloc(&e->aarena, total));
+  HIPCHECK(e, hipMemset(e->aarena, 0, total));
+  size_t off = 0;
+  for (auto& r : reqs) {
+    *r.p = static_cast<char*>(e->aarena) + off;
+    off += (r.bytes + 255) & ~size_t(255);
+  }
+  HIPCHECK(e, hipHostMalloc((void**)&e->params_host, (size_t)B * sizeof(CropParam), hipHostMallocDefault));
+  HIPCHECK(e, hipHostMalloc((void**)&e->res_host, (size_t)B * 8 * 4, hipHostMallocDefault));
+  return MMT_OK;
+}
+
+// ---------------------------------------------------------------- timing probe
+void probe_begin(mmt_engine* e, const char* cls, double flops, double bytes) {
+  TimingProbe* p = e->probe.get();
+  if (!p || p->cls != cls) return;
+  if (p->used == p->ev.size()) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    p->ev.push_back({a, b});
+  }
+  hipEventRecord(p->ev[p->used].first, e->stream);
+  p->pending_work.push_back({flops, bytes});
+}
+void probe_end(mmt_engine* e, const char* cls) {
+  TimingProbe* p = e->probe.get();
+  if (!p || p->cls != cls) return;
+  hipEventRecord(p->ev[p->used].second, e->stream);
+  p->used++;
+}
+void probe_collect(mmt_engine* e) {
+  TimingProbe* p = e->probe.get();
+  if (!p) return;
+  for (size_t i = 0; i < p->used; ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p->ev[i].first, p->ev[i].second) == hipSuccess) {
+      p->total_ms += ms;
+      p->launches++;
+      p->flops += p->pending_work[i].first;
+      p->bytes += p->pending_work[i].second;
+    }
+  }
+  p->used = 0;
+  p->pending_work.clear();
+}
+
+// ---------------------------------------------------------------- the per-frame launch sequence
+GemmArgs dense(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, const float* bias, void* Cp, int64_t ldc,
+               const float* R, int64_t ldr, int M, int N, int K) {
+  GemmArgs a{};
+  a.g[0] = GemmGroup{A, lda, W, ldw, bias, Cp, ldc, R, ldr};
+  a.groups = 1;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.amode = A_DENSE;
+  return a;
+}
+
+void run_gemm(mmt_engine* e, const char* cls, const GemmArgs& a, int epi) {
+  const double flops = 2.0 * a.M * a.N * (double)a.K * a.groups;
+  const double bytes = ((double)a.M * a.K + (double)a.N * a.K) * 2.0 * a.groups;
+  probe_begin(e, cls, flops, bytes);
+  gemm(a, epi, e->stream);
+  probe_end(e, cls);
+}
+
+void enqueue_forward(mmt_engine* e, int b0, int n) {
+  const auto& c = e->cfg;
+  hipStream_t s = e->stream;
+  const int Lz = e->Lz, Lx = e->Lx, L = e->L;
+  const bool vipt = c.model == MMT_MODEL_VIPT;
+  const bool prompted = vipt && c.prompt_type != MMT_PROMPT_NONE;
+  const bool deep = vipt && c.prompt_type == MMT_PROMPT_DEEP;
+  bf16_t* A_rgb = e->A_rgb + (size_t)b0 * L * C;
+  bf16_t* A_aux = e->A_aux + (size_t)b0 * L * C;
+
+  // 1. crop + normalise + patchify the search region of every sequence
+  CropArgs ca{};
+  ca.params = e->params_dev;
+  ca.B = n;
+  ca.out_sz = c.search_size;
+  ca.C = c.in_chans;
+  ca.A_rgb = A_rgb;
+  ca.A_aux = A_aux;
+  ca.rows_per_seq = L;
+  ca.row0 = Lz;
+  ca.dbg_patch = e->dbg_patch;
+  crop_patchify(ca, s);
+
+  // 2. patch embedding (template rows were written at initialize)
+  float* X = e->X;
+  float* X2 = e->X2;
+  if (vipt) {
+    GemmArgs g = dense(A_rgb, C, e->pe_w, C, e->pe_b, e->tok_rgb, C, nullptr, 0, n * L, C, C);
+    g.g[1] = GemmGroup{A_aux, C, e->pep_w, C, e->pep_b, e->tok_aux, C, nullptr, 0};
+    g.groups = 2;
+    run_gemm(e, "patch", g, EPI_F32);
+  } else {
+    GemmArgs g = dense(A_rgb, C, e->pe_w, C, e->pe_b, X, C, e->pos, C, n * L, C, C);
+    g.pos_rows = L;
+    run_gemm(e, "patch", g, EPI_POS_F32);
+  }
+  init_indices(e->gidx0, e->slot2pos, n, Lz, Lx, s);
+
+  PromptArgs pa{};
+  pa.B = n;
+  pa.Lz = Lz;
+  pa.Lx = Lx;
+  pa.a8 = e->a8;
+  pa.c8 = e->c8;
+  pa.P = e->P;
+  if (prompted) {  // layer-0 prompt: vit_ce_prompt.py:205-219
+    pa.layer = 0;
+    pa.srcA = e->tok_rgb;
+    pa.srcA_rows = L;
+    pa.srcB = e->tok_aux;
+    pa.slot2pos = nullptr;
+    pa.lnA_w = e->pw[0].nw;
+    pa.lnA_b = e->pw[0].nb;
+    pa.lnB_w = e->pw[0].nw;
+    pa.lnB_b = e->pw[0].nb;
+    pa.w00 = e->pw[0].w00;
+    pa.b00 = e->pw[0].b00;
+    pa.w01 = e->pw[0].w01;
+    pa.b01 = e->pw[0].b01;
+    pa.w1 = e->pw[0].w1;
+    pa.b1 = e->pw[0].b1;
+    pa.smooth = e->pw[0].smooth;
+    pa.X = X;
+    pa.X_rows = L;
+    pa.tok_rgb = e->tok_rgb;
+    pa.pos = e->pos;
+    prompt_reduce(pa, s);
+    prompt_expand(pa, s);
+  }
+
+  int* gin = e->gidx0;
+  int* gout = e->gidx1;
+  int removed_off = 0;
+  int Ls = Lx;
+  for (int i = 0; i < DEPTH; ++i) {
+    const LayerW& w = e->lw[i];
+    const int Na = Lz + Ls;
+    if (deep && i >= 1) {  // vit_ce_prompt.py:268-310
+      pa.layer = i;
+      pa.srcA = X;
+      pa.srcA_rows = Na;
+      pa.srcB = e->P;
+      pa.slot2pos = e->slot2pos;
+      pa.lnA_w = e->pw[i - 1].nw;
+      pa.lnA_b = e->pw[i - 1].nb;
+      pa.lnB_w = e->pw[i].nw;
+      pa.lnB_b = e->pw[i].nb;
+      pa.w00 = e->pw[i].w00;
+      pa.b00 = e->pw[i].b00;
+      pa.w01 = e->pw[i].w01;
+      pa.b01 = e->pw[i].b01;
+      pa.w1 = e->pw[i].w1;
+      pa.b1 = e->pw[i].b1;
+      pa.smooth = e->pw[i].smooth;
+      pa.X = X;
+      pa.X_rows = Na;
+      prompt_reduce(pa, s);
+      prompt_expand(pa, s);
+    }
+    layernorm(X, w.n1w, w.n1b, e->Hn, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+    run_gemm(e, "qkv", dense(e->Hn, C, w.qkv_w, C, w.qkv_b, e->QKV, 3 * C, nullptr, 0, n * Na, 3 * C, C), EPI_BF16);
+    const bool ce = e->keep_at[i] != e->ls_before[i];
+    AttnArgs aa{};
+    aa.qkv = e->QKV;
+    aa.out = e->O;
+    aa.B = n;
+    aa.N = Na;
+    aa.heads = HEADS;
+    aa.ce_query = ce ? c.ce_template_index : -1;
+    aa.ce_lens_t = Lz;
+    aa.ce_prob = e->ce_prob;
+    probe_begin(e, "attn", 4.0 * n * HEADS * (double)Na * Na * 64, (double)n * Na * 4 * C * 2);
+    attention(aa, s);
+    probe_end(e, "attn");
+    run_gemm(e, "proj", dense(e->O, C, w.proj_w, C, w.proj_b, X, C, X, C, n * Na, C, C), EPI_RESID_F32);
+    if (ce) {  // attn_blocks.py:99-101
+      const int keep = e->keep_at[i];
+      CEArgs ce_a{};
+      ce_a.B = n;
+      ce_a.Lz = Lz;
+      ce_a.Ls = Ls;
+      ce_a.keep = keep;
+      ce_a.heads = HEADS;
+      ce_a.Lx = Lx;
+      ce_a.prob = e->ce_prob;
+      ce_a.gidx_in = gin;
+      ce_a.gidx_out = gout;
+      ce_a.gather = e->gather;
+      ce_a.slot2pos = e->slot2pos;
+      ce_a.removed = e->removed;
+      ce_a.removed_off = removed_off;
+      ce_select(ce_a, s);
+      removed_off += Ls - keep;
+      std::swap(gin, gout);
+      Ls = keep;
+      layernorm(X, w.n2w, w.n2b, e->Hn, nullptr, n * (Lz + Ls), Lz + Ls, e->gather, Na, X2, s);
+      std::swap(X, X2);
+    } else {
+      layernorm(X, w.n2w, w.n2b, e->Hn, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+    }
+    const int Nm = Lz + Ls;
+    run_gemm(e, "fc1", dense(e->Hn, C, w.fc1_w, C, w.fc1_b, e->Hm, MLPD, nullptr, 0, n * Nm, MLPD, C),
+             EPI_GELU_BF16);
+    run_gemm(e, "fc2", dense(e->Hm, MLPD, w.fc2_w, MLPD, w.fc2_b, X, C, X, C, n * Nm, C, MLPD), EPI_RESID_F32);
+  }
+  final_norm_recover(X, Lz + Ls, e->slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, e->feat, e->dbg_feat, s);
+
+  // CENTER head: conv1 of the three branches fused (N = 3*hc), then per-branch grouped convs
+  const int hc = c.head_channels, fs = e->fs, M = n * Lx;
+  {
+    GemmArgs g{};
+    g.g[0] = GemmGroup{e->feat, C, e->hw1, 9 * C, e->hb1, e->h1, 3 * hc, nullptr, 0};
+    g.groups = 1;
+    g.M = M;
+    g.N = 3 * hc;
+    g.K = 9 * C;
+    g.amode = A_CONV3;
+    g.conv_hw = fs;
+    g.conv_cin = C;
+    run_gemm(e, "conv1", g, EPI_RELU_BF16);
+  }
+  const int ch[4] = {hc, hc / 2, hc / 4, hc / 8};
+  for (int j = 0; j < 3; ++j) {   // conv2, conv3, conv4
+    const int ci = ch[j], co = ch[j + 1];
+    GemmArgs g{};
+    for (int k = 0; k < 3; ++k) {
+      const bf16_t* A;
+      int64_t lda;
+      if (j == 0) {
+        A = e->h1 + k * hc;
+        lda = 3 * hc;
+      } else {
+        A = (j == 1 ? e->h2 : e->h3) + (size_t)k * M * ci;
+        lda = ci;
+      }
+      void* Cout = j == 0 ? (void*)(e->h2 + (size_t)k * M * co)
+                          : (j == 1 ? (void*)(e->h3 + (size_t)k * M * co) : (void*)(e->h4 + (size_t)k * M * co));
+      g.g[k] = GemmGroup{A, lda, e->hw[j] + (size_t)k * co * 9 * ci, 9 * ci, e->hb[j] + k * co, Cout, co, nullptr, 0};
+    }
+    g.groups = 3;
+    g.M = M;
+    g.N = co;
+    g.K = 9 * ci;
+    g.amode = A_CONV3;
+    g.conv_hw = fs;
+    g.conv_cin = ci;
+    run_gemm(e, j == 0 ? "conv2" : (j == 1 ? "conv3" : "conv4"), g, j == 2 ? EPI_RELU_F32 : EPI_RELU_BF16);
+  }
+  DecodeArgs da{};
+  da.B = n;
+  da.fs = fs;
+  da.h4 = e->h4;
+  da.w5 = e->w5;
+  da.b5 = e->b5;
+  da.hann = e->hann;
+  da.res = e->res;
+  da.maps = e->dbg_maps;
+  decode(da, s);
+}
+
+// crop geometry of processing_utils.py:32-41 in doubles with Python rounding (round half to even)
+int geometry(mmt_engine* e, const double box[4], double factor, int out_sz, int* x1, int* y1, int* crop_sz,
+             double* rf) {
+  const double x = box[0], y = box[1], w = box[2], h = box[3];
+  const double cs = std::ceil(std::sqrt(w * h) * factor);
+  if (!(cs >= 1.0)) return e->fail(MMT_E_BOX, "Too small bounding box.");
+  if (cs > 1e6) return e->fail(MMT_E_ARG, "crop size out of range");
+  *crop_sz = (int)cs;
+  *x1 = (int)std::nearbyint(x + 0.5 * w - cs * 0.5);
+  *y1 = (int)std::nearbyint(y + 0.5 * h - cs * 0.5);
+  *rf = (double)out_sz / cs;
+  return MMT_OK;
+}
+
+int stage_frame(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww, int Cc, int64_t stride,
+                int is_device, const uint8_t** dev) {
+  if (!frame || Hh < 2 || Ww < 2 || Cc != e->cfg.in_chans || stride < (int64_t)Ww * Cc)
+    return e->fail(MMT_E_ARG, "bad frame (expect H x W x in_chans uint8, H,W >= 2)");
+  if (is_device) {
+    *dev = frame;
+    return MMT_OK;
+  }
+  const size_t bytes = (size_t)stride * Hh;
+  if (e->frame_cap[slot] < bytes) {
+    if (e->frame_dev[slot]) hipFree(e->frame_dev[slot]);
+    e->frame_dev[slot] = nullptr;
+    HIPCHECK(e, hipMalloc(&e->frame_dev[slot], bytes));
+    e->frame_cap[slot] = bytes;
+  }
+  HIPCHECK(e, hipMemcpyAsync(e->frame_dev[slot], frame, bytes, hipMemcpyHostToDevice, e->stream));
+  *dev = e->frame_dev[slot];
+  return MMT_OK;
+}
+
+// vipt.py:84-88 + box_ops.py:97-106, float/double exactly as the reference's tensor/python mix
+void update_state(mmt_engine* e, int slot, const float* r, int Hh, int Ww, double rf) {
+  const float S = (float)e->cfg.search_size;
+  const float frf = (float)rf;
+  const double cx = (double)((r[0] * S) / frf), cy = (double)((r[1] * S) / frf);
+  const double w = (double)((r[2] * S) / frf), h = (double)((r[3] * S) / frf);
+  auto& st = e->state[slot];
+  const double cx_prev = st[0] + 0.5 * st[2], cy_prev = st[1] + 0.5 * st[3];
+  const double half = 0.5 * e->cfg.search_size / rf;
+  const double cxr = cx + (cx_prev - half), cyr = cy + (cy_prev - half);
+  double x1 = cxr - 0.5 * w, y1 = cyr - 0.5 * h, bw = w, bh = h;
+  const double margin = 10;
+  double x2 = x1 + bw, y2 = y1 + bh;
+  x1 = std::min(std::max(0.0, x1), Ww - margin);
+  x2 = std::min(std::max(margin, x2), (double)Ww);
+  y1 = std::min(std::max(0.0, y1), Hh - margin);
+  y2 = std::min(std::max(margin, y2), (double)Hh);
+  bw = std::max(margin, x2 - x1);
+  bh = std::max(margin, y2 - y1);
+  st = {x1, y1, bw, bh};
+}
+
+int launch(mmt_engine* e, int b0, int n) {
+  if (!e->cfg.use_graphs || e->probe) {
+    enqueue_forward(e, b0, n);
+    HIPCHECK(e, hipGetLastError());
+    return MMT_OK;
+  }
+  auto key = std::make_pair(b0, n);
+  auto it = e->graphs.find(key);
+  if (it == e->graphs.end()) {
+    enqueue_forward(e, b0, n);  // warm / validate eagerly once
+    HIPCHECK(e, hipGetLastError());
+    hipGraph_t g;
+    HIPCHECK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    enqueue_forward(e, b0, n);
+    HIPCHECK(e, hipStreamEndCapture(e->stream, &g));
+    hipGraphExec_t ge;
+    HIPCHECK(e, hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    it = e->graphs.emplace(key, ge).first;
+    return MMT_OK;  // the eager run above already produced this frame's result
+  }
+  HIPCHECK(e, hipGraphLaunch(it->second, e->stream));
+  return MMT_OK;
+}
+
+int check_engine(mmt_engine* e) {
+  if (!e) return MMT_E_ARG;
+  if (!e->finalized) return e->fail(MMT_E_STATE, "engine not finalized (load every state_dict key first)");
+  HIPCHECK(e, hipSetDevice(e->device));
+  return MMT_OK;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+const char* mmt_version(void) { return "mmtrack-mi355x 0.1 (gfx950)"; }
+
+int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
+  if (!cfg || !out) return MMT_E_ARG;
+  *out = nullptr;
+  auto e = std::make_unique<mmt_engine>();
+  e->cfg = *cfg;
+  e->device = device;
+  const auto& c = e->cfg;
+  if (c.template_size % 16 || c.search_size % 16 || c.template_size <= 0 || c.search_size <= 0 ||
+      c.max_batch <= 0 || c.n_ce < 0 || c.n_ce > 12 || c.head_channels != 256 ||
+      (c.model == MMT_MODEL_VIPT && (c.in_chans != 6 || c.prompt_type == MMT_PROMPT_NONE)) ||
+      (c.model == MMT_MODEL_OSTRACK && c.in_chans != 3)) {
+    *out = nullptr;
+    return MMT_E_ARG;
+  }
+  e->Lz = (c.template_size / 16) * (c.template_size / 16);
+  e->Lx = (c.search_size / 16) * (c.search_size / 16);
+  e->L = e->Lz + e->Lx;
+  e->fs = c.search_size / 16;
+  e->tfs = c.template_size / 16;
+  if (e->L > 1024 || (c.n_ce > 0 && (c.ce_template_index < 0 || c.ce_template_index >= e->Lz))) return MMT_E_ARG;
+  e->nprompt = c.model == MMT_MODEL_VIPT ? (c.prompt_type == MMT_PROMPT_DEEP ? DEPTH : (c.prompt_type ? 1 : 0)) : 0;
+  int Ls = e->Lx;
+  for (int i = 0; i < DEPTH; ++i) {
+    e->ls_before.push_back(Ls);
+    for (int k = 0; k < c.n_ce; ++k)
+      if (c.ce_loc[k] == i) {
+        const int keep = (int)std::ceil(c.ce_keep_ratio[k] * Ls);  // attn_blocks.py:40
+        if (keep < Ls && keep > 0) Ls = keep;
+      }
+    e->keep_at.push_back(Ls);
+  }
+  if (hipSetDevice(device) != hipSuccess) return MMT_E_HIP;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
+  build_expected(e.get());
+  e->frame_dev.assign(c.max_batch, nullptr);
+  e->frame_cap.assign(c.max_batch, 0);
+  e->state.assign(c.max_batch, {0, 0, 0, 0});
+  e->active.assign(c.max_batch, 0);
+  e->last_rf.assign(c.max_batch, 1.0);
+  if (alloc_acts(e.get()) != MMT_OK) return MMT_E_HIP;
+  *out = e.release();
+  return MMT_OK;
+}
+
+void mmt_destroy(mmt_engine* e) {
+  if (!e) return;
+  hipSetDevice(e->device);
+  hipStreamSynchronize(e->stream);
+  for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second);
+  if (e->probe)
+    for (auto& p : e->probe->ev) {
+      hipEventDestroy(p.first);
+      hipEventDestroy(p.second);
+    }
+  for (auto* p : e->frame_dev)
+    if (p) hipFree(p);
+  if (e->warena) hipFree(e->warena);
+  if (e->aarena) hipFree(e->aarena);
+  if (e->params_host) hipHostFree(e->params_host);
+  if (e->res_host) hipHostFree(e->res_host);
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+}
+
+const char* mmt_last_error(const mmt_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int mmt_num_expected_keys(const mmt_engine* e) { return e ? (int)e->expected_order.size() : 0; }
+const char* mmt_expected_key(const mmt_engine* e, int i) {
+  return (e && i >= 0 && i < (int)e->expected_order.size()) ? e->expected_order[i].c_str() : nullptr;
+}
+
+int mmt_set_tensor(mmt_engine* e, const char* key, const float* data, const int64_t* shape, int ndim) {
+  if (!e || !key || (!data && ndim > 0)) return MMT_E_ARG;
+  auto it = e->expected.find(key);
+  if (it == e->expected.end()) return e->fail(MMT_E_WEIGHTS, std::string("Unexpected key(s) in state_dict: ") + key);
+  std::vector<int64_t> shp(shape, shape + ndim);
+  if (shp != it->second) return e->fail(MMT_E_WEIGHTS, std::string("size mismatch for ") + key);
+  int64_t n = 1;
+  for (auto d : shp) n *= d;
+  HostTensor t;
+  t.shape = shp;
+  t.data.assign(data, data + (ndim ? n : 1));
+  e->host[key] = std::move(t);
+  e->finalized = false;
+  return MMT_OK;
+}
+
+int mmt_finalize(mmt_engine* e) {
+  if (!e) return MMT_E_ARG;
+  std::string missing;
+  for (auto& k : e->expected_order)
+    if (!e->host.count(k)) missing += (missing.empty() ? "" : ", ") + k;
+  if (!missing.empty()) return e->fail(MMT_E_WEIGHTS, "Missing key(s) in state_dict: " + missing);
+  HIPCHECK(e, hipSetDevice(e->device));
+  if (e->warena) {
+    hipFree(e->warena);
+    e->warena = nullptr;
+    e->wused = 0;
+  }
+  for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second);
+  e->graphs.clear();
+  int r = pack_weights(e);
+  if (r != MMT_OK) return r;
+  e->host.clear();
+  e->finalized = true;
+  return MMT_OK;
+}
+
+int mmt_initialize(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride,
+                   int is_device, const double init_xywh[4]) {
+  int r = check_engine(e);
+  if (r) return r;
+  if (slot < 0 || slot >= e->cfg.max_batch || !init_xywh) return e->fail(MMT_E_ARG, "bad slot / box");
+  int x1, y1, cs;
+  double rf;
+  TRY(geometry(e, init_xywh, e->cfg.template_factor, e->cfg.template_size, &x1, &y1, &cs, &rf));
+  const uint8_t* dev;
+  TRY(stage_frame(e, slot, frame, Hh, Ww, Cc, row_stride, is_device, &dev));
+  CropParam p{dev, row_stride, Hh, Ww, Cc, x1, y1, cs, 0};
+  e->params_host[0] = p;
+  HIPCHECK(e, hipMemcpyAsync(e->params_dev, e->params_host, sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
+  CropArgs ca{};
+  ca.params = e->params_dev;
+  ca.B = 1;
+  ca.out_sz = e->cfg.template_size;
+  ca.C = e->cfg.in_chans;
+  ca.A_rgb = e->A_rgb + (size_t)slot * e->L * C;
+  ca.A_aux = e->A_aux + (size_t)slot * e->L * C;
+  ca.rows_per_seq = e->L;
+  ca.row0 = 0;
+  ca.dbg_patch = nullptr;
+  crop_patchify(ca, e->stream);
+  HIPCHECK(e, hipGetLastError());
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  e->state[slot] = {init_xywh[0], init_xywh[1], init_xywh[2], init_xywh[3]};
+  e->active[slot] = 1;
+  return MMT_OK;
+}
+
+int mmt_track_batch(mmt_engine* e, int first_slot, int n, const uint8_t* const* frames, const int* Hs,
+                    const int* Ws, int Cc, const int64_t* row_stride, int is_device, double* out_xywh,
+                    float* out_score) {
+  int r = check_engine(e);
+  if (r) return r;
+  if (n <= 0 || first_slot < 0 || first_slot + n > e->cfg.max_batch || !frames || !Hs || !Ws || !row_stride)
+    return e->fail(MMT_E_ARG, "bad batch");
+  for (int i = 0; i < n; ++i) {
+    const int slot = first_slot + i;
+    if (!e->active[slot]) return e->fail(MMT_E_STATE, "track() before initialize() on slot " + std::to_string(slot));
+    int x1, y1, cs;
+    double rf;
+    TRY(geometry(e, e->state[slot].data(), e->cfg.search_factor, e->cfg.search_size, &x1, &y1, &cs, &rf));
+    const uint8_t* dev;
+    TRY(stage_frame(e, slot, frames[i], Hs[i], Ws[i], Cc, row_stride[i], is_device, &dev));
+    e->params_host[i] = CropParam{dev, row_stride[i], Hs[i], Ws[i], Cc, x1, y1, cs, 0};
+    e->last_rf[slot] = rf;
+  }
+  HIPCHECK(e, hipMemcpyAsync(e->params_dev, e->params_host, n * sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
+  TRY(launch(e, first_slot, n));
+  HIPCHECK(e, hipMemcpyAsync(e->res_host, e->res, (size_t)n * 8 * 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  probe_collect(e);
+  for (int i = 0; i < n; ++i) {
+    const int slot = first_slot + i;
+    update_state(e, slot, e->res_host + 8 * i, Hs[i], Ws[i], e->last_rf[slot]);
+    if (out_xywh)
+      for (int k = 0; k < 4; ++k) out_xywh[4 * i + k] = e->state[slot][k];
+    if (out_score) out_score[i] = e->res_host[8 * i + 4];
+  }
+  e->last_batch = n;
+  return MMT_OK;
+}
+
+int mmt_track(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride,
+              int is_device, double out_xywh[4], float* out_score) {
+  return mmt_track_batch(e, slot, 1, &frame, &Hh, &Ww, Cc, &row_stride, is_device, out_xywh, out_score);
+}
+
+int mmt_get_state(const mmt_engine* e, int slot, double out_xywh[4]) {
+  if (!e || slot < 0 || slot >= e->cfg.max_batch || !out_xywh) return MMT_E_ARG;
+  for (int k = 0; k < 4; ++k) out_xywh[k] = e->state[slot][k];
+  return MMT_OK;
+}
+
+int mmt_set_state(mmt_engine* e, int slot, const double xywh[4]) {
+  if (!e || slot < 0 || slot >= e->cfg.max_batch || !xywh) return MMT_E_ARG;
+  e->state[slot] = {xywh[0], xywh[1], xywh[2], xywh[3]};
+  return MMT_OK;
+}
+
+int mmt_debug_fetch(mmt_engine* e, const char* what, int bi, void* dst, size_t nbytes) {
+  int r = check_engine(e);
+  if (r) return r;
+  if (!e->cfg.debug_outputs) return e->fail(MMT_E_STATE, "engine built without debug_outputs");
+  if (!what || !dst || bi < 0 || bi >= e->cfg.max_batch) return e->fail(MMT_E_ARG, "bad debug fetch");
+  const void* src = nullptr;
+  size_t sz = 0;
+  const std::string w(what);
+  const int S = e->cfg.search_size;
+  if (w == "crop") {
+    sz = (size_t)S * S * e->cfg.in_chans;
+    src = e->dbg_patch + bi * sz;
+  } else if (w == "maps") {
+    sz = (size_t)5 * e->Lx * 4;
+    src = reinterpret_cast<const char*>(e->dbg_maps) + bi * sz;
+  } else if (w == "feat") {
+    sz = (size_t)e->L * C * 4;
+    src = reinterpret_cast<const char*>(e->dbg_feat) + bi * sz;
+  } else if (w == "removed") {
+    sz = (size_t)e->Lx * 4;
+    src = reinterpret_cast<const char*>(e->removed) + bi * sz;
+  } else if (w == "result") {
+    sz = 8 * 4;
+    src = reinterpret_cast<const char*>(e->res) + bi * sz;
+  } else {
+    return e->fail(MMT_E_ARG, "unknown debug buffer " + w);
+  }
+  if (nbytes < sz) return e->fail(MMT_E_ARG, "debug buffer too small");
+  HIPCHECK(e, hipMemcpy(dst, src, sz, hipMemcpyDeviceToHost));
+  return MMT_OK;
+}
+
+int mmt_timing_enable(mmt_engine* e, const char* cls) {
+  if (!e) return MMT_E_ARG;
+  if (!cls || !*cls) {
+    if (e->probe)
+      for (auto& p : e->probe->ev) {
+        hipEventDestroy(p.first);
+        hipEventDestroy(p.second);
+      }
+    e->probe.reset();
+    return MMT_OK;
+  }
+  if (!e->probe) e->probe = std::make_unique<TimingProbe>();
+  e->probe->cls = cls;
+  e->probe->launches = 0;
+  e->probe->total_ms = e->probe->flops = e->probe->bytes = 0;
+  return MMT_OK;
+}
+
+int mmt_timing_read(mmt_engine* e, int* launches, double* total_ms, double* flops, double* bytes) {
+  if (!e || !e->probe) return MMT_E_STATE;
+  if (launches) *launches = (int)e->probe->launches;
+  if (total_ms) *total_ms = e->probe->total_ms;
+  if (flops) *flops = e->probe->flops;
+  if (bytes) *bytes = e->probe->bytes;
+  return MMT_OK;
+}
+
+int mmt_xcorr(const float* z, const float* x, float* out, int B, int Cc, int hz, int wz, int hx, int wx, float scale,
+              float bias, void* stream) {
+  if (!z || !x || !out || B <= 0 || Cc <= 0 || hz <= 0 || wz <= 0 || hx < hz || wx < wz || 16 * hz * wz > 16384)
+    return MMT_E_ARG;
+  xcorr(z, x, out, B, Cc, hz, wz, hx, wx, scale, bias, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, void* Cp, int64_t ldc,
+                const float* R, int64_t ldr, int M, int N, int K, int epi, int conv_hw, int conv_cin, int pos_rows,
+                void* stream) {
+  if (!A || !W || !Cp || M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 32 || epi < 0 || epi > 6) return MMT_E_ARG;
+  if ((epi == EPI_RESID_F32 || epi == EPI_POS_F32) && !R) return MMT_E_ARG;
+  if (conv_hw > 0 && (conv_cin % 64 || K != 9 * conv_cin || (epi != EPI_RELU_BF16 && epi != EPI_RELU_F32)))
+    return MMT_E_ARG;
+  GemmArgs a{};
+  a.g[0] = GemmGroup{(const bf16_t*)A, lda, (const bf16_t*)W, ldw, bias, Cp, ldc, R, ldr};
+  a.groups = 1;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.amode = conv_hw > 0 ? A_CONV3 : A_DENSE;
+  a.conv_hw = conv_hw;
+  a.conv_cin = conv_cin;
+  a.pos_rows = pos_rows > 0 ? pos_rows : 1;
+  gemm(a, epi, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_op_attention(const void* qkv, void* out, int B, int N, int heads, int ce_query, int ce_lens_t,
+                     float* ce_prob, void* stream) {
+  if (!qkv || !out || B <= 0 || N <= 0 || N > 1024 || heads <= 0) return MMT_E_ARG;
+  if (ce_query >= 0 && (!ce_prob || ce_lens_t < 0 || ce_lens_t >= N || ce_query >= N)) return MMT_E_ARG;
+  AttnArgs a{};
+  a.qkv = (const bf16_t*)qkv;
+  a.out = (bf16_t*)out;
+  a.B = B;
+  a.N = N;
+  a.heads = heads;
+  a.ce_query = ce_query;
+  a.ce_lens_t = ce_lens_t;
+  a.ce_prob = ce_prob;
+  attention(a, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_op_layernorm(const float* x, const float* w, const float* b, void* out_bf16, float* out_f32, int rows,
+                     void* stream) {
+  if (!x || !w || !b || rows <= 0 || (!out_bf16 && !out_f32)) return MMT_E_ARG;
+  layernorm(x, w, b, (bf16_t*)out_bf16, out_f32, rows, rows, nullptr, rows, nullptr, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+}  // extern "C"

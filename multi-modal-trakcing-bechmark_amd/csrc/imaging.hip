@@ -1,0 +1,192 @@
+// Frame-side kernels of the tracking path, gfx950:
+//  * crop_patchify: sample_target (processing_utils.py:14-81: square crop, zero pad, cv2 INTER_LINEAR
+//    resize) + PreprocessorMM normalisation (data_utils.py:20-24) + the k16s16 patch unfold that feeds
+//    the patch-embed GEMM, in one pass straight from the HBM-resident H x W x C uint8 frame (the padded
+//    crop is never materialised);
+//  * decode: the CENTER head's conv5 1x1 + sigmoid/clamp (head.py:110-124, 177-201), the Hann window
+//    (vipt.py:79-80) and cal_bbox's first-occurrence argmax + gather (head.py:142-160);
+//  * xcorr: SiamFC / DiMP per-sequence cross-correlation (grouped conv2d).
+#include <float.h>
+
+#include "kernels.h"
+
+namespace mmt {
+
+__constant__ float kMean[6] = {0.485f, 0.456f, 0.406f, 0.485f, 0.456f, 0.406f};
+__constant__ float kStd[6] = {0.229f, 0.224f, 0.225f, 0.229f, 0.224f, 0.225f};
+
+// padded-crop pixel: image row y1 + r is real only for 0 <= y <= H-2 (the reference slices
+// im[y1+y1_pad : y2-y2_pad] with y2_pad = max(y2-H+1, 0), which drops the last row/col)
+__device__ __forceinline__ int crop_px(const CropParam& p, int r, int x, int c) {
+  const int yy = p.y1 + r, xx = p.x1 + x;
+  if (yy < 0 || yy > p.H - 2 || xx < 0 || xx > p.W - 2) return 0;
+  return p.frame[(int64_t)yy * p.stride + (int64_t)xx * p.C + c];
+}
+
+__global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
+  const int b = blockIdx.y;
+  const CropParam p = a.params[b];
+  const int O = a.out_sz;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= O * O) return;
+  const int oy = idx / O, ox = idx - oy * O;
+  const int S = p.crop_sz;
+  const double scale = 1.0 / ((double)O / (double)S);
+  int u8[6];
+  if (fabs(scale - 2.0) < DBL_EPSILON) {
+    // cv::resize reroutes an exact 2x down-scale to INTER_AREA's fast path
+    for (int c = 0; c < a.C; ++c) {
+      const int s = crop_px(p, 2 * oy, 2 * ox, c) + crop_px(p, 2 * oy, 2 * ox + 1, c) +
+                    crop_px(p, 2 * oy + 1, 2 * ox, c) + crop_px(p, 2 * oy + 1, 2 * ox + 1, c);
+      u8[c] = (s + 2) >> 2;
+    }
+  } else {
+    float fx = (float)((ox + 0.5) * scale - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0.f; sx = 0; }
+    if (sx >= S - 1) { fx = 0.f; sx = S - 1; }
+    const int a0 = __float2int_rn((1.f - fx) * 2048.f), a1 = __float2int_rn(fx * 2048.f);
+    float fy = (float)((oy + 0.5) * scale - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const int b0 = __float2int_rn((1.f - fy) * 2048.f), b1 = __float2int_rn(fy * 2048.f);
+    const int r0 = min(max(sy, 0), S - 1), r1 = min(max(sy + 1, 0), S - 1);
+    const int sx1 = min(sx + 1, S - 1);
+    for (int c = 0; c < a.C; ++c) {
+      const int d0 = crop_px(p, r0, sx, c) * a0 + crop_px(p, r0, sx1, c) * a1;
+      const int d1 = crop_px(p, r1, sx, c) * a0 + crop_px(p, r1, sx1, c) * a1;
+      const int v = (((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16);
+      u8[c] = min(max((v + 2) >> 2, 0), 255);
+    }
+  }
+  const int np = O / 16;
+  const int patch = (oy >> 4) * np + (ox >> 4);
+  const int within = (oy & 15) * 16 + (ox & 15);
+  const int64_t rowoff = ((int64_t)b * a.rows_per_seq + a.row0 + patch) * 768;
+  for (int c = 0; c < a.C; ++c) {
+    const float t = ((float)u8[c] / 255.0f - kMean[c]) / kStd[c];
+    bf16_t* dst = (c < 3 ? a.A_rgb : a.A_aux) + rowoff + (c % 3) * 256 + within;
+    *dst = f2bf(t);
+    if (a.dbg_patch) a.dbg_patch[((int64_t)b * O * O + idx) * a.C + c] = (uint8_t)u8[c];
+  }
+}
+
+void crop_patchify(const CropArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(crop_kernel, dim3((a.out_sz * a.out_sz + 255) / 256, a.B), dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------ decode
+__device__ __forceinline__ float sigmoid_clamp(float x) {
+  const float y = 1.0f / (1.0f + expf(-x));
+  return fminf(fmaxf(y, 1e-4f), 1.0f - 1e-4f);
+}
+
+__global__ __launch_bounds__(256) void decode_kernel(const DecodeArgs a) {
+  __shared__ float sv[256];
+  __shared__ int si[256];
+  __shared__ float sw[5 * 32 + 5];
+  const int b = blockIdx.x, tid = threadIdx.x, n = a.fs * a.fs;
+  if (tid < 165) sw[tid] = tid < 160 ? a.w5[tid] : a.b5[tid - 160];
+  __syncthreads();
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  for (int p = tid; p < n; p += 256) {
+    float acc[5];
+#pragma unroll
+    for (int o = 0; o < 5; ++o) acc[o] = sw[160 + o];
+    const int br_of[5] = {0, 1, 1, 2, 2};
+#pragma unroll
+    for (int o = 0; o < 5; ++o) {
+      const float* h = a.h4 + ((int64_t)br_of[o] * a.B * n + (int64_t)b * n + p) * 32;
+      float s = 0.f;
+      for (int k = 0; k < 32; ++k) s += h[k] * sw[o * 32 + k];
+      acc[o] += s;
+    }
+    const float ctr = sigmoid_clamp(acc[0]);
+    const float resp = a.hann[p] * ctr;
+    if (a.maps) {
+      float* mp = a.maps + (int64_t)b * 5 * n;
+      mp[p] = ctr;
+      mp[n + p] = sigmoid_clamp(acc[3]);
+      mp[2 * n + p] = sigmoid_clamp(acc[4]);
+      mp[3 * n + p] = acc[1];
+      mp[4 * n + p] = acc[2];
+    }
+    if (resp > best) { best = resp; bidx = p; }
+  }
+  sv[tid] = best;
+  si[tid] = bidx;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) {
+      const float v2 = sv[tid + st];
+      const int i2 = si[tid + st];
+      if (v2 > sv[tid] || (v2 == sv[tid] && i2 < si[tid])) { sv[tid] = v2; si[tid] = i2; }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int p = si[0];
+    float acc[5];
+    const int br_of[5] = {0, 1, 1, 2, 2};
+    for (int o = 0; o < 5; ++o) {
+      const float* h = a.h4 + ((int64_t)br_of[o] * a.B * n + (int64_t)b * n + p) * 32;
+      float s = 0.f;
+      for (int k = 0; k < 32; ++k) s += h[k] * sw[o * 32 + k];
+      acc[o] = sw[160 + o] + s;
+    }
+    const int iy = p / a.fs, ix = p - iy * a.fs;
+    float* r = a.res + (int64_t)b * 8;
+    r[0] = ((float)ix + acc[1]) / (float)a.fs;
+    r[1] = ((float)iy + acc[2]) / (float)a.fs;
+    r[2] = sigmoid_clamp(acc[3]);
+    r[3] = sigmoid_clamp(acc[4]);
+    r[4] = sv[0];
+    r[5] = (float)p;
+    r[6] = 0.f;
+    r[7] = 0.f;
+  }
+}
+
+void decode(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(decode_kernel, dim3(a.B), dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------ cross-correlation
+// One thread per output pixel, channel loop with the exemplar staged in LDS per 16-channel slab.
+__global__ __launch_bounds__(256) void xcorr_kernel(const float* Z, const float* X, float* out, int C, int hz,
+                                                    int wz, int hx, int wx, float scale, float bias) {
+  extern __shared__ float zs[];
+  const int b = blockIdx.y;
+  const int ho = hx - hz + 1, wo = wx - wz + 1;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int y = idx / wo, x = idx - (idx / wo) * wo;
+  const bool live = idx < ho * wo;
+  float acc = 0.f;
+  const int zsz = hz * wz;
+  for (int c0 = 0; c0 < C; c0 += 16) {
+    const int cn = min(16, C - c0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < cn * zsz; i += 256) zs[i] = Z[((int64_t)b * C + c0) * zsz + i];
+    __syncthreads();
+    if (live) {
+      for (int c = 0; c < cn; ++c) {
+        const float* xp = X + (((int64_t)b * C + c0 + c) * hx + y) * wx + x;
+        const float* zp = zs + c * zsz;
+        for (int i = 0; i < hz; ++i)
+          for (int j = 0; j < wz; ++j) acc += xp[i * wx + j] * zp[i * wz + j];
+      }
+    }
+  }
+  if (live) out[((int64_t)b * ho + y) * wo + x] = acc * scale + bias;
+}
+
+void xcorr(const float* Z, const float* X, float* out, int B, int C, int hz, int wz, int hx, int wx, float scale,
+           float bias, hipStream_t s) {
+  const int n = (hx - hz + 1) * (wx - wz + 1);
+  hipLaunchKernelGGL(xcorr_kernel, dim3((n + 255) / 256, B), dim3(256), 16 * hz * wz * sizeof(float), s, Z, X, out,
+                     C, hz, wz, hx, wx, scale, bias);
+}
+
+}  // namespace mmt

@@ -1,0 +1,136 @@
+// Launch interfaces of the hand-written gfx950 kernels (host side).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace mmt {
+
+// ---------------------------------------------------------------- GEMM (MFMA bf16 -> fp32)
+// C[m][n] = epi( sum_k A[m][k] * W[n][k] + bias[n] ), A: M x K (lda), W: N x K (ldw), both bf16, K-contiguous.
+enum Epi : int {
+  EPI_BF16 = 0,        // bias -> bf16
+  EPI_GELU_BF16 = 1,   // bias, exact GELU -> bf16
+  EPI_RESID_F32 = 2,   // C(f32) = R(f32) + (acc + bias)
+  EPI_RELU_BF16 = 3,   // bias, ReLU -> bf16            (head conv, BN folded)
+  EPI_F32 = 4,         // bias -> f32
+  EPI_RELU_F32 = 5,    // bias, ReLU -> f32
+  EPI_POS_F32 = 6,     // C(f32) = (acc + bias) + R[m % pos_rows]  (OSTrack patch-embed + pos_embed)
+};
+enum AMode : int { A_DENSE = 0, A_CONV3 = 1 };
+
+struct GemmGroup {
+  const bf16_t* A; int64_t lda;
+  const bf16_t* W; int64_t ldw;
+  const float* bias;
+  void* C; int64_t ldc;
+  const float* R; int64_t ldr;
+};
+
+struct GemmArgs {
+  GemmGroup g[3];
+  int groups;
+  int M, N, K;
+  int amode;
+  int conv_hw;      // A_CONV3: feature map is conv_hw x conv_hw (NHWC rows), zero padding 1
+  int conv_cin;     // A_CONV3: input channels (multiple of 64)
+  int pos_rows;     // EPI_POS_F32
+};
+
+void gemm(const GemmArgs& a, int epi, hipStream_t s);
+
+// ---------------------------------------------------------------- attention
+struct AttnArgs {
+  const bf16_t* qkv;   // [B][N][3*C]
+  bf16_t* out;         // [B][N][C]
+  int B, N, heads;     // head dim 64, C = 64*heads
+  int ce_query;        // template token whose probability row is exported (-1: none)
+  int ce_lens_t;       // template length; exported keys are [ce_lens_t, N)
+  float* ce_prob;      // [B][heads][N - ce_lens_t]
+};
+void attention(const AttnArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- layer norm (row of 768)
+// out_bf16[r] = LN(x[src(r)]), src(r) = gather ? b*in_pitch + gather[b][t] : r ; optional copy of x[src] to xcopy[r]
+void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, float* out_f32, int rows,
+               int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy, hipStream_t s);
+
+// ---------------------------------------------------------------- ViPT prompt blocks
+struct PromptArgs {
+  int layer;                 // 0: inputs are the two patch-embed outputs
+  int B, Lz, Lx;             // slots per sequence = Lz + Lx
+  const float* srcA;         // layer 0: tok_rgb [B][L][768]; else residual X [B][Nrows][768] (compact)
+  int srcA_rows;             // rows per sequence of srcA
+  const float* srcB;         // layer 0: tok_aux [B][L][768]; else previous prompt P [B][L][768]
+  const int* slot2pos;       // [B][Lx] compact position (or -1) of search slots; null at layer 0
+  const float* lnA_w; const float* lnA_b;   // prompt_norms[i-1] (layer 0: prompt_norms[0])
+  const float* lnB_w; const float* lnB_b;   // prompt_norms[i]
+  const float* w00; const float* b00;       // conv0_0 [8][768]
+  const float* w01; const float* b01;       // conv0_1 [8][768]
+  const float* w1; const float* b1;         // conv1x1 [768][8]
+  float smooth;                             // fovea.smooth (device scalar copied to host at load)
+  float* a8;                 // scratch [B][L][8]
+  float* c8;                 // scratch [B][L][8]
+  float* P;                  // out prompt [B][L][768] (full slot layout)
+  float* X;                  // residual (layer 0: written [B][L][768]; else += at compact positions)
+  int X_rows;                // rows per sequence of X
+  const float* tok_rgb;      // layer 0: the RGB tokens added to the prompt
+  const float* pos;          // layer 0: pos_embed [L][768]
+};
+void prompt_reduce(const PromptArgs& a, hipStream_t s);
+void prompt_expand(const PromptArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- candidate elimination
+struct CEArgs {
+  int B, Lz, Ls, keep, heads, Lx;
+  const float* prob;      // [B][heads][Ls]
+  const int* gidx_in;     // [B][Ls] slot id of compact search token
+  int* gidx_out;          // [B][keep]
+  int* gather;            // [B][Lz + keep] source compact row of each new row
+  int* slot2pos;          // [B][Lx] updated
+  int* removed;           // [B][Lx] removed slot ids, appended at removed_off
+  int removed_off;
+};
+void ce_select(const CEArgs& a, hipStream_t s);
+void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s);
+
+// final norm + token recovery (zeros at pruned slots) -> head input NHWC bf16 [B][Lx][768]
+void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
+                        int B, int Lz, int Lx, bf16_t* feat, float* feat_f32_dbg, hipStream_t s);
+
+// ---------------------------------------------------------------- crop + normalise + patchify
+struct CropParam {                 // one per sequence (device memory, rewritten every frame)
+  const uint8_t* frame;            // H x W x C uint8, row stride in bytes
+  int64_t stride;
+  int H, W, C;
+  int x1, y1, crop_sz;             // processing_utils.py:32-41
+  int pad_;
+};
+struct CropArgs {
+  const CropParam* params;         // [B]
+  int B, out_sz, C;                // C = 6 (RGB+aux) or 3
+  bf16_t* A_rgb; bf16_t* A_aux;    // [B][rows_per_seq][768]
+  int rows_per_seq, row0;          // patch rows land at row0 + patch index
+  uint8_t* dbg_patch;              // optional [B][out][out][C]
+};
+void crop_patchify(const CropArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- head tail + decode
+struct DecodeArgs {
+  int B, fs;                       // feature map fs x fs
+  const float* h4;                 // [3][B][fs*fs][32]  (ctr, offset, size) conv4 outputs (ReLU'd)
+  const float* w5;                 // [5][32]: ctr, off_x, off_y, size_w, size_h
+  const float* b5;                 // [5]
+  const float* hann;               // [fs*fs]
+  float* res;                      // [B][8]: cx, cy, w, h, score, idx
+  float* maps;                     // optional [B][5][fs*fs] (ctr, size w/h, offset x/y)
+};
+void decode(const DecodeArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- SiamFC / DiMP correlation
+// out[b][y][x] = scale * sum_{c,i,j} X[b][c][y+i][x+j] * Z[b][c][i][j] + bias   (valid, fp32)
+void xcorr(const float* Z, const float* X, float* out, int B, int C, int hz, int wz, int hx, int wx, float scale,
+           float bias, hipStream_t s);
+
+}  // namespace mmt

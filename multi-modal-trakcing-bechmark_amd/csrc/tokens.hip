@@ -1,0 +1,320 @@
+// Bandwidth-bound token kernels of the ViPT path, gfx950: LayerNorm, the
+// modality-prompt blocks, candidate elimination, final norm + token recovery.
+// Rows are 768 fp32 (one wave per row, 3 x float4 per lane).
+#include "kernels.h"
+
+namespace mmt {
+
+constexpr int C768 = 768;
+constexpr float LN_EPS = 1e-6f;   // vit_ce_prompt.py:121
+
+struct Row12 { float4 v[3]; };
+
+__device__ __forceinline__ Row12 load_row(const float* p, int lane) {
+  Row12 r;
+  const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) r.v[i] = q[lane + 64 * i];
+  return r;
+}
+__device__ __forceinline__ Row12 zero_row() {
+  Row12 r;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) r.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  return r;
+}
+
+// LayerNorm over 768 (F.layer_norm semantics: biased variance, eps inside sqrt)
+__device__ __forceinline__ Row12 ln_row(const Row12& x, const float* w, const float* b, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) s += x.v[i].x + x.v[i].y + x.v[i].z + x.v[i].w;
+  const float mean = wave_sum(s) * (1.0f / C768);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 d = make_float4(x.v[i].x - mean, x.v[i].y - mean, x.v[i].z - mean, x.v[i].w - mean);
+    q += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / C768) + LN_EPS);
+  Row12 y;
+  const float4* w4 = reinterpret_cast<const float4*>(w);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 ww = w4[lane + 64 * i], bb = b4[lane + 64 * i];
+    y.v[i] = make_float4((x.v[i].x - mean) * rstd * ww.x + bb.x, (x.v[i].y - mean) * rstd * ww.y + bb.y,
+                         (x.v[i].z - mean) * rstd * ww.z + bb.z, (x.v[i].w - mean) * rstd * ww.w + bb.w);
+  }
+  return y;
+}
+
+__device__ __forceinline__ void store_bf16(bf16_t* p, const Row12& y, int lane) {
+  uint2* q = reinterpret_cast<uint2*>(p);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    uint2 o;
+    o.x = (uint32_t)f2bf(y.v[i].x) | ((uint32_t)f2bf(y.v[i].y) << 16);
+    o.y = (uint32_t)f2bf(y.v[i].z) | ((uint32_t)f2bf(y.v[i].w) << 16);
+    q[lane + 64 * i] = o;
+  }
+}
+__device__ __forceinline__ void store_f32(float* p, const Row12& y, int lane) {
+  float4* q = reinterpret_cast<float4*>(p);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) q[lane + 64 * i] = y.v[i];
+}
+
+// ------------------------------------------------------------------ LayerNorm (optionally fused CE gather)
+__global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w, const float* b, bf16_t* ob,
+                                                 float* of, int rows, int rows_per_seq, const int* gather,
+                                                 int in_rows_per_seq, float* xcopy) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  int64_t src = r;
+  if (gather) {
+    const int bs = r / rows_per_seq;
+    src = (int64_t)bs * in_rows_per_seq + gather[r];
+  }
+  const Row12 xv = load_row(x + src * C768, lane);
+  if (xcopy) store_f32(xcopy + (int64_t)r * C768, xv, lane);
+  const Row12 y = ln_row(xv, w, b, lane);
+  if (ob) store_bf16(ob + (int64_t)r * C768, y, lane);
+  if (of) store_f32(of + (int64_t)r * C768, y, lane);
+}
+
+void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, float* out_f32, int rows,
+               int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy, hipStream_t s) {
+  hipLaunchKernelGGL(ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_f32, rows,
+                     rows_per_seq, gather, in_rows_per_seq, xcopy);
+}
+
+// ------------------------------------------------------------------ prompt block, part 1
+// For every slot s of every sequence: a8 = conv0_0(LN_A(srcA[s])), c8 = conv0_1(LN_B(srcB[s]))
+// (Prompt_block.forward, vit_ce_prompt.py:62-68, on token2feature maps; a pruned search slot
+// is a zero row, vit_ce_prompt.py:276-283, whose LN is the LN bias).
+__device__ __forceinline__ void dot8(const Row12& y, const float* W, const float* bias, float* out, int lane) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float4* w4 = reinterpret_cast<const float4*>(W + c * C768);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float4 ww = w4[lane + 64 * i];
+      s += y.v[i].x * ww.x + y.v[i].y * ww.y + y.v[i].z * ww.z + y.v[i].w * ww.w;
+    }
+    s = wave_sum(s);
+    if (lane == c) out[c] = s + bias[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) {
+  const int L = a.Lz + a.Lx;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= a.B * L) return;
+  const int b = row / L, s = row - b * L;
+  Row12 xa;
+  if (a.layer == 0) {
+    xa = load_row(a.srcA + (int64_t)row * C768, lane);
+  } else {
+    const int pos = s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];
+    xa = pos >= 0 ? load_row(a.srcA + ((int64_t)b * a.srcA_rows + pos) * C768, lane) : zero_row();
+  }
+  const Row12 ya = ln_row(xa, a.lnA_w, a.lnA_b, lane);
+  dot8(ya, a.w00, a.b00, a.a8 + (int64_t)row * 8, lane);
+  const Row12 xb = load_row(a.srcB + (int64_t)row * C768, lane);
+  const Row12 yb = ln_row(xb, a.lnB_w, a.lnB_b, lane);
+  dot8(yb, a.w01, a.b01, a.c8 + (int64_t)row * 8, lane);
+}
+
+void prompt_reduce(const PromptArgs& a, hipStream_t s) {
+  const int rows = a.B * (a.Lz + a.Lx);
+  hipLaunchKernelGGL(prompt_reduce_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------ prompt block, part 2
+// Fovea (vit_ce_prompt.py:33-47): per channel, softmax over the part's h*w positions of
+// x*smooth, times x; + conv0_1 branch; conv1x1 8 -> 768 (+bias) -> prompt P (full slot
+// layout). Residual: layer 0  X = (tok_rgb + P) + pos   (vit_ce_prompt.py:218, 240-241)
+//                   layer i   X[pos(s)] += P[s]          (vit_ce_prompt.py:310, attn_blocks.py:9-18)
+constexpr int PCHUNK = 64;
+
+__global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) {
+  __shared__ float red[256];
+  __shared__ float smax[8], ssum[8];
+  __shared__ float f[PCHUNK][8];
+  const int L = a.Lz + a.Lx, b = blockIdx.y, tid = threadIdx.x;
+  const int nbz = (a.Lz + PCHUNK - 1) / PCHUNK;
+  int lo, n, t0;
+  if ((int)blockIdx.x < nbz) {
+    lo = 0; n = a.Lz; t0 = blockIdx.x * PCHUNK;
+  } else {
+    lo = a.Lz; n = a.Lx; t0 = a.Lz + (blockIdx.x - nbz) * PCHUNK;
+  }
+  const int t1 = min(t0 + PCHUNK, lo + n);
+  const float* a8 = a.a8 + (int64_t)b * L * 8;
+  const float* c8 = a.c8 + (int64_t)b * L * 8;
+  const float sm = a.smooth;
+  // per-channel max of x*smooth over the part
+  const int c = tid & 7, stripe = tid >> 3;
+  float mx = -INFINITY;
+  for (int t = lo + stripe; t < lo + n; t += 32) mx = fmaxf(mx, a8[t * 8 + c] * sm);
+  red[tid] = mx;
+  __syncthreads();
+  if (tid < 8) {
+    float v = -INFINITY;
+    for (int k = 0; k < 32; ++k) v = fmaxf(v, red[k * 8 + tid]);
+    smax[tid] = v;
+  }
+  __syncthreads();
+  const float cm = smax[c];
+  float sum = 0.f;
+  for (int t = lo + stripe; t < lo + n; t += 32) sum += __expf(a8[t * 8 + c] * sm - cm);
+  red[tid] = sum;
+  __syncthreads();
+  if (tid < 8) {
+    float v = 0.f;
+    for (int k = 0; k < 32; ++k) v += red[k * 8 + tid];
+    ssum[tid] = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < (t1 - t0) * 8; i += 256) {
+    const int t = t0 + i / 8, ch = i & 7;
+    const float v = a8[t * 8 + ch];
+    const float msk = __expf(v * sm - smax[ch]) / ssum[ch];
+    f[i / 8][ch] = msk * v + c8[t * 8 + ch];
+  }
+  __syncthreads();
+  float w1r[3][8], b1r[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int col = tid + 256 * k;
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) w1r[k][ch] = a.w1[col * 8 + ch];
+    b1r[k] = a.b1[col];
+  }
+  for (int t = t0; t < t1; ++t) {
+    int pos;
+    if (a.layer == 0) pos = t;
+    else pos = t < a.Lz ? t : a.slot2pos[b * a.Lx + (t - a.Lz)];
+    float* prow = a.P + ((int64_t)b * L + t) * C768;
+    float* xrow = pos >= 0 ? a.X + ((int64_t)b * a.X_rows + pos) * C768 : nullptr;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int col = tid + 256 * k;
+      float v = b1r[k];
+#pragma unroll
+      for (int ch = 0; ch < 8; ++ch) v += w1r[k][ch] * f[t - t0][ch];
+      prow[col] = v;
+      if (a.layer == 0) {
+        xrow[col] = (a.tok_rgb[((int64_t)b * L + t) * C768 + col] + v) + a.pos[(int64_t)t * C768 + col];
+      } else if (xrow) {
+        xrow[col] += v;
+      }
+    }
+  }
+}
+
+void prompt_expand(const PromptArgs& a, hipStream_t s) {
+  const int nb = (a.Lz + PCHUNK - 1) / PCHUNK + (a.Lx + PCHUNK - 1) / PCHUNK;
+  hipLaunchKernelGGL(prompt_expand_kernel, dim3(nb, a.B), dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------ candidate elimination
+// attn_blocks.py:37-73: score = mean over heads of the CTR_POINT template row of P over the
+// search keys, sort descending, keep ceil(ratio * Ls); ties broken by the lower index.
+__device__ __forceinline__ bool before(float ka, int va, float kb, int vb) {
+  return ka > kb || (ka == kb && va < vb);
+}
+
+__global__ __launch_bounds__(512) void ce_select_kernel(const CEArgs a) {
+  __shared__ float key[1024];
+  __shared__ int val[1024];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  int P2 = 1;
+  while (P2 < a.Ls) P2 <<= 1;
+  const float* prob = a.prob + (int64_t)b * a.heads * a.Ls;
+  for (int i = tid; i < P2; i += 512) {
+    float s = -INFINITY;
+    if (i < a.Ls) {
+      s = 0.f;
+      for (int h = 0; h < a.heads; ++h) s += prob[h * a.Ls + i];
+      s = s / (float)a.heads;
+    }
+    key[i] = s;
+    val[i] = i;
+  }
+  __syncthreads();
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P2; i += 512) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;   // this sub-sequence sorted in "before" order
+          const bool ib = before(key[i], val[i], key[ixj], val[ixj]);
+          if (up ? !ib : ib) {
+            const float tk = key[i]; key[i] = key[ixj]; key[ixj] = tk;
+            const int tv = val[i]; val[i] = val[ixj]; val[ixj] = tv;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int Ln = a.Lz + a.keep;
+  for (int i = tid; i < a.Ls; i += 512) {
+    const int src = val[i];
+    const int slot = a.gidx_in[b * a.Ls + src];
+    if (i < a.keep) {
+      a.gidx_out[b * a.keep + i] = slot;
+      a.gather[b * Ln + a.Lz + i] = a.Lz + src;
+      a.slot2pos[b * a.Lx + slot] = a.Lz + i;
+    } else {
+      a.removed[b * a.Lx + a.removed_off + (i - a.keep)] = slot;
+      a.slot2pos[b * a.Lx + slot] = -1;
+    }
+  }
+  for (int t = tid; t < a.Lz; t += 512) a.gather[b * Ln + t] = t;
+}
+
+void ce_select(const CEArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(ce_select_kernel, dim3(a.B), dim3(512), 0, s, a);
+}
+
+__global__ void init_indices_kernel(int* gidx, int* slot2pos, int B, int Lz, int Lx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * Lx) return;
+  const int j = i % Lx;
+  gidx[i] = j;
+  slot2pos[i] = Lz + j;
+}
+
+void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s) {
+  hipLaunchKernelGGL(init_indices_kernel, dim3((B * Lx + 255) / 256), dim3(256), 0, s, gidx, slot2pos, B, Lz, Lx);
+}
+
+// ------------------------------------------------------------------ final norm + recover_tokens
+// vit_ce_prompt.py:318-339: LN over the surviving tokens, then scatter the search tokens back
+// to their 16x16 slots; pruned slots are exact zeros.
+__global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int rows_per_seq, const int* slot2pos,
+                                                         const float* w, const float* b, int B, int Lz, int Lx,
+                                                         bf16_t* feat, float* dbg) {
+  const int L = Lz + Lx;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= B * L) return;
+  const int bs = r / L, s = r - bs * L;
+  int pos = s < Lz ? s : slot2pos[bs * Lx + (s - Lz)];
+  Row12 y = zero_row();
+  if (pos >= 0) y = ln_row(load_row(X + ((int64_t)bs * rows_per_seq + pos) * C768, lane), w, b, lane);
+  if (s >= Lz) store_bf16(feat + ((int64_t)bs * Lx + (s - Lz)) * C768, y, lane);
+  if (dbg) store_f32(dbg + (int64_t)r * C768, y, lane);
+}
+
+void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
+                        int B, int Lz, int Lx, bf16_t* feat, float* feat_f32_dbg, hipStream_t s) {
+  const int rows = B * (Lz + Lx);
+  hipLaunchKernelGGL(final_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, X, rows_per_seq, slot2pos, w, b, B,
+                     Lz, Lx, feat, feat_f32_dbg);
+}
+
+}  // namespace mmt

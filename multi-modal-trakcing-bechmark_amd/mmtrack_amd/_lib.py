@@ -1,0 +1,86 @@
+"""ctypes binding of the in-tree C-ABI library ``libmmtrack.so`` (include/mmtrack.h).
+
+The product path has no fallback: if the HIP library is missing or fails to load, importing
+this module raises, so nothing can silently run on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MMTRACK_LIB", os.path.join(_HERE, "libmmtrack.so"))
+
+MMT_OK, MMT_E_ARG, MMT_E_STATE, MMT_E_HIP, MMT_E_WEIGHTS, MMT_E_BOX = 0, -1, -2, -3, -4, -5
+MMT_MODEL_VIPT, MMT_MODEL_OSTRACK = 0, 1
+MMT_PROMPT_NONE, MMT_PROMPT_SHAW, MMT_PROMPT_DEEP = 0, 1, 2
+
+
+class MmtConfig(ctypes.Structure):
+    _fields_ = [
+        ("model", ctypes.c_int),
+        ("prompt_type", ctypes.c_int),
+        ("in_chans", ctypes.c_int),
+        ("template_size", ctypes.c_int),
+        ("search_size", ctypes.c_int),
+        ("template_factor", ctypes.c_double),
+        ("search_factor", ctypes.c_double),
+        ("n_ce", ctypes.c_int),
+        ("ce_loc", ctypes.c_int * 12),
+        ("ce_keep_ratio", ctypes.c_double * 12),
+        ("ce_template_index", ctypes.c_int),
+        ("head_channels", ctypes.c_int),
+        ("max_batch", ctypes.c_int),
+        ("use_graphs", ctypes.c_int),
+        ("debug_outputs", ctypes.c_int),
+    ]
+
+
+# every symbol include/mmtrack.h declares: name -> (restype, argtypes)
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_D = ctypes.c_double
+_F = ctypes.c_float
+_I64 = ctypes.c_int64
+SIGNATURES = {
+    "mmt_create": (_I, [ctypes.POINTER(MmtConfig), _I, ctypes.POINTER(_P)]),
+    "mmt_destroy": (None, [_P]),
+    "mmt_last_error": (ctypes.c_char_p, [_P]),
+    "mmt_version": (ctypes.c_char_p, []),
+    "mmt_set_tensor": (_I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(_I64), _I]),
+    "mmt_finalize": (_I, [_P]),
+    "mmt_num_expected_keys": (_I, [_P]),
+    "mmt_expected_key": (ctypes.c_char_p, [_P, _I]),
+    "mmt_initialize": (_I, [_P, _I, _P, _I, _I, _I, _I64, _I, ctypes.POINTER(_D)]),
+    "mmt_track": (_I, [_P, _I, _P, _I, _I, _I, _I64, _I, ctypes.POINTER(_D), ctypes.POINTER(_F)]),
+    "mmt_track_batch": (_I, [_P, _I, _I, ctypes.POINTER(_P), ctypes.POINTER(_I), ctypes.POINTER(_I), _I,
+                             ctypes.POINTER(_I64), _I, ctypes.POINTER(_D), ctypes.POINTER(_F)]),
+    "mmt_get_state": (_I, [_P, _I, ctypes.POINTER(_D)]),
+    "mmt_set_state": (_I, [_P, _I, ctypes.POINTER(_D)]),
+    "mmt_debug_fetch": (_I, [_P, ctypes.c_char_p, _I, _P, ctypes.c_size_t]),
+    "mmt_timing_enable": (_I, [_P, ctypes.c_char_p]),
+    "mmt_timing_read": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_D), ctypes.POINTER(_D), ctypes.POINTER(_D)]),
+    "mmt_xcorr": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P]),
+    "mmt_op_gemm": (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "mmt_op_attention": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "mmt_op_layernorm": (_I, [_P, _P, _P, _P, _P, _I, _P]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libmmtrack.so (raises ImportError if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libmmtrack.so not found at {LIB_PATH}; build it with "
+                          f"`make -C multi-modal-trakcing-bechmark_amd/csrc` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
