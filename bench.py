@@ -1,0 +1,180 @@
+"""Headline benchmark: tracked frames/sec/GPU, ViPT-deep ViT-B, 128^2 template / 256^2 search, bf16.
+
+One "step" = one tracking step of B independent sequences on each GPU (mmt_track_batch): crop +
+normalise from the HBM-resident frame, dual patch-embed, 12 ViT-B blocks with deep prompts and CE,
+CENTER head, windowed argmax decode, box back-mapping.  Frames are synthetic 640x480x6 uint8
+(RGB + thermal-like aux) already resident in HBM; weights are the seeded synthetic law of
+mmtrack_amd.synth (no checkpoint ships with the reference).
+
+Multi-GPU: one process per GPU (torchrun), sequences sharded per rank, no data-path collective
+(the reference shards sequences over a Pool, test_rgbt_mgpus.py:180-184); a gloo barrier and a
+max-over-ranks of the timed region only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "multi-modal-trakcing-bechmark_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0
+
+WORKLOADS = {
+    # name: (engine kwargs, synth shape kwargs, frame H, W, C, published-config description)
+    "vipt_deep_rgbt": (dict(), dict(kind="vipt", prompt_type="vipt_deep"), 480, 640, 6,
+                       "ViPT-deep RGB-T, ViT-B/16, template 128 / search 256 (BASELINE configs[1])"),
+    "vipt_deep_rgbd": (dict(), dict(kind="vipt", prompt_type="vipt_deep"), 360, 640, 6,
+                       "ViPT-deep RGB-D (DepthTrack shapes 640x360) (BASELINE configs[2])"),
+    "ostrack384": (dict(model="ostrack", prompt_type="none", in_chans=3, template_size=192, search_size=384,
+                        search_factor=5.0), dict(kind="ostrack", search_size=384, template_size=192), 480, 640, 3,
+                   "OSTrack RGB ViT-B, template 192 / search 384 (BASELINE configs[3])"),
+}
+GFLOP_PER_FRAME = {"vipt_deep_rgbt": 45.80, "vipt_deep_rgbd": 45.80, "ostrack384": 109.34}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(workload, frames_np, gts, seconds=12.0):
+    """The fp32 CPU oracle tracker (oracle/tracker.py) on the same synthetic frames, bounded sample."""
+    from mmtrack_amd import synth
+    from oracle import tracker as otracker
+    from oracle import vipt as ov
+    ekw, skw, H, W, C, _ = WORKLOADS[workload]
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = synth.make_state_dict(0, **skw)
+    cfg = ov.NetCfg(kind=skw["kind"], prompt_type=skw.get("prompt_type", "vipt_deep"),
+                    search_size=skw.get("search_size", 256), template_size=skw.get("template_size", 128))
+    tr = otracker.OracleTracker(sd, cfg, search_factor=ekw.get("search_factor", 4.0))
+    tr.initialize(frames_np[0], {"init_bbox": list(gts[0])})
+    tr.track(frames_np[1])  # warm
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        tr.track(frames_np[2 + n % (len(frames_np) - 2)])
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} frames of one sequence through the fp32 CPU oracle tracker "
+                      f"(crop+net+decode, torch {threads} threads, {dt:.1f}s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=32, help="sequences tracked per GPU per step")
+    ap.add_argument("--workload", default="vipt_deep_rgbt", choices=list(WORKLOADS))
+    ap.add_argument("--frames", type=int, default=8, help="distinct synthetic frames per sequence (cycled)")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--probe", default="fc1", help="kernel class timed with HIP events for the roofline")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+    torch.cuda.set_device(local)
+
+    from mmtrack_amd import Engine, EngineConfig, synth
+    ekw, skw, H, W, C, desc = WORKLOADS[args.workload]
+    B = args.batch
+    cfg = EngineConfig(max_batch=B, use_graphs=not args.no_graphs, **ekw)
+    sd = synth.make_state_dict(0, **skw)
+    eng = Engine(cfg, sd, device=local)
+
+    # synthetic video, HBM-resident; every sequence tracks its own target box in it
+    video_np, gts = synth.make_frames(1000 + rank, args.frames + 1, H, W, C)
+    video = torch.from_numpy(video_np).cuda()
+    boxes0 = [[60.0 + (37 * i) % (W - 160), 40.0 + (23 * i) % (H - 120), 30.0 + (i % 5) * 6, 24.0 + (i % 3) * 8]
+              for i in range(B)]
+    for i in range(B):
+        eng.initialize(i, video[0], boxes0[i])
+    torch.cuda.synchronize()
+    frame_lists = [[video[1 + t]] * B for t in range(args.frames)]
+
+    def step(k):
+        eng.track_batch(0, frame_lists[k % args.frames])
+
+    # the roofline probe brackets every launch of the dominant kernel class with HIP events that are
+    # captured into the replayed graph, so its per-launch times come from the timed region itself
+    if args.probe:
+        eng.timing_enable(args.probe)
+    for k in range(max(args.warmup, 2)):
+        step(k)
+    if args.probe:
+        eng.timing_enable(args.probe)   # reset counters: keep only the timed region
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    frames_total = world * B * args.steps
+    value = frames_total / elapsed
+
+    roof = None
+    if args.probe:
+        tr = eng.timing_read()
+        eng.timing_enable(None)
+        if tr["launches"]:
+            avg_ms = tr["total_ms"] / tr["launches"]
+            fl = tr["flops"] / tr["launches"]
+            achieved = fl / (avg_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "kernel": f"gemm[{args.probe}]", "achieved": round(achieved, 1),
+                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                    "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 2), "flop_per_launch": fl,
+                    "launches": tr["launches"]}
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args.workload, video_np, gts, args.cpu_seconds)
+        gf = GFLOP_PER_FRAME[args.workload]
+        line = {
+            "metric": "tracked frames/sec/GPU, ViPT ViT-B 256² search bf16, at 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": args.workload, "description": desc, "sequences_per_gpu": B,
+                       "global_batch": B * world, "frame": f"{W}x{H}x{C} uint8 (HBM-resident)",
+                       "template": cfg.template_size, "search": cfg.search_size, "parallelism": f"seq-shard x{world}",
+                       "graphs": cfg.use_graphs, "weights": "synthetic seeded (no checkpoint ships)"},
+            "per_gpu_fps": round(value / world, 2),
+            "model_tflops": round(value * gf / 1e3, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -11,6 +11,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/mmtrack.h"
@@ -48,13 +49,20 @@ struct PromptW {
   float smooth;
 };
 
+struct GraphEntry {
+  hipGraphExec_t exec = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;   // probe events captured as graph nodes
+  std::vector<std::pair<double, double>> work;         // flops / bytes of each bracketed launch
+};
+
 struct TimingProbe {
   std::string cls;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;  // pool
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;  // eager pool
   size_t used = 0;
   long launches = 0;
   double total_ms = 0, flops = 0, bytes = 0;
   std::vector<std::pair<double, double>> pending_work;  // flops/bytes of each pending pair
+  GraphEntry* capture = nullptr;                        // set while capturing a graph
 };
 
 }  // namespace
@@ -111,7 +119,7 @@ struct mmt_engine {
   std::vector<double> last_rf;
   int last_batch = 0;
 
-  std::map<std::pair<int, int>, hipGraphExec_t> graphs;
+  std::map<std::tuple<int, int, std::string>, GraphEntry> graphs;
   std::unique_ptr<TimingProbe> probe;
 
   int fail(int code, const std::string& m) {
@@ -374,6 +382,15 @@ int alloc_acts(mmt_engine* e) {
 void probe_begin(mmt_engine* e, const char* cls, double flops, double bytes) {
   TimingProbe* p = e->probe.get();
   if (!p || p->cls != cls) return;
+  if (p->capture) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    p->capture->ev.push_back({a, b});
+    p->capture->work.push_back({flops, bytes});
+    hipEventRecord(a, e->stream);
+    return;
+  }
   if (p->used == p->ev.size()) {
     hipEvent_t a, b;
     hipEventCreate(&a);
@@ -386,9 +403,27 @@ void probe_begin(mmt_engine* e, const char* cls, double flops, double bytes) {
 void probe_end(mmt_engine* e, const char* cls) {
   TimingProbe* p = e->probe.get();
   if (!p || p->cls != cls) return;
+  if (p->capture) {
+    hipEventRecord(p->capture->ev.back().second, e->stream);
+    return;
+  }
   hipEventRecord(p->ev[p->used].second, e->stream);
   p->used++;
 }
+void probe_collect_graph(mmt_engine* e, const GraphEntry& g) {
+  TimingProbe* p = e->probe.get();
+  if (!p) return;
+  for (size_t i = 0; i < g.ev.size(); ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, g.ev[i].first, g.ev[i].second) == hipSuccess) {
+      p->total_ms += ms;
+      p->launches++;
+      p->flops += g.work[i].first;
+      p->bytes += g.work[i].second;
+    }
+  }
+}
+
 void probe_collect(mmt_engine* e) {
   TimingProbe* p = e->probe.get();
   if (!p) return;
@@ -682,28 +717,43 @@ void update_state(mmt_engine* e, int slot, const float* r, int Hh, int Ww, doubl
   st = {x1, y1, bw, bh};
 }
 
-int launch(mmt_engine* e, int b0, int n) {
-  if (!e->cfg.use_graphs || e->probe) {
+int launch(mmt_engine* e, int b0, int n, const GraphEntry** replayed) {
+  *replayed = nullptr;
+  if (!e->cfg.use_graphs) {
     enqueue_forward(e, b0, n);
     HIPCHECK(e, hipGetLastError());
     return MMT_OK;
   }
-  auto key = std::make_pair(b0, n);
+  const std::string pc = e->probe ? e->probe->cls : std::string();
+  auto key = std::make_tuple(b0, n, pc);
   auto it = e->graphs.find(key);
   if (it == e->graphs.end()) {
-    enqueue_forward(e, b0, n);  // warm / validate eagerly once
-    HIPCHECK(e, hipGetLastError());
-    hipGraph_t g;
-    HIPCHECK(e, hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    // first use of this batch shape: run eagerly (validates every launch, yields this frame's
+    // result), then capture the identical launch sequence for replay
+    TimingProbe* p = e->probe.get();
+    if (p) {
+      p->used = 0;
+      p->pending_work.clear();
+    }
     enqueue_forward(e, b0, n);
-    HIPCHECK(e, hipStreamEndCapture(e->stream, &g));
-    hipGraphExec_t ge;
-    HIPCHECK(e, hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    HIPCHECK(e, hipGetLastError());
+    GraphEntry entry;
+    if (p) p->capture = &entry;
+    hipGraph_t g;
+    hipError_t st = hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal);
+    if (st == hipSuccess) {
+      enqueue_forward(e, b0, n);
+      st = hipStreamEndCapture(e->stream, &g);
+    }
+    if (p) p->capture = nullptr;
+    if (st != hipSuccess) return e->fail(MMT_E_HIP, std::string("graph capture: ") + hipGetErrorString(st));
+    HIPCHECK(e, hipGraphInstantiate(&entry.exec, g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
-    it = e->graphs.emplace(key, ge).first;
-    return MMT_OK;  // the eager run above already produced this frame's result
+    e->graphs.emplace(key, std::move(entry));
+    return MMT_OK;
   }
-  HIPCHECK(e, hipGraphLaunch(it->second, e->stream));
+  HIPCHECK(e, hipGraphLaunch(it->second.exec, e->stream));
+  *replayed = &it->second;
   return MMT_OK;
 }
 
@@ -769,7 +819,13 @@ void mmt_destroy(mmt_engine* e) {
   if (!e) return;
   hipSetDevice(e->device);
   hipStreamSynchronize(e->stream);
-  for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second);
+  for (auto& kv : e->graphs) {
+    hipGraphExecDestroy(kv.second.exec);
+    for (auto& pr : kv.second.ev) {
+      hipEventDestroy(pr.first);
+      hipEventDestroy(pr.second);
+    }
+  }
   if (e->probe)
     for (auto& p : e->probe->ev) {
       hipEventDestroy(p.first);
@@ -820,7 +876,13 @@ int mmt_finalize(mmt_engine* e) {
     e->warena = nullptr;
     e->wused = 0;
   }
-  for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second);
+  for (auto& kv : e->graphs) {
+    hipGraphExecDestroy(kv.second.exec);
+    for (auto& pr : kv.second.ev) {
+      hipEventDestroy(pr.first);
+      hipEventDestroy(pr.second);
+    }
+  }
   e->graphs.clear();
   int r = pack_weights(e);
   if (r != MMT_OK) return r;
@@ -879,10 +941,14 @@ int mmt_track_batch(mmt_engine* e, int first_slot, int n, const uint8_t* const* 
     e->last_rf[slot] = rf;
   }
   HIPCHECK(e, hipMemcpyAsync(e->params_dev, e->params_host, n * sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
-  TRY(launch(e, first_slot, n));
+  const GraphEntry* replayed = nullptr;
+  TRY(launch(e, first_slot, n, &replayed));
   HIPCHECK(e, hipMemcpyAsync(e->res_host, e->res, (size_t)n * 8 * 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
-  probe_collect(e);
+  if (replayed)
+    probe_collect_graph(e, *replayed);
+  else
+    probe_collect(e);
   for (int i = 0; i < n; ++i) {
     const int slot = first_slot + i;
     update_state(e, slot, e->res_host + 8 * i, Hs[i], Ws[i], e->last_rf[slot]);

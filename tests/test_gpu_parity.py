@@ -34,7 +34,7 @@ NETS = {
                   EngineConfig(prompt_type="vipt_shaw", debug_outputs=True, use_graphs=False)),
     "ostrack384": (dict(kind="ostrack", search_size=384, template_size=192),
                    EngineConfig(model="ostrack", prompt_type="none", in_chans=3, template_size=192, search_size=384,
-                                search_factor=5.0, debug_outputs=True, use_graphs=False)),
+                                search_factor=4.0, debug_outputs=True, use_graphs=False)),
 }
 
 
