@@ -69,6 +69,8 @@ typedef struct mmt_config {
   int max_batch;           /* sequences (slots) this engine tracks concurrently    */
   int use_graphs;          /* capture the per-frame launch sequence in a hipGraph   */
   int debug_outputs;       /* keep crops / score maps / features for parity tests   */
+  int precision;           /* 0: bf16 GEMM operands (fp32 accumulate, fp32 residual / LN / softmax);
+                              1: fp32-faithful "bf16x3" split products (hi*hi + lo*hi + hi*lo)     */
 } mmt_config;
 
 /* lifecycle */

@@ -23,10 +23,13 @@ constexpr int KB = 64;         // keys per LDS tile
 constexpr int VT_PITCH = 68;   // bf16 per transposed-V row (136 B)
 constexpr int CE_MAX = 1024;   // max tokens for the exported CE row
 
-template <int WAVES>
+template <int WAVES, bool SPLIT>
 __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[KB * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[64 * VT_PITCH];
+  // SPLIT (fp32-faithful): every operand is an (hi, lo) bf16 pair and each product is
+  // hi*hi + lo*hi + hi*lo; the LDS images of K and V^T are held for both halves.
+  constexpr int NH = SPLIT ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[NH][KB * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[NH][64 * VT_PITCH];
   __shared__ float ce_row[CE_MAX];
 
   const int b = blockIdx.z, h = blockIdx.y;
@@ -37,14 +40,18 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
   const int qi = q0 + (lane & 15);
   const int g = lane >> 4;
 
-  bf16x8 qf[2];
+  const bf16_t* base_lo = SPLIT ? a.qkv_lo + (int64_t)b * N * C3 : nullptr;
+  bf16x8 qf[NH][2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (qi < N)
-      qf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)qi * C3 + h * 64 + 32 * s + 8 * g);
-    else
-      qf[s] = bf16x8{};
-  }
+  for (int hl = 0; hl < NH; ++hl)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16_t* bb = hl ? base_lo : base;
+      if (qi < N)
+        qf[hl][s] = *reinterpret_cast<const bf16x8*>(bb + (int64_t)qi * C3 + h * 64 + 32 * s + 8 * g);
+      else
+        qf[hl][s] = bf16x8{};
+    }
 
   f32x4 o[4];
 #pragma unroll
@@ -55,18 +62,19 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
 
   for (int kb = 0; kb < N; kb += KB) {
     __syncthreads();
-    for (int q = tid; q < KB * 8; q += WAVES * 64) {
-      const int r = q >> 3, c = q & 7, key = kb + r;
+    for (int q = tid; q < NH * KB * 8; q += WAVES * 64) {
+      const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
+      const int r = qq >> 3, c = qq & 7, key = kb + r;
       uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
       if (key < N) {
-        const bf16_t* row = base + (int64_t)key * C3 + h * 64 + c * 8;
+        const bf16_t* row = (hl ? base_lo : base) + (int64_t)key * C3 + h * 64 + c * 8;
         kv = *reinterpret_cast<const uint4*>(row + Cd);
         vv = *reinterpret_cast<const uint4*>(row + 2 * Cd);
       }
-      *reinterpret_cast<uint4*>(Ks + r * 64 + ((c ^ (r & 7)) << 3)) = kv;
+      *reinterpret_cast<uint4*>(Ks[hl] + r * 64 + ((c ^ (r & 7)) << 3)) = kv;
       const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(c * 8 + e) * VT_PITCH + r] = ve[e];
+      for (int e = 0; e < 8; ++e) Vt[hl][(c * 8 + e) * VT_PITCH + r] = ve[e];
     }
     __syncthreads();
 
@@ -77,8 +85,13 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int r = 16 * t + (lane & 15), c = 4 * s + g;
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + r * 64 + ((c ^ (r & 7)) << 3));
-        sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], sc[t], 0, 0, 0);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks[0] + r * 64 + ((c ^ (r & 7)) << 3));
+        sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][s], sc[t], 0, 0, 0);
+        if (SPLIT) {
+          const bf16x8 kl = *reinterpret_cast<const bf16x8*>(Ks[NH - 1] + r * 64 + ((c ^ (r & 7)) << 3));
+          sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qf[0][s], sc[t], 0, 0, 0);
+          sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[NH - 1][s], sc[t], 0, 0, 0);
+        }
       }
     }
     float bmax = -INFINITY;
@@ -122,32 +135,56 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
 
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      bf16x8 pf;
+      bf16x8 pf, pl;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         pf[r] = (__bf16)sc[2 * u][r];
         pf[4 + r] = (__bf16)sc[2 * u + 1][r];
+        if (SPLIT) {
+          pl[r] = (__bf16)(sc[2 * u][r] - (float)pf[r]);
+          pl[4 + r] = (__bf16)(sc[2 * u + 1][r] - (float)pf[4 + r]);
+        }
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const bf16_t* vrow = Vt + (16 * dt + (lane & 15)) * VT_PITCH + 32 * u + 4 * g;
-        const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(vrow);
-        const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(vrow + 16);
+        const int vo = (16 * dt + (lane & 15)) * VT_PITCH + 32 * u + 4 * g;
+        const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(Vt[0] + vo);
+        const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(Vt[0] + vo + 16);
         const bf16x8 vf = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+        if (SPLIT) {
+          const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(Vt[NH - 1] + vo);
+          const bf16x4 w1 = *reinterpret_cast<const bf16x4*>(Vt[NH - 1] + vo + 16);
+          const bf16x8 vl = __builtin_shufflevector(w0, w1, 0, 1, 2, 3, 4, 5, 6, 7);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, pf, o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl, o[dt], 0, 0, 0);
+        }
       }
     }
   }
 
   const float inv = 1.0f / l;
   if (qi < N) {
-    bf16_t* orow = a.out + ((int64_t)b * N + qi) * Cd + h * 64;
+    const int64_t orow = ((int64_t)b * N + qi) * Cd + h * 64;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
+      float v[4];
+      bf16_t hv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = o[dt][r] * inv;
+        hv[r] = f2bf(v[r]);
+      }
       uint2 w;
-      w.x = (uint32_t)f2bf(o[dt][0] * inv) | ((uint32_t)f2bf(o[dt][1] * inv) << 16);
-      w.y = (uint32_t)f2bf(o[dt][2] * inv) | ((uint32_t)f2bf(o[dt][3] * inv) << 16);
-      *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = w;
+      w.x = (uint32_t)hv[0] | ((uint32_t)hv[1] << 16);
+      w.y = (uint32_t)hv[2] | ((uint32_t)hv[3] << 16);
+      *reinterpret_cast<uint2*>(a.out + orow + 16 * dt + 4 * g) = w;
+      if (SPLIT) {
+        uint2 lo;
+        lo.x = (uint32_t)f2bf(v[0] - bf2f(hv[0])) | ((uint32_t)f2bf(v[1] - bf2f(hv[1])) << 16);
+        lo.y = (uint32_t)f2bf(v[2] - bf2f(hv[2])) | ((uint32_t)f2bf(v[3] - bf2f(hv[3])) << 16);
+        *reinterpret_cast<uint2*>(a.out_lo + orow + 16 * dt + 4 * g) = lo;
+      }
     }
   }
   __syncthreads();
@@ -160,18 +197,26 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
   }
 }
 
-void attention(const AttnArgs& a, hipStream_t s) {
+template <bool SPLIT>
+static void attention_t(const AttnArgs& a, hipStream_t s) {
   const int per4 = a.B * a.heads * ((a.N + 63) / 64);
   if (per4 >= 240) {
     dim3 grid((a.N + 63) / 64, a.heads, a.B);
-    hipLaunchKernelGGL(attn_kernel<4>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_kernel<4, SPLIT>), grid, dim3(256), 0, s, a);
   } else if (per4 * 2 >= 240) {
     dim3 grid((a.N + 31) / 32, a.heads, a.B);
-    hipLaunchKernelGGL(attn_kernel<2>, grid, dim3(128), 0, s, a);
+    hipLaunchKernelGGL((attn_kernel<2, SPLIT>), grid, dim3(128), 0, s, a);
   } else {
     dim3 grid((a.N + 15) / 16, a.heads, a.B);
-    hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL((attn_kernel<1, SPLIT>), grid, dim3(64), 0, s, a);
   }
+}
+
+void attention(const AttnArgs& a, hipStream_t s) {
+  if (a.qkv_lo)
+    attention_t<true>(a, s);
+  else
+    attention_t<false>(a, s);
 }
 
 }  // namespace mmt

@@ -42,6 +42,7 @@ inline uint16_t host_bf16(float f) {
 
 struct LayerW {
   bf16_t *qkv_w, *proj_w, *fc1_w, *fc2_w;
+  bf16_t *qkv_wl, *proj_wl, *fc1_wl, *fc2_wl;   // low halves (fp32-faithful mode)
   float *qkv_b, *proj_b, *fc1_b, *fc2_b, *n1w, *n1b, *n2w, *n2b;
 };
 struct PromptW {
@@ -88,11 +89,12 @@ struct mmt_engine {
   LayerW lw[DEPTH];
   PromptW pw[DEPTH];
   int nprompt = 0;
-  bf16_t *pe_w = nullptr, *pep_w = nullptr;
+  bf16_t *pe_w = nullptr, *pep_w = nullptr, *pe_wl = nullptr, *pep_wl = nullptr;
   float *pe_b = nullptr, *pep_b = nullptr, *pos = nullptr, *norm_w = nullptr, *norm_b = nullptr;
-  bf16_t* hw1 = nullptr;
+  bf16_t *hw1 = nullptr, *hw1l = nullptr;
   float* hb1 = nullptr;
   bf16_t* hw[3] = {};   // conv2..4, [3 branches] contiguous
+  bf16_t* hwl[3] = {};
   float* hb[3] = {};
   float *w5 = nullptr, *b5 = nullptr, *hann = nullptr;
 
@@ -100,6 +102,10 @@ struct mmt_engine {
   void* aarena = nullptr;
   bf16_t *A_rgb = nullptr, *A_aux = nullptr, *Hn = nullptr, *QKV = nullptr, *O = nullptr, *Hm = nullptr,
          *feat = nullptr, *h1 = nullptr, *h2 = nullptr, *h3 = nullptr;
+  // low halves of every bf16 GEMM operand (fp32-faithful mode only, else null)
+  bf16_t *A_rgb_l = nullptr, *A_aux_l = nullptr, *Hn_l = nullptr, *QKV_l = nullptr, *O_l = nullptr, *Hm_l = nullptr,
+         *feat_l = nullptr, *h1_l = nullptr, *h2_l = nullptr, *h3_l = nullptr, *zero = nullptr;
+  bool split = false;
   float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *P = nullptr, *a8 = nullptr,
         *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
@@ -223,12 +229,28 @@ int upload_f32(mmt_engine* e, float** dst, const std::vector<float>& v) {
   HIPCHECK(e, hipMemcpy(*dst, v.data(), v.size() * 4, hipMemcpyHostToDevice));
   return MMT_OK;
 }
-int upload_bf16(mmt_engine* e, bf16_t** dst, const std::vector<float>& v) {
-  std::vector<uint16_t> t(v.size());
-  for (size_t i = 0; i < v.size(); ++i) t[i] = host_bf16(v[i]);
+inline float host_bf2f(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+// GEMM weight: bf16 hi part, and in fp32-faithful mode the bf16 residual lo = bf16(w - hi)
+int upload_w(mmt_engine* e, bf16_t** dst, bf16_t** dst_lo, const std::vector<float>& v) {
+  std::vector<uint16_t> t(v.size()), tl(v.size());
+  for (size_t i = 0; i < v.size(); ++i) {
+    t[i] = host_bf16(v[i]);
+    tl[i] = host_bf16(v[i] - host_bf2f(t[i]));
+  }
   *dst = walloc<bf16_t>(e, v.size());
   if (!*dst) return e->fail(MMT_E_HIP, "weight arena overflow");
   HIPCHECK(e, hipMemcpy(*dst, t.data(), t.size() * 2, hipMemcpyHostToDevice));
+  *dst_lo = nullptr;
+  if (e->split) {
+    *dst_lo = walloc<bf16_t>(e, v.size());
+    if (!*dst_lo) return e->fail(MMT_E_HIP, "weight arena overflow");
+    HIPCHECK(e, hipMemcpy(*dst_lo, tl.data(), tl.size() * 2, hipMemcpyHostToDevice));
+  }
   return MMT_OK;
 }
 
@@ -261,12 +283,12 @@ void fold_conv(mmt_engine* e, const std::string& p, int cout, int cin, std::vect
 int pack_weights(mmt_engine* e) {
   const auto& c = e->cfg;
   const bool vipt = c.model == MMT_MODEL_VIPT;
-  e->wcap = 200ull << 20;
+  e->wcap = (e->split ? 400ull : 200ull) << 20;
   HIPCHECK(e, hipMalloc(&e->warena, e->wcap));
-  TRY(upload_bf16(e, &e->pe_w, H(e, "backbone.patch_embed.proj.weight")));
+  TRY(upload_w(e, &e->pe_w, &e->pe_wl, H(e, "backbone.patch_embed.proj.weight")));
   TRY(upload_f32(e, &e->pe_b, H(e, "backbone.patch_embed.proj.bias")));
   if (vipt) {
-    TRY(upload_bf16(e, &e->pep_w, H(e, "backbone.patch_embed_prompt.proj.weight")));
+    TRY(upload_w(e, &e->pep_w, &e->pep_wl, H(e, "backbone.patch_embed_prompt.proj.weight")));
     TRY(upload_f32(e, &e->pep_b, H(e, "backbone.patch_embed_prompt.proj.bias")));
   }
   std::vector<float> pos(H(e, "backbone.pos_embed_z"));
@@ -289,13 +311,13 @@ int pack_weights(mmt_engine* e) {
   for (int i = 0; i < DEPTH; ++i) {
     const std::string p = "backbone.blocks." + std::to_string(i) + ".";
     LayerW& w = e->lw[i];
-    TRY(upload_bf16(e, &w.qkv_w, H(e, p + "attn.qkv.weight")));
+    TRY(upload_w(e, &w.qkv_w, &w.qkv_wl, H(e, p + "attn.qkv.weight")));
     TRY(upload_f32(e, &w.qkv_b, H(e, p + "attn.qkv.bias")));
-    TRY(upload_bf16(e, &w.proj_w, H(e, p + "attn.proj.weight")));
+    TRY(upload_w(e, &w.proj_w, &w.proj_wl, H(e, p + "attn.proj.weight")));
     TRY(upload_f32(e, &w.proj_b, H(e, p + "attn.proj.bias")));
-    TRY(upload_bf16(e, &w.fc1_w, H(e, p + "mlp.fc1.weight")));
+    TRY(upload_w(e, &w.fc1_w, &w.fc1_wl, H(e, p + "mlp.fc1.weight")));
     TRY(upload_f32(e, &w.fc1_b, H(e, p + "mlp.fc1.bias")));
-    TRY(upload_bf16(e, &w.fc2_w, H(e, p + "mlp.fc2.weight")));
+    TRY(upload_w(e, &w.fc2_w, &w.fc2_wl, H(e, p + "mlp.fc2.weight")));
     TRY(upload_f32(e, &w.fc2_b, H(e, p + "mlp.fc2.bias")));
     TRY(upload_f32(e, &w.n1w, H(e, p + "norm1.weight")));
     TRY(upload_f32(e, &w.n1b, H(e, p + "norm1.bias")));
@@ -312,7 +334,7 @@ int pack_weights(mmt_engine* e) {
     std::vector<float> w((size_t)3 * hc * 9 * C), b((size_t)3 * hc);
     for (int k = 0; k < 3; ++k)
       fold_conv(e, std::string("box_head.conv1_") + br[k], hc, C, w, b, (size_t)k * hc * 9 * C, (size_t)k * hc);
-    TRY(upload_bf16(e, &e->hw1, w));
+    TRY(upload_w(e, &e->hw1, &e->hw1l, w));
     TRY(upload_f32(e, &e->hb1, b));
   }
   for (int j = 2; j <= 4; ++j) {
@@ -321,7 +343,7 @@ int pack_weights(mmt_engine* e) {
     for (int k = 0; k < 3; ++k)
       fold_conv(e, std::string("box_head.conv") + std::to_string(j) + "_" + br[k], co, ci, w, b,
                 (size_t)k * co * 9 * ci, (size_t)k * co);
-    TRY(upload_bf16(e, &e->hw[j - 2], w));
+    TRY(upload_w(e, &e->hw[j - 2], &e->hwl[j - 2], w));
     TRY(upload_f32(e, &e->hb[j - 2], b));
   }
   {
@@ -359,6 +381,16 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->slot2pos, (size_t)B * Lx * 4},      {(void**)&e->gather, (size_t)B * L * 4},
       {(void**)&e->removed, (size_t)B * Lx * 4},       {(void**)&e->params_dev, (size_t)B * sizeof(CropParam)},
   };
+  reqs.push_back({(void**)&e->zero, 256});
+  if (e->split) {
+    const std::vector<Req> lo = {
+        {(void**)&e->A_rgb_l, (size_t)B * L * C * 2},   {(void**)&e->A_aux_l, (size_t)B * L * C * 2},
+        {(void**)&e->Hn_l, (size_t)B * L * C * 2},      {(void**)&e->QKV_l, (size_t)B * L * 3 * C * 2},
+        {(void**)&e->O_l, (size_t)B * L * C * 2},       {(void**)&e->Hm_l, (size_t)B * L * MLPD * 2},
+        {(void**)&e->feat_l, (size_t)B * Lx * C * 2},   {(void**)&e->h1_l, (size_t)B * Lx * 3 * hc * 2},
+        {(void**)&e->h2_l, (size_t)B * Lx * 3 * (hc / 2) * 2}, {(void**)&e->h3_l, (size_t)B * Lx * 3 * (hc / 4) * 2}};
+    reqs.insert(reqs.end(), lo.begin(), lo.end());
+  }
   if (e->cfg.debug_outputs) {
     reqs.push_back({(void**)&e->dbg_patch, (size_t)B * S * S * Cin});
     reqs.push_back({(void**)&e->dbg_maps, (size_t)B * 5 * Lx * 4});
@@ -441,11 +473,14 @@ void probe_collect(mmt_engine* e) {
 }
 
 // ---------------------------------------------------------------- the per-frame launch sequence
-GemmArgs dense(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, const float* bias, void* Cp, int64_t ldc,
-               const float* R, int64_t ldr, int M, int N, int K) {
+GemmArgs dense(mmt_engine* e, const bf16_t* A, const bf16_t* Al, int64_t lda, const bf16_t* W, const bf16_t* Wl,
+               int64_t ldw, const float* bias, void* Cp, void* Cl, int64_t ldc, const float* R, int64_t ldr, int M,
+               int N, int K) {
   GemmArgs a{};
-  a.g[0] = GemmGroup{A, lda, W, ldw, bias, Cp, ldc, R, ldr};
+  a.g[0] = GemmGroup{A, Al, lda, W, Wl, ldw, bias, Cp, Cl, ldc, R, ldr};
   a.groups = 1;
+  a.split = e->split ? 1 : 0;
+  a.zero = e->zero;
   a.M = M;
   a.N = N;
   a.K = K;
@@ -461,6 +496,12 @@ void run_gemm(mmt_engine* e, const char* cls, const GemmArgs& a, int epi) {
   probe_end(e, cls);
 }
 
+// offset a possibly-null low-half pointer
+template <class T>
+inline T* off(T* p, size_t o) {
+  return p ? p + o : nullptr;
+}
+
 void enqueue_forward(mmt_engine* e, int b0, int n) {
   const auto& c = e->cfg;
   hipStream_t s = e->stream;
@@ -470,6 +511,8 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
   const bool deep = vipt && c.prompt_type == MMT_PROMPT_DEEP;
   bf16_t* A_rgb = e->A_rgb + (size_t)b0 * L * C;
   bf16_t* A_aux = e->A_aux + (size_t)b0 * L * C;
+  bf16_t* A_rgb_l = off(e->A_rgb_l, (size_t)b0 * L * C);
+  bf16_t* A_aux_l = off(e->A_aux_l, (size_t)b0 * L * C);
 
   // 1. crop + normalise + patchify the search region of every sequence
   CropArgs ca{};
@@ -479,6 +522,8 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
   ca.C = c.in_chans;
   ca.A_rgb = A_rgb;
   ca.A_aux = A_aux;
+  ca.A_rgb_lo = A_rgb_l;
+  ca.A_aux_lo = A_aux_l;
   ca.rows_per_seq = L;
   ca.row0 = Lz;
   ca.dbg_patch = e->dbg_patch;
@@ -488,12 +533,13 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
   float* X = e->X;
   float* X2 = e->X2;
   if (vipt) {
-    GemmArgs g = dense(A_rgb, C, e->pe_w, C, e->pe_b, e->tok_rgb, C, nullptr, 0, n * L, C, C);
-    g.g[1] = GemmGroup{A_aux, C, e->pep_w, C, e->pep_b, e->tok_aux, C, nullptr, 0};
+    GemmArgs g = dense(e, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, e->tok_rgb, nullptr, C, nullptr, 0,
+                       n * L, C, C);
+    g.g[1] = GemmGroup{A_aux, A_aux_l, C, e->pep_w, e->pep_wl, C, e->pep_b, e->tok_aux, nullptr, C, nullptr, 0};
     g.groups = 2;
     run_gemm(e, "patch", g, EPI_F32);
   } else {
-    GemmArgs g = dense(A_rgb, C, e->pe_w, C, e->pe_b, X, C, e->pos, C, n * L, C, C);
+    GemmArgs g = dense(e, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, X, nullptr, C, e->pos, C, n * L, C, C);
     g.pos_rows = L;
     run_gemm(e, "patch", g, EPI_POS_F32);
   }
@@ -506,23 +552,26 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
   pa.a8 = e->a8;
   pa.c8 = e->c8;
   pa.P = e->P;
+  auto set_prompt = [&](int i, int lnA) {
+    pa.layer = i;
+    pa.lnA_w = e->pw[lnA].nw;
+    pa.lnA_b = e->pw[lnA].nb;
+    pa.lnB_w = e->pw[i].nw;
+    pa.lnB_b = e->pw[i].nb;
+    pa.w00 = e->pw[i].w00;
+    pa.b00 = e->pw[i].b00;
+    pa.w01 = e->pw[i].w01;
+    pa.b01 = e->pw[i].b01;
+    pa.w1 = e->pw[i].w1;
+    pa.b1 = e->pw[i].b1;
+    pa.smooth = e->pw[i].smooth;
+  };
   if (prompted) {  // layer-0 prompt: vit_ce_prompt.py:205-219
-    pa.layer = 0;
+    set_prompt(0, 0);
     pa.srcA = e->tok_rgb;
     pa.srcA_rows = L;
     pa.srcB = e->tok_aux;
     pa.slot2pos = nullptr;
-    pa.lnA_w = e->pw[0].nw;
-    pa.lnA_b = e->pw[0].nb;
-    pa.lnB_w = e->pw[0].nw;
-    pa.lnB_b = e->pw[0].nb;
-    pa.w00 = e->pw[0].w00;
-    pa.b00 = e->pw[0].b00;
-    pa.w01 = e->pw[0].w01;
-    pa.b01 = e->pw[0].b01;
-    pa.w1 = e->pw[0].w1;
-    pa.b1 = e->pw[0].b1;
-    pa.smooth = e->pw[0].smooth;
     pa.X = X;
     pa.X_rows = L;
     pa.tok_rgb = e->tok_rgb;
@@ -539,33 +588,27 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
     const LayerW& w = e->lw[i];
     const int Na = Lz + Ls;
     if (deep && i >= 1) {  // vit_ce_prompt.py:268-310
-      pa.layer = i;
+      set_prompt(i, i - 1);
       pa.srcA = X;
       pa.srcA_rows = Na;
       pa.srcB = e->P;
       pa.slot2pos = e->slot2pos;
-      pa.lnA_w = e->pw[i - 1].nw;
-      pa.lnA_b = e->pw[i - 1].nb;
-      pa.lnB_w = e->pw[i].nw;
-      pa.lnB_b = e->pw[i].nb;
-      pa.w00 = e->pw[i].w00;
-      pa.b00 = e->pw[i].b00;
-      pa.w01 = e->pw[i].w01;
-      pa.b01 = e->pw[i].b01;
-      pa.w1 = e->pw[i].w1;
-      pa.b1 = e->pw[i].b1;
-      pa.smooth = e->pw[i].smooth;
       pa.X = X;
       pa.X_rows = Na;
       prompt_reduce(pa, s);
       prompt_expand(pa, s);
     }
-    layernorm(X, w.n1w, w.n1b, e->Hn, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
-    run_gemm(e, "qkv", dense(e->Hn, C, w.qkv_w, C, w.qkv_b, e->QKV, 3 * C, nullptr, 0, n * Na, 3 * C, C), EPI_BF16);
+    layernorm(X, w.n1w, w.n1b, e->Hn, e->Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+    run_gemm(e, "qkv",
+             dense(e, e->Hn, e->Hn_l, C, w.qkv_w, w.qkv_wl, C, w.qkv_b, e->QKV, e->QKV_l, 3 * C, nullptr, 0, n * Na,
+                   3 * C, C),
+             EPI_BF16);
     const bool ce = e->keep_at[i] != e->ls_before[i];
     AttnArgs aa{};
     aa.qkv = e->QKV;
+    aa.qkv_lo = e->QKV_l;
     aa.out = e->O;
+    aa.out_lo = e->O_l;
     aa.B = n;
     aa.N = Na;
     aa.heads = HEADS;
@@ -575,7 +618,9 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
     probe_begin(e, "attn", 4.0 * n * HEADS * (double)Na * Na * 64, (double)n * Na * 4 * C * 2);
     attention(aa, s);
     probe_end(e, "attn");
-    run_gemm(e, "proj", dense(e->O, C, w.proj_w, C, w.proj_b, X, C, X, C, n * Na, C, C), EPI_RESID_F32);
+    run_gemm(e, "proj",
+             dense(e, e->O, e->O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
+             EPI_RESID_F32);
     if (ce) {  // attn_blocks.py:99-101
       const int keep = e->keep_at[i];
       CEArgs ce_a{};
@@ -596,27 +641,27 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       removed_off += Ls - keep;
       std::swap(gin, gout);
       Ls = keep;
-      layernorm(X, w.n2w, w.n2b, e->Hn, nullptr, n * (Lz + Ls), Lz + Ls, e->gather, Na, X2, s);
+      layernorm(X, w.n2w, w.n2b, e->Hn, e->Hn_l, nullptr, n * (Lz + Ls), Lz + Ls, e->gather, Na, X2, s);
       std::swap(X, X2);
     } else {
-      layernorm(X, w.n2w, w.n2b, e->Hn, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+      layernorm(X, w.n2w, w.n2b, e->Hn, e->Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
     }
     const int Nm = Lz + Ls;
-    run_gemm(e, "fc1", dense(e->Hn, C, w.fc1_w, C, w.fc1_b, e->Hm, MLPD, nullptr, 0, n * Nm, MLPD, C),
+    run_gemm(e, "fc1",
+             dense(e, e->Hn, e->Hn_l, C, w.fc1_w, w.fc1_wl, C, w.fc1_b, e->Hm, e->Hm_l, MLPD, nullptr, 0, n * Nm, MLPD,
+                   C),
              EPI_GELU_BF16);
-    run_gemm(e, "fc2", dense(e->Hm, MLPD, w.fc2_w, MLPD, w.fc2_b, X, C, X, C, n * Nm, C, MLPD), EPI_RESID_F32);
+    run_gemm(e, "fc2",
+             dense(e, e->Hm, e->Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C, n * Nm, C, MLPD),
+             EPI_RESID_F32);
   }
-  final_norm_recover(X, Lz + Ls, e->slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, e->feat, e->dbg_feat, s);
+  final_norm_recover(X, Lz + Ls, e->slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, e->feat, e->feat_l, e->dbg_feat, s);
 
   // CENTER head: conv1 of the three branches fused (N = 3*hc), then per-branch grouped convs
   const int hc = c.head_channels, fs = e->fs, M = n * Lx;
   {
-    GemmArgs g{};
-    g.g[0] = GemmGroup{e->feat, C, e->hw1, 9 * C, e->hb1, e->h1, 3 * hc, nullptr, 0};
-    g.groups = 1;
-    g.M = M;
-    g.N = 3 * hc;
-    g.K = 9 * C;
+    GemmArgs g = dense(e, e->feat, e->feat_l, C, e->hw1, e->hw1l, 9 * C, e->hb1, e->h1, e->h1_l, 3 * hc, nullptr, 0,
+                       M, 3 * hc, 9 * C);
     g.amode = A_CONV3;
     g.conv_hw = fs;
     g.conv_cin = C;
@@ -625,25 +670,35 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
   const int ch[4] = {hc, hc / 2, hc / 4, hc / 8};
   for (int j = 0; j < 3; ++j) {   // conv2, conv3, conv4
     const int ci = ch[j], co = ch[j + 1];
-    GemmArgs g{};
+    GemmArgs g = dense(e, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, M, co,
+                       9 * ci);
     for (int k = 0; k < 3; ++k) {
-      const bf16_t* A;
+      const bf16_t *A, *Al;
       int64_t lda;
       if (j == 0) {
         A = e->h1 + k * hc;
+        Al = off(e->h1_l, (size_t)k * hc);
         lda = 3 * hc;
       } else {
         A = (j == 1 ? e->h2 : e->h3) + (size_t)k * M * ci;
+        Al = off(j == 1 ? e->h2_l : e->h3_l, (size_t)k * M * ci);
         lda = ci;
       }
-      void* Cout = j == 0 ? (void*)(e->h2 + (size_t)k * M * co)
-                          : (j == 1 ? (void*)(e->h3 + (size_t)k * M * co) : (void*)(e->h4 + (size_t)k * M * co));
-      g.g[k] = GemmGroup{A, lda, e->hw[j] + (size_t)k * co * 9 * ci, 9 * ci, e->hb[j] + k * co, Cout, co, nullptr, 0};
+      void *Cout, *Cl;
+      if (j == 0) {
+        Cout = e->h2 + (size_t)k * M * co;
+        Cl = off(e->h2_l, (size_t)k * M * co);
+      } else if (j == 1) {
+        Cout = e->h3 + (size_t)k * M * co;
+        Cl = off(e->h3_l, (size_t)k * M * co);
+      } else {
+        Cout = e->h4 + (size_t)k * M * co;
+        Cl = nullptr;
+      }
+      g.g[k] = GemmGroup{A, Al, lda, e->hw[j] + (size_t)k * co * 9 * ci, off(e->hwl[j], (size_t)k * co * 9 * ci),
+                         9 * ci, e->hb[j] + k * co, Cout, Cl, co, nullptr, 0};
     }
     g.groups = 3;
-    g.M = M;
-    g.N = co;
-    g.K = 9 * ci;
     g.amode = A_CONV3;
     g.conv_hw = fs;
     g.conv_cin = ci;
@@ -791,6 +846,8 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   e->fs = c.search_size / 16;
   e->tfs = c.template_size / 16;
   if (e->L > 1024 || (c.n_ce > 0 && (c.ce_template_index < 0 || c.ce_template_index >= e->Lz))) return MMT_E_ARG;
+  if (c.precision < 0 || c.precision > 1) return MMT_E_ARG;
+  e->split = c.precision == 1;
   e->nprompt = c.model == MMT_MODEL_VIPT ? (c.prompt_type == MMT_PROMPT_DEEP ? DEPTH : (c.prompt_type ? 1 : 0)) : 0;
   int Ls = e->Lx;
   for (int i = 0; i < DEPTH; ++i) {
@@ -911,6 +968,8 @@ int mmt_initialize(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww
   ca.C = e->cfg.in_chans;
   ca.A_rgb = e->A_rgb + (size_t)slot * e->L * C;
   ca.A_aux = e->A_aux + (size_t)slot * e->L * C;
+  ca.A_rgb_lo = off(e->A_rgb_l, (size_t)slot * e->L * C);
+  ca.A_aux_lo = off(e->A_aux_l, (size_t)slot * e->L * C);
   ca.rows_per_seq = e->L;
   ca.row0 = 0;
   ca.dbg_patch = nullptr;
@@ -1051,9 +1110,12 @@ int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const fl
   if ((epi == EPI_RESID_F32 || epi == EPI_POS_F32) && !R) return MMT_E_ARG;
   if (conv_hw > 0 && (conv_cin % 64 || K != 9 * conv_cin || (epi != EPI_RELU_BF16 && epi != EPI_RELU_F32)))
     return MMT_E_ARG;
+  static bf16_t* zero = nullptr;
+  if (!zero && hipMalloc(&zero, 256) == hipSuccess) hipMemset(zero, 0, 256);
   GemmArgs a{};
-  a.g[0] = GemmGroup{(const bf16_t*)A, lda, (const bf16_t*)W, ldw, bias, Cp, ldc, R, ldr};
+  a.g[0] = GemmGroup{(const bf16_t*)A, nullptr, lda, (const bf16_t*)W, nullptr, ldw, bias, Cp, nullptr, ldc, R, ldr};
   a.groups = 1;
+  a.zero = zero;
   a.M = M;
   a.N = N;
   a.K = K;
@@ -1071,7 +1133,9 @@ int mmt_op_attention(const void* qkv, void* out, int B, int N, int heads, int ce
   if (ce_query >= 0 && (!ce_prob || ce_lens_t < 0 || ce_lens_t >= N || ce_query >= N)) return MMT_E_ARG;
   AttnArgs a{};
   a.qkv = (const bf16_t*)qkv;
+  a.qkv_lo = nullptr;
   a.out = (bf16_t*)out;
+  a.out_lo = nullptr;
   a.B = B;
   a.N = N;
   a.heads = heads;
@@ -1085,7 +1149,7 @@ int mmt_op_attention(const void* qkv, void* out, int B, int N, int heads, int ce
 int mmt_op_layernorm(const float* x, const float* w, const float* b, void* out_bf16, float* out_f32, int rows,
                      void* stream) {
   if (!x || !w || !b || rows <= 0 || (!out_bf16 && !out_f32)) return MMT_E_ARG;
-  layernorm(x, w, b, (bf16_t*)out_bf16, out_f32, rows, rows, nullptr, rows, nullptr, (hipStream_t)stream);
+  layernorm(x, w, b, (bf16_t*)out_bf16, nullptr, out_f32, rows, rows, nullptr, rows, nullptr, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 

@@ -2,90 +2,132 @@
 //
 //   C[m][n] = epi( sum_k A[m][k] * W[n][k] + bias[n] )
 //
-// The ViT-B dense contractions of the tracking path (attn.py:17-19 qkv/proj,
-// timm Mlp fc1/fc2, patch_embed.py:20 as a k16s16 conv, head.py:8-21 3x3 convs
-// as implicit GEMMs over the NHWC token map) all have this shape: activations
-// [tokens x K] and nn.Linear / conv weights [out x K], both K-contiguous.
+// The dense contractions of the tracking path (attn.py:17-19 qkv/proj, timm Mlp fc1/fc2,
+// patch_embed.py:20 as a k16s16 conv, head.py:8-21 3x3 convs as implicit GEMMs over the NHWC
+// token map) all have this shape: activations [tokens x K] and weights [out x K], K-contiguous.
 //
-// Tile: BM x BN x 64, 256 threads = 4 waves, v_mfma_f32_16x16x32_bf16.
-// LDS: two buffers of (BM+BN) x 64 bf16, 16-B chunks XOR-swizzled by row
-// (chunk ^ (row & 7)) so both the 8-lane ds_write_b128 groups and the
-// 16-lane ds_read_b128 fragment groups are conflict-free.  Global->register
-// staging of tile k+1 overlaps the MFMAs of tile k; one barrier per K-tile.
-// The MFMA is issued as W-fragment x A-fragment so each lane ends with four
-// consecutive output columns of one row: 8-B (bf16) / 16-B (fp32) stores.
+// * tiles BM x BN x 64; 4 or 8 waves, each a 64x64 (or smaller) block of v_mfma_f32_16x16x32_bf16;
+// * operands move HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR staging); each wave-
+//   instruction fills 8 LDS rows of 128 B; the 16-B chunks are XOR-swizzled by row (chunk ^ (row&7))
+//   by pre-swizzling the per-lane SOURCE address, so the fragment ds_read_b128s are conflict-free;
+// * two LDS stages: the loads of K-tile k+1 are in flight while tile k is multiplied;
+// * XCD-aware tile order: blocks that share an XCD (b % 8) get a compact rectangle of output tiles
+//   (a few W column tiles x all A rows, or an A row slice x all W tiles), so the L2 of each XCD
+//   serves the re-reads;
+// * SPLIT (fp32-faithful "bf16x3" mode): A = Ah + Al, W = Wh + Wl as bf16 pairs,
+//   acc += Wh*Ah + Wl*Ah + Wh*Al  (relative error ~1e-5, vs ~2e-3 for plain bf16);
+// * the MFMA is issued W-fragment x A-fragment, so a lane ends with 4 consecutive output columns
+//   of one row: 8-B (bf16) / 16-B (fp32) epilogue stores.
 #include "kernels.h"
 
 namespace mmt {
 
-template <int BM, int BN, int WM, int WN>
-struct TileCfg {
-  static constexpr int WN_WAVES = BN / WN;
-  static constexpr int WM_WAVES = BM / WM;
-  static_assert(WM_WAVES * WN_WAVES == 4, "tile must map onto 4 waves");
-  static constexpr int FM = WM / 16;
-  static constexpr int FN = WN / 16;
-  static constexpr int ACH = BM * 8 / 256;  // 16-B chunks per thread per A tile
-  static constexpr int BCH = BN * 8 / 256;
-  static_assert(ACH >= 1 && BCH >= 1, "tile too small");
-};
-
 __device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((c ^ (r & 7)) << 3); }
 
-template <int BM, int BN, int WM, int WN, int EPI, int AM>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
-  using T = TileCfg<BM, BN, WM, WN>;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * 64];
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
 
-  const GemmGroup g = args.g[blockIdx.z];
+template <int BM, int BN, int WMW, int WNW, bool SPLIT>
+struct Tile {
+  static constexpr int NW = WMW * WNW;
+  static constexpr int NT = NW * 64;
+  static constexpr int WM = BM / WMW, WN = BN / WNW;
+  static constexpr int FM = WM / 16, FN = WN / 16;
+  static constexpr int AROWS = SPLIT ? 2 * BM : BM;
+  static constexpr int ROWS = AROWS + (SPLIT ? 2 * BN : BN);
+  static constexpr int GROUPS = ROWS / 8;           // 8 rows per wave-instruction
+  static constexpr int STAGE = ROWS * 64;           // bf16 elements per stage
+  static_assert(GROUPS % NW == 0, "row groups must divide over waves");
+};
+
+// logical tile id -> (tm, tn): column-group-major with Wc tile columns per group, tm-major inside
+__device__ __forceinline__ void tile_of(int id, int tiles_m, int tiles_n, int wc, int& tm, int& tn) {
+  const int per = tiles_m * wc;
+  const int grp = id / per, rem = id - grp * per;
+  const int width = min(wc, tiles_n - grp * wc);
+  tm = rem / width;
+  tn = grp * wc + (rem - tm * width);
+}
+
+template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT>
+__global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args) {
+  using T = Tile<BM, BN, WMW, WNW, SPLIT>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * T::STAGE];
+
+  const GemmGroup& g = args.g[blockIdx.z];
   const int M = args.M, N = args.N, K = args.K;
-  const int tiles_n = N / BN;
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN, ntiles = tiles_m * tiles_n;
+  // XCD-aware remap (bijective): blocks b, b+8, ... (one XCD) take a contiguous logical range
+  const int b = blockIdx.x, x = b & 7, j = b >> 3;
+  const int q = ntiles >> 3, r8 = ntiles & 7;
+  const int id = (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + j;
+  int tm, tn;
+  tile_of(id, tiles_m, tiles_n, args.wc, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / T::WN_WAVES, wn = wave % T::WN_WAVES;
+  const int wm = wave / WNW, wn = wave % WNW;
 
-  uint4 ra[T::ACH], rb[T::BCH];
-
-  auto load = [&](int k0) {
+  // ---- per-lane source rows of this wave's load groups (fixed over K)
+  constexpr int GPW = T::GROUPS / T::NW;
+  const bf16_t* src[GPW];
+  int64_t conv_pix[GPW];   // A_CONV3: base pixel row (b*plane + y*hw + x) or -1, y/x packed
+  int conv_yx[GPW];
 #pragma unroll
-    for (int i = 0; i < T::ACH; ++i) {
-      const int q = tid + 256 * i, r = q >> 3, c = q & 7;
-      const int m = m0 + r;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (AM == A_DENSE) {
-        if (m < M) v = *reinterpret_cast<const uint4*>(g.A + (int64_t)m * g.lda + k0 + c * 8);
-      } else {
-        // implicit 3x3 conv, pad 1, NHWC: k = tap * cin + ch (cin % 64 == 0 -> one tap per K-tile)
-        const int hw = args.conv_hw, cin = args.conv_cin;
-        const int tap = k0 / cin, ch = k0 - tap * cin;
-        const int ky = tap / 3, kx = tap - ky * 3;
-        const int plane = hw * hw;
-        const int bimg = m / plane, p = m - bimg * plane;
-        const int y = p / hw + ky - 1, x = p - (p / hw) * hw + kx - 1;
-        if (m < M && y >= 0 && y < hw && x >= 0 && x < hw)
-          v = *reinterpret_cast<const uint4*>(g.A + ((int64_t)bimg * plane + y * hw + x) * g.lda + ch + c * 8);
+  for (int i = 0; i < GPW; ++i) {
+    const int grp = wave + i * T::NW;
+    const int row = grp * 8 + (lane >> 3);
+    const bf16_t* p = args.zero;
+    conv_pix[i] = -1;
+    conv_yx[i] = 0;
+    if (row < T::AROWS) {
+      const int lr = SPLIT ? (row % BM) : row;
+      const bool lo = SPLIT && row >= BM;
+      const int m = m0 + lr;
+      if (m < M) {
+        if (AM == A_DENSE) {
+          p = (lo ? g.A_lo : g.A) + (int64_t)m * g.lda;
+        } else {
+          const int hw = args.conv_hw, plane = hw * hw;
+          const int bi = m / plane, pp = m - bi * plane;
+          const int y = pp / hw, xx = pp - y * hw;
+          conv_pix[i] = (int64_t)bi * plane;
+          conv_yx[i] = (y << 16) | xx;
+          p = lo ? g.A_lo : g.A;
+        }
       }
-      ra[i] = v;
+    } else {
+      const int wr = row - T::AROWS;
+      const int lr = SPLIT ? (wr % BN) : wr;
+      const bool lo = SPLIT && wr >= BN;
+      p = (lo ? g.W_lo : g.W) + (int64_t)(n0 + lr) * g.ldw;
     }
+    src[i] = p;
+  }
+
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * 64;
+    bf16_t* sbase = smem + stage * T::STAGE;
 #pragma unroll
-    for (int i = 0; i < T::BCH; ++i) {
-      const int q = tid + 256 * i, r = q >> 3, c = q & 7;
-      rb[i] = *reinterpret_cast<const uint4*>(g.W + (int64_t)(n0 + r) * g.ldw + k0 + c * 8);
-    }
-  };
-  auto store = [&](int buf) {
-    bf16_t* As = smem + buf * (BM + BN) * 64;
-    bf16_t* Bs = As + BM * 64;
-#pragma unroll
-    for (int i = 0; i < T::ACH; ++i) {
-      const int q = tid + 256 * i;
-      *reinterpret_cast<uint4*>(As + swz(q >> 3, q & 7)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < T::BCH; ++i) {
-      const int q = tid + 256 * i;
-      *reinterpret_cast<uint4*>(Bs + swz(q >> 3, q & 7)) = rb[i];
+    for (int i = 0; i < GPW; ++i) {
+      const int grp = wave + i * T::NW;
+      const int row = grp * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (row & 7);
+      const bf16_t* p = src[i];
+      if (p != args.zero) {
+        if (AM == A_CONV3 && row < T::AROWS) {
+          const int hw = args.conv_hw, cin = args.conv_cin;
+          const int tap = k0 / cin, ch = k0 - tap * cin;
+          const int ky = tap / 3, kx = tap - ky * 3;
+          const int y = (conv_yx[i] >> 16) + ky - 1, xx = (conv_yx[i] & 0xffff) + kx - 1;
+          if (y >= 0 && y < hw && xx >= 0 && xx < hw)
+            p = p + (conv_pix[i] + y * hw + xx) * g.lda + ch + c * 8;
+          else
+            p = args.zero;
+        } else {
+          p = p + k0 + c * 8;
+        }
+      }
+      __builtin_amdgcn_global_load_lds((gptr_t)p, (lptr_t)(sbase + grp * 8 * 64), 16, 0, 0);
     }
   };
 
@@ -93,113 +135,150 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
   for (int i = 0; i < T::FM; ++i)
 #pragma unroll
-    for (int j = 0; j < T::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int jj = 0; jj < T::FN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
-    const bf16_t* As = smem + buf * (BM + BN) * 64;
-    const bf16_t* Bs = As + BM * 64;
+  auto compute = [&](int stage) {
+    const bf16_t* S = smem + stage * T::STAGE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = 4 * s + (lane >> 4);
-      bf16x8 af[T::FM], bw[T::FN];
+      bf16x8 ah[T::FM], bh[T::FN];
+      bf16x8 al[SPLIT ? T::FM : 1], bl[SPLIT ? T::FN : 1];
+#pragma unroll
+      for (int i = 0; i < T::FM; ++i) {
+        const int row = wm * T::WM + i * 16 + (lane & 15);
+        ah[i] = *reinterpret_cast<const bf16x8*>(S + swz(row, c));
+        if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(S + swz(BM + row, c));
+      }
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj) {
+        const int row = T::AROWS + wn * T::WN + jj * 16 + (lane & 15);
+        bh[jj] = *reinterpret_cast<const bf16x8*>(S + swz(row, c));
+        if (SPLIT) bl[jj] = *reinterpret_cast<const bf16x8*>(S + swz(BN + row, c));
+      }
 #pragma unroll
       for (int i = 0; i < T::FM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WM + i * 16 + (lane & 15), c));
 #pragma unroll
-      for (int j = 0; j < T::FN; ++j)
-        bw[j] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WN + j * 16 + (lane & 15), c));
-#pragma unroll
-      for (int i = 0; i < T::FM; ++i)
-#pragma unroll
-        for (int j = 0; j < T::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+        for (int jj = 0; jj < T::FN; ++jj) {
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[jj], ah[i], acc[i][jj], 0, 0, 0);
+          if (SPLIT) {
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[jj], ah[i], acc[i][jj], 0, 0, 0);
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[jj], al[i], acc[i][jj], 0, 0, 0);
+          }
+        }
     }
   };
 
   const int nk = K / 64;
-  load(0);
-  store(0);
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load((kt + 1) * 64);
-    compute(cur);
-    if (kt + 1 < nk) store(cur ^ 1);
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    compute(kt & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  // epilogue: lane owns C[m][n..n+3]
+  // ---- epilogue: lane owns C[m][n..n+3]
 #pragma unroll
   for (int i = 0; i < T::FM; ++i) {
-    const int m = m0 + wm * WM + i * 16 + (lane & 15);
+    const int m = m0 + wm * T::WM + i * 16 + (lane & 15);
     if (m >= M) continue;
 #pragma unroll
-    for (int j = 0; j < T::FN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-      float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-      float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z, v3 = acc[i][j][3] + bv.w;
-      if (EPI == EPI_GELU_BF16) {
-        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
-      }
-      if (EPI == EPI_RELU_BF16 || EPI == EPI_RELU_F32) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
+    for (int jj = 0; jj < T::FN; ++jj) {
+      const int n = n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4;
+      const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float v[4] = {acc[i][jj][0] + bv.x, acc[i][jj][1] + bv.y, acc[i][jj][2] + bv.z, acc[i][jj][3] + bv.w};
+      if (EPI == EPI_GELU_BF16)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+      if (EPI == EPI_RELU_BF16 || EPI == EPI_RELU_F32)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      const int64_t off = (int64_t)m * g.ldc + n;
       if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
+        bf16_t h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = f2bf(v[e]);
         uint2 o;
-        o.x = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
-        o.y = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C) + (int64_t)m * g.ldc + n) = o;
-      } else {
-        float4 o = make_float4(v0, v1, v2, v3);
-        if (EPI == EPI_RESID_F32) {
-          const float4 r = *reinterpret_cast<const float4*>(g.R + (int64_t)m * g.ldr + n);
-          o = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
-        } else if (EPI == EPI_POS_F32) {
-          const float4 r = *reinterpret_cast<const float4*>(g.R + (int64_t)(m % args.pos_rows) * g.ldr + n);
-          o = make_float4(v0 + r.x, v1 + r.y, v2 + r.z, v3 + r.w);
+        o.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+        o.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C) + off) = o;
+        if (SPLIT && g.C_lo) {
+          uint2 lo;
+          lo.x = (uint32_t)f2bf(v[0] - bf2f(h[0])) | ((uint32_t)f2bf(v[1] - bf2f(h[1])) << 16);
+          lo.y = (uint32_t)f2bf(v[2] - bf2f(h[2])) | ((uint32_t)f2bf(v[3] - bf2f(h[3])) << 16);
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C_lo) + off) = lo;
         }
-        *reinterpret_cast<float4*>(static_cast<float*>(g.C) + (int64_t)m * g.ldc + n) = o;
+      } else {
+        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+        if (EPI == EPI_RESID_F32) {
+          const float4 rr = *reinterpret_cast<const float4*>(g.R + (int64_t)m * g.ldr + n);
+          o = make_float4(rr.x + v[0], rr.y + v[1], rr.z + v[2], rr.w + v[3]);
+        } else if (EPI == EPI_POS_F32) {
+          const float4 rr = *reinterpret_cast<const float4*>(g.R + (int64_t)(m % args.pos_rows) * g.ldr + n);
+          o = make_float4(v[0] + rr.x, v[1] + rr.y, v[2] + rr.z, v[3] + rr.w);
+        }
+        *reinterpret_cast<float4*>(static_cast<float*>(g.C) + off) = o;
       }
     }
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int AM>
-static void launch_one(const GemmArgs& a, hipStream_t s) {
-  dim3 grid(((a.M + BM - 1) / BM) * (a.N / BN), 1, a.groups);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, EPI, AM>), grid, dim3(256), 0, s, a);
+template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT>
+static void launch_one(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.N / BN;
+  // column-group width: ~tiles_n/8 columns per XCD when there are enough W tiles, else whole rows
+  int wc = tiles_n;
+  if (tiles_n >= 8) {
+    wc = tiles_n / 8;
+    while (tiles_n % wc) --wc;
+  }
+  a.wc = wc;
+  dim3 grid(tiles_m * tiles_n, 1, a.groups);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI, AM, SPLIT>), grid, dim3(WMW * WNW * 64), 0, s, a);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WMW, int WNW, bool SPLIT>
 static void launch_cfg(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.amode == A_CONV3) {
-    switch (epi) {
-      case EPI_RELU_BF16: return launch_one<BM, BN, WM, WN, EPI_RELU_BF16, A_CONV3>(a, s);
-      case EPI_RELU_F32: return launch_one<BM, BN, WM, WN, EPI_RELU_F32, A_CONV3>(a, s);
-      default: break;
-    }
+    if (epi == EPI_RELU_BF16) return launch_one<BM, BN, WMW, WNW, EPI_RELU_BF16, A_CONV3, SPLIT>(a, s);
+    if (epi == EPI_RELU_F32) return launch_one<BM, BN, WMW, WNW, EPI_RELU_F32, A_CONV3, SPLIT>(a, s);
     return;
   }
   switch (epi) {
-    case EPI_BF16: return launch_one<BM, BN, WM, WN, EPI_BF16, A_DENSE>(a, s);
-    case EPI_GELU_BF16: return launch_one<BM, BN, WM, WN, EPI_GELU_BF16, A_DENSE>(a, s);
-    case EPI_RESID_F32: return launch_one<BM, BN, WM, WN, EPI_RESID_F32, A_DENSE>(a, s);
-    case EPI_F32: return launch_one<BM, BN, WM, WN, EPI_F32, A_DENSE>(a, s);
-    case EPI_POS_F32: return launch_one<BM, BN, WM, WN, EPI_POS_F32, A_DENSE>(a, s);
+    case EPI_BF16: return launch_one<BM, BN, WMW, WNW, EPI_BF16, A_DENSE, SPLIT>(a, s);
+    case EPI_GELU_BF16: return launch_one<BM, BN, WMW, WNW, EPI_GELU_BF16, A_DENSE, SPLIT>(a, s);
+    case EPI_RESID_F32: return launch_one<BM, BN, WMW, WNW, EPI_RESID_F32, A_DENSE, SPLIT>(a, s);
+    case EPI_F32: return launch_one<BM, BN, WMW, WNW, EPI_F32, A_DENSE, SPLIT>(a, s);
+    case EPI_POS_F32: return launch_one<BM, BN, WMW, WNW, EPI_POS_F32, A_DENSE, SPLIT>(a, s);
     default: break;
   }
 }
 
+template <bool SPLIT>
+static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
+  const int target = 200;   // aim for at least ~one tile per CU of the 256
+  const int t256 = (a.M + 255) / 256, t128 = (a.M + 127) / 128, t64 = (a.M + 63) / 64;
+  if constexpr (!SPLIT) {
+    if (a.N % 128 == 0 && t256 * (a.N / 128) * a.groups >= target) return launch_cfg<256, 128, 4, 2, false>(a, epi, s);
+  }
+  if (a.N % 128 == 0 && t128 * (a.N / 128) * a.groups >= target) return launch_cfg<128, 128, 2, 2, SPLIT>(a, epi, s);
+  if (a.N % 64 == 0) {
+    if (t128 * (a.N / 64) * a.groups >= target) return launch_cfg<128, 64, 2, 2, SPLIT>(a, epi, s);
+    return launch_cfg<64, 64, 2, 2, SPLIT>(a, epi, s);
+  }
+  if (t64 * (a.N / 32) * a.groups >= target) return launch_cfg<64, 32, 4, 1, SPLIT>(a, epi, s);
+  return launch_cfg<32, 32, 2, 1, SPLIT>(a, epi, s);
+}
+
 void gemm(const GemmArgs& a, int epi, hipStream_t s) {
-  const int mt128 = (a.M + 127) / 128, mt64 = (a.M + 63) / 64;
-  const int target = 240;  // >= ~1 tile per CU of the 256
-  if (a.N % 128 == 0 && mt128 * (a.N / 128) * a.groups >= target)
-    return launch_cfg<128, 128, 64, 64>(a, epi, s);
-  if (a.N % 128 == 0 && mt64 * (a.N / 128) * a.groups >= target)
-    return launch_cfg<64, 128, 32, 64>(a, epi, s);
-  if (a.N % 64 == 0)
-    return launch_cfg<64, 64, 32, 32>(a, epi, s);
-  return launch_cfg<64, 32, 16, 32>(a, epi, s);
+  if (a.split)
+    gemm_dispatch<true>(a, epi, s);
+  else
+    gemm_dispatch<false>(a, epi, s);
 }
 
 }  // namespace mmt

@@ -66,8 +66,11 @@ __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
   const int64_t rowoff = ((int64_t)b * a.rows_per_seq + a.row0 + patch) * 768;
   for (int c = 0; c < a.C; ++c) {
     const float t = ((float)u8[c] / 255.0f - kMean[c]) / kStd[c];
-    bf16_t* dst = (c < 3 ? a.A_rgb : a.A_aux) + rowoff + (c % 3) * 256 + within;
-    *dst = f2bf(t);
+    const int64_t o = rowoff + (c % 3) * 256 + within;
+    const bf16_t h = f2bf(t);
+    (c < 3 ? a.A_rgb : a.A_aux)[o] = h;
+    bf16_t* lo = c < 3 ? a.A_rgb_lo : a.A_aux_lo;
+    if (lo) lo[o] = f2bf(t - bf2f(h));
     if (a.dbg_patch) a.dbg_patch[((int64_t)b * O * O + idx) * a.C + c] = (uint8_t)u8[c];
   }
 }

@@ -21,10 +21,10 @@ enum Epi : int {
 enum AMode : int { A_DENSE = 0, A_CONV3 = 1 };
 
 struct GemmGroup {
-  const bf16_t* A; int64_t lda;
-  const bf16_t* W; int64_t ldw;
+  const bf16_t* A; const bf16_t* A_lo; int64_t lda;     // A_lo: low half of the split operand (SPLIT)
+  const bf16_t* W; const bf16_t* W_lo; int64_t ldw;
   const float* bias;
-  void* C; int64_t ldc;
+  void* C; void* C_lo; int64_t ldc;                     // C_lo: bf16 outputs also emit their low half
   const float* R; int64_t ldr;
 };
 
@@ -36,6 +36,9 @@ struct GemmArgs {
   int conv_hw;      // A_CONV3: feature map is conv_hw x conv_hw (NHWC rows), zero padding 1
   int conv_cin;     // A_CONV3: input channels (multiple of 64)
   int pos_rows;     // EPI_POS_F32
+  int split;        // 1: fp32-faithful bf16x3 products
+  int wc;           // (set by the launcher) tile columns per XCD group
+  const bf16_t* zero;   // >= 16 zero bytes (source of padding / tail rows)
 };
 
 void gemm(const GemmArgs& a, int epi, hipStream_t s);
@@ -43,7 +46,9 @@ void gemm(const GemmArgs& a, int epi, hipStream_t s);
 // ---------------------------------------------------------------- attention
 struct AttnArgs {
   const bf16_t* qkv;   // [B][N][3*C]
+  const bf16_t* qkv_lo;  // split mode: low halves (else null)
   bf16_t* out;         // [B][N][C]
+  bf16_t* out_lo;      // split mode
   int B, N, heads;     // head dim 64, C = 64*heads
   int ce_query;        // template token whose probability row is exported (-1: none)
   int ce_lens_t;       // template length; exported keys are [ce_lens_t, N)
@@ -53,8 +58,8 @@ void attention(const AttnArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- layer norm (row of 768)
 // out_bf16[r] = LN(x[src(r)]), src(r) = gather ? b*in_pitch + gather[b][t] : r ; optional copy of x[src] to xcopy[r]
-void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, float* out_f32, int rows,
-               int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy, hipStream_t s);
+void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float* out_f32,
+               int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy, hipStream_t s);
 
 // ---------------------------------------------------------------- ViPT prompt blocks
 struct PromptArgs {
@@ -97,7 +102,7 @@ void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s
 
 // final norm + token recovery (zeros at pruned slots) -> head input NHWC bf16 [B][Lx][768]
 void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
-                        int B, int Lz, int Lx, bf16_t* feat, float* feat_f32_dbg, hipStream_t s);
+                        int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float* feat_f32_dbg, hipStream_t s);
 
 // ---------------------------------------------------------------- crop + normalise + patchify
 struct CropParam {                 // one per sequence (device memory, rewritten every frame)
@@ -111,6 +116,7 @@ struct CropArgs {
   const CropParam* params;         // [B]
   int B, out_sz, C;                // C = 6 (RGB+aux) or 3
   bf16_t* A_rgb; bf16_t* A_aux;    // [B][rows_per_seq][768]
+  bf16_t* A_rgb_lo; bf16_t* A_aux_lo;  // split mode low halves (else null)
   int rows_per_seq, row0;          // patch rows land at row0 + patch index
   uint8_t* dbg_patch;              // optional [B][out][out][C]
 };

@@ -59,6 +59,17 @@ __device__ __forceinline__ void store_bf16(bf16_t* p, const Row12& y, int lane) 
     q[lane + 64 * i] = o;
   }
 }
+__device__ __forceinline__ void store_bf16_lo(bf16_t* p, const Row12& y, int lane) {   // y - bf16(y)
+  uint2* q = reinterpret_cast<uint2*>(p);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 v = y.v[i];
+    uint2 o;
+    o.x = (uint32_t)f2bf(v.x - bf2f(f2bf(v.x))) | ((uint32_t)f2bf(v.y - bf2f(f2bf(v.y))) << 16);
+    o.y = (uint32_t)f2bf(v.z - bf2f(f2bf(v.z))) | ((uint32_t)f2bf(v.w - bf2f(f2bf(v.w))) << 16);
+    q[lane + 64 * i] = o;
+  }
+}
 __device__ __forceinline__ void store_f32(float* p, const Row12& y, int lane) {
   float4* q = reinterpret_cast<float4*>(p);
 #pragma unroll
@@ -67,8 +78,8 @@ __device__ __forceinline__ void store_f32(float* p, const Row12& y, int lane) {
 
 // ------------------------------------------------------------------ LayerNorm (optionally fused CE gather)
 __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w, const float* b, bf16_t* ob,
-                                                 float* of, int rows, int rows_per_seq, const int* gather,
-                                                 int in_rows_per_seq, float* xcopy) {
+                                                 bf16_t* olo, float* of, int rows, int rows_per_seq,
+                                                 const int* gather, int in_rows_per_seq, float* xcopy) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
   int64_t src = r;
@@ -80,12 +91,13 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
   if (xcopy) store_f32(xcopy + (int64_t)r * C768, xv, lane);
   const Row12 y = ln_row(xv, w, b, lane);
   if (ob) store_bf16(ob + (int64_t)r * C768, y, lane);
+  if (olo) store_bf16_lo(olo + (int64_t)r * C768, y, lane);
   if (of) store_f32(of + (int64_t)r * C768, y, lane);
 }
 
-void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, float* out_f32, int rows,
-               int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy, hipStream_t s) {
-  hipLaunchKernelGGL(ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_f32, rows,
+void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float* out_f32,
+               int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy, hipStream_t s) {
+  hipLaunchKernelGGL(ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_f32, rows,
                      rows_per_seq, gather, in_rows_per_seq, xcopy);
 }
 
@@ -298,7 +310,7 @@ void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s
 // to their 16x16 slots; pruned slots are exact zeros.
 __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int rows_per_seq, const int* slot2pos,
                                                          const float* w, const float* b, int B, int Lz, int Lx,
-                                                         bf16_t* feat, float* dbg) {
+                                                         bf16_t* feat, bf16_t* feat_lo, float* dbg) {
   const int L = Lz + Lx;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= B * L) return;
@@ -307,14 +319,15 @@ __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int row
   Row12 y = zero_row();
   if (pos >= 0) y = ln_row(load_row(X + ((int64_t)bs * rows_per_seq + pos) * C768, lane), w, b, lane);
   if (s >= Lz) store_bf16(feat + ((int64_t)bs * Lx + (s - Lz)) * C768, y, lane);
+  if (s >= Lz && feat_lo) store_bf16_lo(feat_lo + ((int64_t)bs * Lx + (s - Lz)) * C768, y, lane);
   if (dbg) store_f32(dbg + (int64_t)r * C768, y, lane);
 }
 
 void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
-                        int B, int Lz, int Lx, bf16_t* feat, float* feat_f32_dbg, hipStream_t s) {
+                        int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float* feat_f32_dbg, hipStream_t s) {
   const int rows = B * (Lz + Lx);
   hipLaunchKernelGGL(final_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, X, rows_per_seq, slot2pos, w, b, B,
-                     Lz, Lx, feat, feat_f32_dbg);
+                     Lz, Lx, feat, feat_lo, feat_f32_dbg);
 }
 
 }  // namespace mmt

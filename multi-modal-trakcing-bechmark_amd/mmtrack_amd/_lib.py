@@ -33,6 +33,7 @@ class MmtConfig(ctypes.Structure):
         ("max_batch", ctypes.c_int),
         ("use_graphs", ctypes.c_int),
         ("debug_outputs", ctypes.c_int),
+        ("precision", ctypes.c_int),
     ]
 
 

@@ -36,6 +36,7 @@ class EngineConfig:
     max_batch: int = 1
     use_graphs: bool = True
     debug_outputs: bool = False
+    precision: str = "bf16"           # "bf16" | "fp32" (fp32-faithful split-bf16 products)
 
     @classmethod
     def from_cfg(cls, cfg, **kw):
@@ -79,6 +80,9 @@ class EngineConfig:
         c.max_batch = self.max_batch
         c.use_graphs = int(self.use_graphs)
         c.debug_outputs = int(self.debug_outputs)
+        if self.precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' or 'fp32', got {self.precision!r}")
+        c.precision = 0 if self.precision == "bf16" else 1
         return c
 
 

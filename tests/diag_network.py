@@ -49,6 +49,8 @@ def run(name, shape, ecfg, ocfg, seeds=(101, 201)):
 def main():
     torch.set_num_threads(8)
     deep = dict(kind="vipt", prompt_type="vipt_deep")
+    run("deep, CE, fp32-faithful", deep, EngineConfig(debug_outputs=True, use_graphs=False, precision="fp32"),
+        ov.NetCfg())
     run("deep, no CE", deep, EngineConfig(ce_loc=[], ce_keep_ratio=[], debug_outputs=True, use_graphs=False),
         ov.NetCfg(ce_loc=[], ce_keep_ratio=[]))
     run("deep, CE", deep, EngineConfig(debug_outputs=True, use_graphs=False), ov.NetCfg())

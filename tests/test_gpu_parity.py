@@ -27,15 +27,24 @@ from oracle import vipt as ov
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
-NETS = {
-    "deep_rgbt": (dict(kind="vipt", prompt_type="vipt_deep"), EngineConfig(debug_outputs=True, use_graphs=False)),
-    "deep_rgbd": (dict(kind="vipt", prompt_type="vipt_deep"), EngineConfig(debug_outputs=True, use_graphs=False)),
-    "shaw_rgbt": (dict(kind="vipt", prompt_type="vipt_shaw"),
-                  EngineConfig(prompt_type="vipt_shaw", debug_outputs=True, use_graphs=False)),
-    "ostrack384": (dict(kind="ostrack", search_size=384, template_size=192),
-                   EngineConfig(model="ostrack", prompt_type="none", in_chans=3, template_size=192, search_size=384,
-                                search_factor=4.0, debug_outputs=True, use_graphs=False)),
+def _cfg(name, **kw):
+    base = dict(debug_outputs=True, use_graphs=False)
+    base.update(kw)
+    if name == "shaw_rgbt":
+        base.setdefault("prompt_type", "vipt_shaw")
+    if name == "ostrack384":
+        base.update(model="ostrack", prompt_type="none", in_chans=3, template_size=192, search_size=384,
+                    search_factor=4.0)
+    return EngineConfig(**base)
+
+
+SHAPES = {
+    "deep_rgbt": dict(kind="vipt", prompt_type="vipt_deep"),
+    "deep_rgbd": dict(kind="vipt", prompt_type="vipt_deep"),
+    "shaw_rgbt": dict(kind="vipt", prompt_type="vipt_shaw"),
+    "ostrack384": dict(kind="ostrack", search_size=384, template_size=192),
 }
+NETS = {name: (SHAPES[name], _cfg(name)) for name in SHAPES}
 
 
 def identity_frames(zp, xp, search_factor, template_factor=2.0):
@@ -65,11 +74,11 @@ def iou(a, b):
 def engines():
     cache = {}
 
-    def get(name):
-        if name not in cache:
-            shape, cfg = NETS[name]
-            cache[name] = Engine(cfg, synth.make_state_dict(0, **shape))
-        return cache[name]
+    def get(name, precision="fp32"):
+        key = (name, precision)
+        if key not in cache:
+            cache[key] = Engine(_cfg(name, precision=precision), synth.make_state_dict(0, **SHAPES[name]))
+        return cache[key]
     yield get
     for e in cache.values():
         e.close()
@@ -77,8 +86,9 @@ def engines():
 
 @pytest.mark.parametrize("name", list(NETS))
 def test_network_matches_reference_golden(engines, name):
-    shape, cfg = NETS[name]
-    eng = engines(name)
+    """fp32-faithful mode: the reference's own outputs, CE decisions identical, argmax exact."""
+    cfg = _cfg(name)
+    eng = engines(name, "fp32")
     g = np.load(os.path.join(GOLDEN, f"net_{name}.npz"))
     C = cfg.in_chans
     for j, (sz, ss) in enumerate(g["seeds"]):
@@ -90,19 +100,47 @@ def test_network_matches_reference_golden(engines, name):
         np.testing.assert_array_equal(eng.debug("crop"), xp)   # the crop really is the identity
         maps = eng.debug("maps")
         res = eng.debug("result")
-        gs = g[f"score_map_{j}"][0, 0]
-        np.testing.assert_allclose(maps[0], gs, atol=2e-2)
-        np.testing.assert_allclose(maps[1:3], g[f"size_map_{j}"][0], atol=2e-2)
-        np.testing.assert_allclose(maps[3:5], g[f"offset_map_{j}"][0], atol=5e-2)
-        assert int(res[5]) == int(g[f"resp_argmax_{j}"][0]), "windowed argmax differs from the reference"
-        # CE decisions: Jaccard of the removed sets per CE stage
         removed = eng.debug("removed")
         ref_removed = g[f"removed_{j}"][0]
-        lens = [ref_removed.shape[0]]
-        jac = len(set(removed[:len(ref_removed)]) & set(ref_removed)) / len(set(removed[:len(ref_removed)]) |
-                                                                             set(ref_removed))
-        print(f"{name}[{j}] CE removed-set Jaccard {jac:.3f}  max|dscore| {np.abs(maps[0] - gs).max():.2e}")
-        assert jac >= 0.9
+        np.testing.assert_array_equal(np.sort(removed[:len(ref_removed)]), np.sort(ref_removed))
+        gs = g[f"score_map_{j}"][0, 0]
+        print(f"{name}[{j}] fp32-faithful max|dscore| {np.abs(maps[0] - gs).max():.2e}")
+        np.testing.assert_allclose(maps[0], gs, atol=1e-3)
+        np.testing.assert_allclose(maps[1:3], g[f"size_map_{j}"][0], atol=1e-3)
+        np.testing.assert_allclose(maps[3:5], g[f"offset_map_{j}"][0], atol=3e-3)
+        assert int(res[5]) == int(g[f"resp_argmax_{j}"][0]), "windowed argmax differs from the reference"
+        feat = eng.debug("feat")
+        np.testing.assert_allclose(feat[::8], g[f"feat_rows_{j}"], atol=5e-3)
+
+
+@pytest.mark.parametrize("name", ["deep_rgbt", "ostrack384"])
+def test_network_bf16_statistics(engines, name):
+    """bf16 mode vs the fp32 oracle over 12 random crop pairs (statistical: CE flips are expected when
+    the reference's own CE margin is below bf16 resolution)."""
+    cfg = _cfg(name)
+    eng = engines(name, "bf16")
+    sd = synth.make_state_dict(0, **SHAPES[name])
+    ocfg = ov.NetCfg(kind=SHAPES[name]["kind"], prompt_type=SHAPES[name].get("prompt_type", "vipt_deep"),
+                     search_size=cfg.search_size, template_size=cfg.template_size)
+    agree, ious = 0, []
+    n = 12
+    for j in range(n):
+        zp = synth.make_patch(500 + j, cfg.template_size, cfg.in_chans)
+        xp = synth.make_patch(600 + j, cfg.search_size, cfg.in_chans)
+        f0, f1, box = identity_frames(zp, xp, cfg.search_factor)
+        eng.initialize(0, f0, box)
+        eng.track(0, f1)
+        res = eng.debug("result")
+        out = ov.forward(sd, ocrop.preprocess(zp), ocrop.preprocess(xp), ocfg, ov.ce_template_mask(ocfg))
+        resp = (ov.hann2d(ocfg.feat_sz) * out["score_map"]).flatten()
+        ref_idx = int(torch.argmax(resp))
+        agree += int(res[5]) == ref_idx
+        pb = out["pred_boxes"][0, 0].numpy()
+        to_xywh = lambda b: [b[0] - b[2] / 2, b[1] - b[3] / 2, b[2], b[3]]
+        ious.append(iou(to_xywh(res[:4]), to_xywh(pb)))
+    print(f"{name} bf16: argmax agreement {agree}/{n}, box IoU median {np.median(ious):.4f} min {min(ious):.4f}")
+    assert agree >= n * 0.5
+    assert np.median(ious) >= 0.9
 
 
 def test_tracker_sequence_matches_reference(engines):
@@ -110,14 +148,14 @@ def test_tracker_sequence_matches_reference(engines):
     g = np.load(os.path.join(GOLDEN, "tracker_deep_rgbt.npz"))
     seed, n, H, W, C = [int(v) for v in g["meta"]]
     frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
-    eng = engines("deep_rgbt")
+    eng = engines("deep_rgbt", "fp32")
     eng.initialize(0, frames[0], list(g["init_box"]))
     ious = []
     for t in range(1, n):
         box, score = eng.track(0, frames[t])
         ious.append(iou(box, g["boxes"][t]))
-    print("per-frame IoU vs reference:", np.round(ious, 4))
-    assert np.mean(ious) >= 0.98
+    print("per-frame IoU vs reference:", np.round(ious, 5))
+    assert min(ious) >= 0.999
 
 
 def test_crop_kernel_bit_exact_vs_oracle(engines):
@@ -136,12 +174,12 @@ def test_crop_kernel_bit_exact_vs_oracle(engines):
         np.testing.assert_array_equal(eng.debug("crop"), ref, err_msg=str(box))
 
 
-def test_batch_equals_single(engines):
-    """track_batch over N sequences == N independent single-sequence tracks."""
-    shape, _ = NETS["deep_rgbt"]
-    cfg = EngineConfig(max_batch=3, debug_outputs=True, use_graphs=True)
-    eng = Engine(cfg, synth.make_state_dict(0, **shape))
-    single = engines("deep_rgbt")
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_batch_equals_single(engines, precision):
+    """track_batch over N sequences (graph-captured) == N independent single-sequence tracks."""
+    cfg = EngineConfig(max_batch=3, debug_outputs=True, use_graphs=True, precision=precision)
+    eng = Engine(cfg, synth.make_state_dict(0, **SHAPES["deep_rgbt"]))
+    single = engines("deep_rgbt", precision)
     seqs = [synth.make_frames(40 + i, 4, 360, 480, 6, box=(200.0 + 10 * i, 150.0, 40.0 + 5 * i, 30.0)) for i in
             range(3)]
     for i, (fr, gt) in enumerate(seqs):
@@ -163,11 +201,11 @@ def test_engine_vs_oracle_tracker(engines):
     frames, gts = synth.make_frames(77, 8, 480, 640, 6)
     sd = synth.make_state_dict(0, kind="vipt", prompt_type="vipt_deep")
     boxes_o, _ = otracker.run_sequence(otracker.OracleTracker(sd, ov.NetCfg()), frames, gts[0])
-    eng = engines("deep_rgbt")
+    eng = engines("deep_rgbt", "fp32")
     eng.initialize(0, frames[0], list(gts[0]))
     ious = [iou(eng.track(0, frames[t])[0], boxes_o[t]) for t in range(1, 8)]
-    print("engine vs oracle IoU:", np.round(ious, 4))
-    assert np.mean(ious) >= 0.98
+    print("engine vs oracle IoU:", np.round(ious, 5))
+    assert min(ious) >= 0.999
 
 
 def test_errors_are_reference_shaped(engines):
