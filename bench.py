@@ -111,14 +111,8 @@ def main():
     def step(k):
         eng.track_batch(0, frame_lists[k % args.frames])
 
-    # the roofline probe brackets every launch of the dominant kernel class with HIP events that are
-    # captured into the replayed graph, so its per-launch times come from the timed region itself
-    if args.probe:
-        eng.timing_enable(args.probe)
     for k in range(max(args.warmup, 2)):
         step(k)
-    if args.probe:
-        eng.timing_enable(args.probe)   # reset counters: keep only the timed region
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -138,8 +132,13 @@ def main():
     frames_total = world * B * args.steps
     value = frames_total / elapsed
 
+    # roofline probe: the same steps again, launched eagerly (HIP cannot time event nodes captured in a
+    # graph), with HIP events on the engine stream around every launch of the dominant kernel class
     roof = None
     if args.probe:
+        eng.timing_enable(args.probe)
+        for k in range(min(args.steps, 20)):
+            step(args.warmup + k)
         tr = eng.timing_read()
         eng.timing_enable(None)
         if tr["launches"]:

@@ -86,6 +86,20 @@ struct PromptArgs {
 void prompt_reduce(const PromptArgs& a, hipStream_t s);
 void prompt_expand(const PromptArgs& a, hipStream_t s);
 
+// LN1 of a block with the prompt residual fused in (writes the updated residual X and LN(X))
+struct LnPromptArgs {
+  int mode;                  // 1: layer 0 (X = tok_rgb + P + pos), 2: deep layer (X += P[slot])
+  int rows, rows_per_seq, Lz, Lx;
+  float* X;
+  const float* P;            // [B][Lz+Lx][768]
+  const float* tok_rgb;      // mode 1
+  const float* pos;          // mode 1: [Lz+Lx][768]
+  const int* gidx;           // mode 2: [B][rows_per_seq - Lz] slot of each compact search token
+  const float* w; const float* b;
+  bf16_t* out; bf16_t* out_lo;
+};
+void ln_prompt(const LnPromptArgs& a, hipStream_t s);
+
 // ---------------------------------------------------------------- candidate elimination
 struct CEArgs {
   int B, Lz, Ls, keep, heads, Lx;

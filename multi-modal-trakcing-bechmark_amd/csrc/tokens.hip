@@ -105,51 +105,100 @@ void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16,
 // For every slot s of every sequence: a8 = conv0_0(LN_A(srcA[s])), c8 = conv0_1(LN_B(srcB[s]))
 // (Prompt_block.forward, vit_ce_prompt.py:62-68, on token2feature maps; a pruned search slot
 // is a zero row, vit_ce_prompt.py:276-283, whose LN is the LN bias).
-__device__ __forceinline__ void dot8(const Row12& y, const float* W, const float* bias, float* out, int lane) {
+// The two 8 x 768 conv weights live in LDS; a wave handles PR_ROWS rows; the 8 per-lane partial
+// dot products are reduced with a transposing butterfly (10 shuffles instead of 8 x 6).
+constexpr int PR_ROWS = 4;
+
+// out[c] (valid in lane c for c < 8) = sum over the wave of part[c]
+__device__ __forceinline__ float reduce8(float (&part)[8], int lane) {
+  // stage xor 32: lanes < 32 keep channels 0-3, others 4-7
+  float v4[4];
+  const bool hi32 = lane & 32;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float send = hi32 ? part[i] : part[i + 4];
+    const float keep = hi32 ? part[i + 4] : part[i];
+    v4[i] = keep + __shfl_xor(send, 32, 64);
+  }
+  float v2[2];
+  const bool hi16 = lane & 16;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float send = hi16 ? v4[i] : v4[i + 2];
+    const float keep = hi16 ? v4[i + 2] : v4[i];
+    v2[i] = keep + __shfl_xor(send, 16, 64);
+  }
+  const bool hi8 = lane & 8;
+  float v1 = (hi8 ? v2[1] : v2[0]) + __shfl_xor(hi8 ? v2[0] : v2[1], 8, 64);
+  v1 += __shfl_xor(v1, 4, 64);
+  v1 += __shfl_xor(v1, 2, 64);
+  v1 += __shfl_xor(v1, 1, 64);
+  // lane holds channel ((lane>>5)&1)*4 + ((lane>>4)&1)*2 + ((lane>>3)&1); gather to lane c
+  const int c = lane & 7;
+  const int src = ((c >> 2) & 1) * 32 + ((c >> 1) & 1) * 16 + (c & 1) * 8;
+  return __shfl(v1, src, 64);
+}
+
+__device__ __forceinline__ void dot8_lds(const Row12& y, const float* Ws, float (&part)[8], int lane) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    const float4* w4 = reinterpret_cast<const float4*>(W + c * C768);
+    const float4* w4 = reinterpret_cast<const float4*>(Ws + c * C768);
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const float4 ww = w4[lane + 64 * i];
       s += y.v[i].x * ww.x + y.v[i].y * ww.y + y.v[i].z * ww.z + y.v[i].w * ww.w;
     }
-    s = wave_sum(s);
-    if (lane == c) out[c] = s + bias[c];
+    part[c] = s;
   }
 }
 
 __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) {
-  const int L = a.Lz + a.Lx;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= a.B * L) return;
-  const int b = row / L, s = row - b * L;
-  Row12 xa;
-  if (a.layer == 0) {
-    xa = load_row(a.srcA + (int64_t)row * C768, lane);
-  } else {
-    const int pos = s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];
-    xa = pos >= 0 ? load_row(a.srcA + ((int64_t)b * a.srcA_rows + pos) * C768, lane) : zero_row();
+  __shared__ __attribute__((aligned(16))) float W0[8 * C768];
+  __shared__ __attribute__((aligned(16))) float W1[8 * C768];
+  for (int i = threadIdx.x; i < 8 * C768 / 4; i += 256) {
+    reinterpret_cast<float4*>(W0)[i] = reinterpret_cast<const float4*>(a.w00)[i];
+    reinterpret_cast<float4*>(W1)[i] = reinterpret_cast<const float4*>(a.w01)[i];
   }
-  const Row12 ya = ln_row(xa, a.lnA_w, a.lnA_b, lane);
-  dot8(ya, a.w00, a.b00, a.a8 + (int64_t)row * 8, lane);
-  const Row12 xb = load_row(a.srcB + (int64_t)row * C768, lane);
-  const Row12 yb = ln_row(xb, a.lnB_w, a.lnB_b, lane);
-  dot8(yb, a.w01, a.b01, a.c8 + (int64_t)row * 8, lane);
+  __syncthreads();
+  const int L = a.Lz + a.Lx, lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * PR_ROWS;
+  const float ba = lane < 8 ? a.b00[lane] : 0.f, bb = lane < 8 ? a.b01[lane] : 0.f;
+  for (int rr = 0; rr < PR_ROWS; ++rr) {
+    const int row = row0 + rr;
+    if (row >= a.B * L) return;
+    const int b = row / L, s = row - b * L;
+    Row12 xa;
+    if (a.layer == 0) {
+      xa = load_row(a.srcA + (int64_t)row * C768, lane);
+    } else {
+      const int pos = s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];
+      xa = pos >= 0 ? load_row(a.srcA + ((int64_t)b * a.srcA_rows + pos) * C768, lane) : zero_row();
+    }
+    const Row12 xb = load_row(a.srcB + (int64_t)row * C768, lane);
+    float part[8];
+    dot8_lds(ln_row(xa, a.lnA_w, a.lnA_b, lane), W0, part, lane);
+    const float ra = reduce8(part, lane);
+    dot8_lds(ln_row(xb, a.lnB_w, a.lnB_b, lane), W1, part, lane);
+    const float rb = reduce8(part, lane);
+    if (lane < 8) {
+      a.a8[(int64_t)row * 8 + lane] = ra + ba;
+      a.c8[(int64_t)row * 8 + lane] = rb + bb;
+    }
+  }
 }
 
 void prompt_reduce(const PromptArgs& a, hipStream_t s) {
   const int rows = a.B * (a.Lz + a.Lx);
-  hipLaunchKernelGGL(prompt_reduce_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, a);
+  const int waves = (rows + PR_ROWS - 1) / PR_ROWS;
+  hipLaunchKernelGGL(prompt_reduce_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, a);
 }
 
 // ------------------------------------------------------------------ prompt block, part 2
 // Fovea (vit_ce_prompt.py:33-47): per channel, softmax over the part's h*w positions of
-// x*smooth, times x; + conv0_1 branch; conv1x1 8 -> 768 (+bias) -> prompt P (full slot
-// layout). Residual: layer 0  X = (tok_rgb + P) + pos   (vit_ce_prompt.py:218, 240-241)
-//                   layer i   X[pos(s)] += P[s]          (vit_ce_prompt.py:310, attn_blocks.py:9-18)
-constexpr int PCHUNK = 64;
+// x*smooth, times x; + conv0_1 branch; conv1x1 8 -> 768 (+bias) -> prompt P (full slot layout).
+// The residual update that consumes P is fused into the next LayerNorm (ln_prompt below).
+constexpr int PCHUNK = 16;
 
 __global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) {
   __shared__ float red[256];
@@ -167,62 +216,52 @@ __global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) 
   const float* a8 = a.a8 + (int64_t)b * L * 8;
   const float* c8 = a.c8 + (int64_t)b * L * 8;
   const float sm = a.smooth;
-  // per-channel max of x*smooth over the part
   const int c = tid & 7, stripe = tid >> 3;
   float mx = -INFINITY;
   for (int t = lo + stripe; t < lo + n; t += 32) mx = fmaxf(mx, a8[t * 8 + c] * sm);
-  red[tid] = mx;
+  mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  if ((tid & 63) < 8) red[(tid >> 6) * 8 + c] = mx;
   __syncthreads();
-  if (tid < 8) {
-    float v = -INFINITY;
-    for (int k = 0; k < 32; ++k) v = fmaxf(v, red[k * 8 + tid]);
-    smax[tid] = v;
-  }
+  if (tid < 8) smax[tid] = fmaxf(fmaxf(red[tid], red[8 + tid]), fmaxf(red[16 + tid], red[24 + tid]));
   __syncthreads();
   const float cm = smax[c];
   float sum = 0.f;
   for (int t = lo + stripe; t < lo + n; t += 32) sum += __expf(a8[t * 8 + c] * sm - cm);
-  red[tid] = sum;
+  sum += __shfl_xor(sum, 8, 64);
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
   __syncthreads();
-  if (tid < 8) {
-    float v = 0.f;
-    for (int k = 0; k < 32; ++k) v += red[k * 8 + tid];
-    ssum[tid] = v;
-  }
+  if ((tid & 63) < 8) red[(tid >> 6) * 8 + c] = sum;
   __syncthreads();
-  for (int i = tid; i < (t1 - t0) * 8; i += 256) {
-    const int t = t0 + i / 8, ch = i & 7;
+  if (tid < 8) ssum[tid] = (red[tid] + red[8 + tid]) + (red[16 + tid] + red[24 + tid]);
+  __syncthreads();
+  if (tid < (t1 - t0) * 8) {
+    const int t = t0 + tid / 8, ch = tid & 7;
     const float v = a8[t * 8 + ch];
     const float msk = __expf(v * sm - smax[ch]) / ssum[ch];
-    f[i / 8][ch] = msk * v + c8[t * 8 + ch];
+    f[tid / 8][ch] = msk * v + c8[t * 8 + ch];
   }
   __syncthreads();
   float w1r[3][8], b1r[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int col = tid + 256 * k;
-#pragma unroll
-    for (int ch = 0; ch < 8; ++ch) w1r[k][ch] = a.w1[col * 8 + ch];
+    const float4* w4 = reinterpret_cast<const float4*>(a.w1 + col * 8);
+    const float4 p0 = w4[0], p1 = w4[1];
+    w1r[k][0] = p0.x; w1r[k][1] = p0.y; w1r[k][2] = p0.z; w1r[k][3] = p0.w;
+    w1r[k][4] = p1.x; w1r[k][5] = p1.y; w1r[k][6] = p1.z; w1r[k][7] = p1.w;
     b1r[k] = a.b1[col];
   }
   for (int t = t0; t < t1; ++t) {
-    int pos;
-    if (a.layer == 0) pos = t;
-    else pos = t < a.Lz ? t : a.slot2pos[b * a.Lx + (t - a.Lz)];
     float* prow = a.P + ((int64_t)b * L + t) * C768;
-    float* xrow = pos >= 0 ? a.X + ((int64_t)b * a.X_rows + pos) * C768 : nullptr;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const int col = tid + 256 * k;
       float v = b1r[k];
 #pragma unroll
       for (int ch = 0; ch < 8; ++ch) v += w1r[k][ch] * f[t - t0][ch];
-      prow[col] = v;
-      if (a.layer == 0) {
-        xrow[col] = (a.tok_rgb[((int64_t)b * L + t) * C768 + col] + v) + a.pos[(int64_t)t * C768 + col];
-      } else if (xrow) {
-        xrow[col] += v;
-      }
+      prow[tid + 256 * k] = v;
     }
   }
 }
@@ -230,6 +269,44 @@ __global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) 
 void prompt_expand(const PromptArgs& a, hipStream_t s) {
   const int nb = (a.Lz + PCHUNK - 1) / PCHUNK + (a.Lx + PCHUNK - 1) / PCHUNK;
   hipLaunchKernelGGL(prompt_expand_kernel, dim3(nb, a.B), dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------ LN1 with the prompt residual fused
+// mode 1 (layer 0):  X[r] = (tok_rgb[r] + P[r]) + pos[t]          (vit_ce_prompt.py:218, 240-241)
+// mode 2 (layer i):  X[r] = X[r] + P[b][slot(t)], slot(t) = t < Lz ? t : gidx[b][t-Lz]
+//                    (candidate_elimination_prompt + x_ori add, attn_blocks.py:9-18, vit_ce_prompt.py:310)
+// then out = LN(X[r]) (norm1 of the block).
+__global__ __launch_bounds__(256) void ln_prompt_kernel(const LnPromptArgs a) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= a.rows) return;
+  const int b = r / a.rows_per_seq, t = r - b * a.rows_per_seq;
+  const int L = a.Lz + a.Lx;
+  Row12 x;
+  if (a.mode == 1) {
+    const Row12 tk = load_row(a.tok_rgb + (int64_t)r * C768, lane);
+    const Row12 pp = load_row(a.P + (int64_t)r * C768, lane);
+    const Row12 ps = load_row(a.pos + (int64_t)t * C768, lane);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      x.v[i] = make_float4((tk.v[i].x + pp.v[i].x) + ps.v[i].x, (tk.v[i].y + pp.v[i].y) + ps.v[i].y,
+                           (tk.v[i].z + pp.v[i].z) + ps.v[i].z, (tk.v[i].w + pp.v[i].w) + ps.v[i].w);
+  } else {
+    const int slot = t < a.Lz ? t : a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (t - a.Lz)];
+    const Row12 xo = load_row(a.X + (int64_t)r * C768, lane);
+    const Row12 pp = load_row(a.P + ((int64_t)b * L + slot) * C768, lane);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      x.v[i] = make_float4(xo.v[i].x + pp.v[i].x, xo.v[i].y + pp.v[i].y, xo.v[i].z + pp.v[i].z,
+                           xo.v[i].w + pp.v[i].w);
+  }
+  store_f32(a.X + (int64_t)r * C768, x, lane);
+  const Row12 y = ln_row(x, a.w, a.b, lane);
+  store_bf16(a.out + (int64_t)r * C768, y, lane);
+  if (a.out_lo) store_bf16_lo(a.out_lo + (int64_t)r * C768, y, lane);
+}
+
+void ln_prompt(const LnPromptArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(ln_prompt_kernel, dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
 }
 
 // ------------------------------------------------------------------ candidate elimination

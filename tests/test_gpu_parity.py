@@ -135,7 +135,8 @@ def test_network_bf16_statistics(engines, name):
         resp = (ov.hann2d(ocfg.feat_sz) * out["score_map"]).flatten()
         ref_idx = int(torch.argmax(resp))
         agree += int(res[5]) == ref_idx
-        pb = out["pred_boxes"][0, 0].numpy()
+        pb = ov.cal_bbox(resp.view(1, 1, ocfg.feat_sz, ocfg.feat_sz), out["size_map"], out["offset_map"],
+                         ocfg.feat_sz)[0].numpy()
         to_xywh = lambda b: [b[0] - b[2] / 2, b[1] - b[3] / 2, b[2], b[3]]
         ious.append(iou(to_xywh(res[:4]), to_xywh(pb)))
     print(f"{name} bf16: argmax agreement {agree}/{n}, box IoU median {np.median(ious):.4f} min {min(ious):.4f}")
