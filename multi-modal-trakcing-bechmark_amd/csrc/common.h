@@ -27,7 +27,17 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Exact-erf GELU (nn.GELU default; vit_ce_prompt.py:122).
+// Exact-erf GELU (nn.GELU default; vit_ce_prompt.py:122), GELU(x) = x * (1 - erfc(x/sqrt2)/2),
+// with erfc from the Chebyshev-fitted form of Numerical Recipes' erfcc (fractional error < 1.2e-7
+// everywhere).  For x < 0 it is x * erfc(|x|/sqrt2) / 2 directly, so there is no cancellation.
+__device__ __forceinline__ float erfc_pos(float z) {   // z >= 0
+  const float t = __frcp_rn(1.0f + 0.5f * z);
+  const float p = -1.26551223f + t * (1.00002368f + t * (0.37409196f + t * (0.09678418f + t * (-0.18628806f +
+                  t * (0.27886807f + t * (-1.13520398f + t * (1.48851587f + t * (-0.82215223f + t * 0.17087277f))))))));
+  return t * __expf(-z * z + p);
+}
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  const float u = fabsf(x) * 0.70710678118654752440f;
+  const float h = 0.5f * erfc_pos(u);
+  return x >= 0.f ? x * (1.0f - h) : x * h;
 }

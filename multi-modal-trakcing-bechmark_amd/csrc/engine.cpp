@@ -1150,6 +1150,11 @@ int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const fl
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 
+int mmt_gemm_force_config(int cfg) {
+  gemm_force_config(cfg);
+  return MMT_OK;
+}
+
 int mmt_op_attention(const void* qkv, void* out, int B, int N, int heads, int ce_query, int ce_lens_t,
                      float* ce_prob, void* stream) {
   if (!qkv || !out || B <= 0 || N <= 0 || N > 1024 || heads <= 0) return MMT_E_ARG;

@@ -27,7 +27,7 @@ __device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((c ^ (r & 7)
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
-template <int BM, int BN, int WMW, int WNW, bool SPLIT>
+template <int BM, int BN, int WMW, int WNW, bool SPLIT, int STAGES = 0>
 struct Tile {
   static constexpr int NW = WMW * WNW;
   static constexpr int NT = NW * 64;
@@ -37,6 +37,7 @@ struct Tile {
   static constexpr int ROWS = AROWS + (SPLIT ? 2 * BN : BN);
   static constexpr int GROUPS = ROWS / 8;           // 8 rows per wave-instruction
   static constexpr int STAGE = ROWS * 64;           // bf16 elements per stage
+  static constexpr int NSTAGE = STAGES ? STAGES : 2;   // LDS ring depth
   static_assert(GROUPS % NW == 0, "row groups must divide over waves");
 };
 
@@ -49,10 +50,10 @@ __device__ __forceinline__ void tile_of(int id, int tiles_m, int tiles_n, int wc
   tn = grp * wc + (rem - tm * width);
 }
 
-template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT>
+template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int STAGES>
 __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args) {
-  using T = Tile<BM, BN, WMW, WNW, SPLIT>;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * T::STAGE];
+  using T = Tile<BM, BN, WMW, WNW, SPLIT, STAGES>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[T::NSTAGE * T::STAGE];
 
   const GemmGroup& g = args.g[blockIdx.z];
   const int M = args.M, N = args.N, K = args.K;
@@ -169,15 +170,28 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
     }
   };
 
+  // K loop over an LDS ring of NSTAGE buffers: tiles kt+1 .. kt+NSTAGE-1 are in flight while tile kt
+  // is multiplied.  A tile is read only after the issuing waves' counted vmcnt retired it AND a
+  // barrier (raw s_barrier: __syncthreads() would drain every in-flight LDS-DMA with vmcnt(0)).
   const int nk = K / 64;
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  constexpr int D = T::NSTAGE - 1;   // tiles in flight ahead of the one being multiplied
+  for (int p = 0; p < D; ++p)
+    if (p < nk) issue(p, p);
+  if (nk > 1 && D > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int stage = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-    compute(kt & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    const int ahead = kt + D;
+    if (ahead < nk) issue(ahead, ahead % T::NSTAGE);
+    compute(stage);
+    stage = stage + 1 == T::NSTAGE ? 0 : stage + 1;
+    // retire tile kt+1: the loads issued after it (tiles kt+2 .. min(kt+D, nk-1)) may stay in flight
+    const int after = min(kt + D, nk - 1) - (kt + 1);
+    if (D > 1 && after >= D - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 
   // ---- epilogue: lane owns C[m][n..n+3]
@@ -226,7 +240,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   }
 }
 
-template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT>
+template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int ST>
 static void launch_one(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.N / BN;
@@ -238,34 +252,51 @@ static void launch_one(const GemmArgs& a0, hipStream_t s) {
   }
   a.wc = wc;
   dim3 grid(tiles_m * tiles_n, 1, a.groups);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI, AM, SPLIT>), grid, dim3(WMW * WNW * 64), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI, AM, SPLIT, ST>), grid, dim3(WMW * WNW * 64), 0, s, a);
 }
 
-template <int BM, int BN, int WMW, int WNW, bool SPLIT>
+template <int BM, int BN, int WMW, int WNW, bool SPLIT, int ST = 2>
 static void launch_cfg(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.amode == A_CONV3) {
-    if (epi == EPI_RELU_BF16) return launch_one<BM, BN, WMW, WNW, EPI_RELU_BF16, A_CONV3, SPLIT>(a, s);
-    if (epi == EPI_RELU_F32) return launch_one<BM, BN, WMW, WNW, EPI_RELU_F32, A_CONV3, SPLIT>(a, s);
+    if (epi == EPI_RELU_BF16) return launch_one<BM, BN, WMW, WNW, EPI_RELU_BF16, A_CONV3, SPLIT, ST>(a, s);
+    if (epi == EPI_RELU_F32) return launch_one<BM, BN, WMW, WNW, EPI_RELU_F32, A_CONV3, SPLIT, ST>(a, s);
     return;
   }
   switch (epi) {
-    case EPI_BF16: return launch_one<BM, BN, WMW, WNW, EPI_BF16, A_DENSE, SPLIT>(a, s);
-    case EPI_GELU_BF16: return launch_one<BM, BN, WMW, WNW, EPI_GELU_BF16, A_DENSE, SPLIT>(a, s);
-    case EPI_RESID_F32: return launch_one<BM, BN, WMW, WNW, EPI_RESID_F32, A_DENSE, SPLIT>(a, s);
-    case EPI_F32: return launch_one<BM, BN, WMW, WNW, EPI_F32, A_DENSE, SPLIT>(a, s);
-    case EPI_POS_F32: return launch_one<BM, BN, WMW, WNW, EPI_POS_F32, A_DENSE, SPLIT>(a, s);
+    case EPI_BF16: return launch_one<BM, BN, WMW, WNW, EPI_BF16, A_DENSE, SPLIT, ST>(a, s);
+    case EPI_GELU_BF16: return launch_one<BM, BN, WMW, WNW, EPI_GELU_BF16, A_DENSE, SPLIT, ST>(a, s);
+    case EPI_RESID_F32: return launch_one<BM, BN, WMW, WNW, EPI_RESID_F32, A_DENSE, SPLIT, ST>(a, s);
+    case EPI_F32: return launch_one<BM, BN, WMW, WNW, EPI_F32, A_DENSE, SPLIT, ST>(a, s);
+    case EPI_POS_F32: return launch_one<BM, BN, WMW, WNW, EPI_POS_F32, A_DENSE, SPLIT, ST>(a, s);
     default: break;
   }
 }
 
+static int g_force_cfg = -1;   // tuning override (mmt_gemm_force_config), -1 = heuristic
+
 template <bool SPLIT>
 static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
-  const int target = 200;   // aim for at least ~one tile per CU of the 256
-  const int t256 = (a.M + 255) / 256, t128 = (a.M + 127) / 128, t64 = (a.M + 63) / 64;
   if constexpr (!SPLIT) {
-    if (a.N % 128 == 0 && t256 * (a.N / 128) * a.groups >= target) return launch_cfg<256, 128, 4, 2, false>(a, epi, s);
+    if (g_force_cfg >= 0 && a.amode == A_DENSE) {
+      switch (g_force_cfg) {
+        case 1: return launch_cfg<256, 128, 4, 2, false, 3>(a, epi, s);
+        case 2: return launch_cfg<256, 128, 4, 2, false, 2>(a, epi, s);
+        case 3: return launch_cfg<128, 128, 2, 2, false, 2>(a, epi, s);
+        case 4: return launch_cfg<128, 128, 2, 2, false, 3>(a, epi, s);
+        case 5: return launch_cfg<128, 128, 4, 2, false, 2>(a, epi, s);
+        case 6: return launch_cfg<256, 256, 4, 2, false, 2>(a, epi, s);
+        case 7: return launch_cfg<128, 256, 2, 4, false, 2>(a, epi, s);
+        case 8: return launch_cfg<64, 128, 2, 2, false, 2>(a, epi, s);
+        default: break;
+      }
+    }
   }
-  if (a.N % 128 == 0 && t128 * (a.N / 128) * a.groups >= target) return launch_cfg<128, 128, 2, 2, SPLIT>(a, epi, s);
+  // Measured on the path's shapes (tests/bench_gemm.py, MI355X): 128x128 tiles with 8 waves (32x64
+  // per wave) and a 2-deep LDS ring (64 KB, two workgroups per CU, so one tile's prologue/epilogue
+  // overlaps the other's MFMAs) beat 256x128 / 256x256 / 3-deep rings on every K=768/3072 GEMM.
+  const int target = 200;   // aim for at least ~one tile per CU of the 256
+  const int t128 = (a.M + 127) / 128, t64 = (a.M + 63) / 64;
+  if (a.N % 128 == 0 && t128 * (a.N / 128) * a.groups >= target) return launch_cfg<128, 128, 4, 2, SPLIT>(a, epi, s);
   if (a.N % 64 == 0) {
     if (t128 * (a.N / 64) * a.groups >= target) return launch_cfg<128, 64, 2, 2, SPLIT>(a, epi, s);
     return launch_cfg<64, 64, 2, 2, SPLIT>(a, epi, s);
@@ -280,5 +311,7 @@ void gemm(const GemmArgs& a, int epi, hipStream_t s) {
   else
     gemm_dispatch<false>(a, epi, s);
 }
+
+void gemm_force_config(int cfg) { g_force_cfg = cfg; }
 
 }  // namespace mmt

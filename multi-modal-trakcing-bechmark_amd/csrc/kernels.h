@@ -42,6 +42,7 @@ struct GemmArgs {
 };
 
 void gemm(const GemmArgs& a, int epi, hipStream_t s);
+void gemm_force_config(int cfg);   // tuning override, -1 = heuristic
 
 // ---------------------------------------------------------------- attention
 struct AttnArgs {

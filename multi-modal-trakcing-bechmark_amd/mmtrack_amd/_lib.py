@@ -63,6 +63,7 @@ SIGNATURES = {
     "mmt_timing_read": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_D), ctypes.POINTER(_D), ctypes.POINTER(_D)]),
     "mmt_xcorr": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P]),
     "mmt_op_gemm": (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "mmt_gemm_force_config": (_I, [_I]),
     "mmt_op_attention": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "mmt_op_layernorm": (_I, [_P, _P, _P, _P, _P, _I, _P]),
 }

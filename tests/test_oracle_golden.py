@@ -80,3 +80,21 @@ def test_cv2_resize_restatement_properties():
     half = ocrop.cv2_resize_linear_u8(im[:64, :64], 32, 32)  # exact 2x -> area average
     ref = (im[:64:2, :64:2].astype(int) + im[1:64:2, :64:2] + im[:64:2, 1:64:2] + im[1:64:2, 1:64:2] + 2) >> 2
     np.testing.assert_array_equal(half, ref)
+
+
+def test_gelu_erfc_form_accuracy():
+    """The kernels' GELU (common.h gelu_erf: NR erfcc form, fp32) vs exact erf GELU (timm Mlp act)."""
+    import math
+    x = np.concatenate([np.linspace(-12, 12, 20001), np.random.default_rng(0).normal(0, 3, 20000)]).astype(np.float32)
+    f = np.float32
+    u = np.abs(x) * f(0.70710678118654752440)
+    t = f(1) / (f(1) + f(0.5) * u)
+    p = f(-1.26551223) + t * (f(1.00002368) + t * (f(0.37409196) + t * (f(0.09678418) + t * (f(-0.18628806) + t * (
+        f(0.27886807) + t * (f(-1.13520398) + t * (f(1.48851587) + t * (f(-0.82215223) + t * f(0.17087277)))))))))
+    h = f(0.5) * (t * np.exp(-u * u + p)).astype(np.float32)
+    y = np.where(x >= 0, x * (f(1) - h), x * h)
+    ref = np.array([0.5 * v * (1 + math.erf(v / math.sqrt(2))) for v in x.astype(np.float64)])
+    err = np.abs(y - ref)
+    assert (err <= 2e-7 * np.maximum(1.0, np.abs(x))).all()       # absolute, everywhere
+    big = np.abs(ref) > 1e-4
+    assert (err[big] / np.abs(ref[big])).max() < 5e-6            # relative, where it matters
