@@ -112,6 +112,34 @@ int mmt_timing_read(mmt_engine* e, int* launches, double* total_ms, double* flop
 int mmt_xcorr(const float* z, const float* x, float* out, int B, int C, int hz, int wz, int hx, int wx,
               float scale, float bias, void* hip_stream);
 
+/* ---- DiMP / mfDiMP target classifier (device pointers, fp32) ------------------------------------
+ *  feat [I][S][C][H][W] (I training images x S sequences), filter [S][C][fh][fw] (fh*fw <= 25).
+ *  mmt_dimp_optimize runs num_iter steepest-descent Gauss-Newton steps in place on `weights`
+ *  (DiMPSteepestDescentGN.forward, optimizer.py:85-170; relu score activation, sigmoid mask);
+ *  bb: host [I][S][4] target boxes (x, y, w, h, image pixels); sample_weight: host [I][S] or NULL
+ *  (= 1/I); losses: host [num_iter + 1] or NULL (when given, the call synchronises the stream). */
+typedef struct mmt_dimp_params {
+  float feat_stride;        /* 16                                            */
+  float log_step_length;    /* optimizer.log_step_length                     */
+  float filter_reg;         /* optimizer.filter_reg                          */
+  float min_filter_reg;     /* 1e-3                                          */
+  float alpha_eps;          /* 0                                             */
+  float bin_displacement;   /* DistanceMap bin displacement                  */
+  int num_dist_bins;        /* <= 32                                         */
+  float label_w[32];        /* label_map_predictor.weight                    */
+  float mask_w[32];         /* target_mask_predictor.0.weight                */
+  float spatial_w[32];      /* spatial_weight_predictor.weight               */
+} mmt_dimp_params;
+
+size_t mmt_dimp_workspace_bytes(int I, int S, int C, int H, int W, int fh, int fw, int num_iter);
+int mmt_dimp_apply_filter(const float* feat, const float* w, float* scores, int I, int S, int C, int H, int W,
+                          int fh, int fw, void* hip_stream);
+int mmt_dimp_feat_transpose(const float* feat, const float* r, float* grad, int I, int S, int C, int H, int W,
+                            int fh, int fw, void* hip_stream);
+int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
+                      const float* bb, const float* sample_weight, const mmt_dimp_params* p, int num_iter,
+                      void* workspace, size_t ws_bytes, float* losses, void* hip_stream);
+
 /* ---- operator-level entry points (device pointers; used by the parity tests and by hosts that
  *      compose their own pipelines).  epi: 0 bias->bf16, 1 bias+GELU->bf16, 2 C(f32) = R + acc + bias,
  *      3 bias+ReLU->bf16, 4 bias->f32, 5 bias+ReLU->f32, 6 C(f32) = acc + bias + R[m % pos_rows].

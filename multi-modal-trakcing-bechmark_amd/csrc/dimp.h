@@ -1,0 +1,45 @@
+// DiMP classifier kernels (dimp.hip) -- launch interfaces.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mmt {
+
+struct DimpMaps {                 // label / target-mask / sample-weight maps from the distance bins
+  int IS, Ho, Wo, nbins;
+  float bin_disp;
+  const float* centers;           // [IS][2] (y, x) in feature cells
+  const float* sqrt_sw;           // [IS] sqrt of the per-sample weight
+  const float* label_w; const float* mask_w; const float* spatial_w;   // [nbins] (device)
+  float* label; float* mask; float* sw;                                 // [IS][Ho][Wo]
+};
+struct DimpFilter {
+  const float* feat;              // [I][S][C][H][W]
+  const float* w;                 // [S][C][fh][fw]
+  int I, S, C, H, W, fh, fw, Ho, Wo;
+  int mode;                       // 0: scores, 1: residual step (out = mapped residual), 2: |J g|^2 partials
+  float* out;
+  const float* label; const float* mask; const float* sw;
+  float* smask;                   // mode 1 writes the activation derivative, mode 2 reads it
+  float* partial;                 // [I*S][ceil(Ho*Wo/256)] block partial sums of squares (or null)
+};
+struct DimpTranspose {
+  const float* feat; const float* r;   // r: [I][S][Ho][Wo]
+  const float* w; float reg;           // optional: grad += reg * w
+  int I, S, C, H, W, fh, fw, Ho, Wo;
+  float* grad;                         // [S][C][fh][fw]
+  float* gsq;                          // [S][C] partial |g|^2 (or null)
+};
+struct DimpUpdate {
+  float* w; const float* grad; const float* gsq; const float* sgsq;
+  int I, S, C, fh, fw, nby;
+  float reg, alpha_eps, step;
+};
+
+void dimp_maps(const DimpMaps& m, hipStream_t s);
+void dimp_filter(const DimpFilter& a, hipStream_t s);
+void dimp_transpose(const DimpTranspose& a, hipStream_t s);
+void dimp_update(const DimpUpdate& a, hipStream_t s);
+void dimp_loss(const float* rsq, int nparts, const float* w, int nw, float reg, int S, float* loss, hipStream_t s);
+
+}  // namespace mmt

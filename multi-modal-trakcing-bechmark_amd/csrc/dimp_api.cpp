@@ -1,0 +1,172 @@
+// C ABI of the DiMP classifier inner loop (include/mmtrack.h, mmt_dimp_*).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/mmtrack.h"
+#include "dimp.h"
+
+using namespace mmt;
+
+namespace {
+
+struct WsLayout {
+  size_t label, mask, sw, rm, smask, scratch, grad, gsq, rsq, sgsq, loss, centers, sqrtsw, params, total;
+};
+
+WsLayout layout(int I, int S, int C, int H, int W, int fh, int fw, int num_iter) {
+  const size_t Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, n = Ho * Wo, IS = (size_t)I * S;
+  const size_t nby = (n + 255) / 256;
+  WsLayout L{};
+  size_t off = 0;
+  auto take = [&](size_t floats) {
+    size_t o = off;
+    off += (floats * 4 + 255) & ~size_t(255);
+    return o;
+  };
+  L.label = take(IS * n);
+  L.mask = take(IS * n);
+  L.sw = take(IS * n);
+  L.rm = take(IS * n);
+  L.smask = take(IS * n);
+  L.scratch = take(IS * n);
+  L.grad = take((size_t)S * C * fh * fw);
+  L.gsq = take((size_t)S * C);
+  L.rsq = take(IS * nby);
+  L.sgsq = take(IS * nby);
+  L.loss = take(num_iter + 1);
+  L.centers = take(IS * 2);
+  L.sqrtsw = take(IS);
+  L.params = take(3 * 32);
+  L.total = off;
+  return L;
+}
+
+bool bad_dims(int I, int S, int C, int H, int W, int fh, int fw) {
+  return I <= 0 || S <= 0 || C <= 0 || H <= 0 || W <= 0 || fh <= 0 || fw <= 0 || fh * fw > 25 || C * fh * fw > 15360;   // weight tile in LDS <= 60 KB
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mmt_dimp_workspace_bytes(int I, int S, int C, int H, int W, int fh, int fw, int num_iter) {
+  if (bad_dims(I, S, C, H, W, fh, fw) || num_iter < 0) return 0;
+  return layout(I, S, C, H, W, fh, fw, num_iter).total;
+}
+
+int mmt_dimp_apply_filter(const float* feat, const float* w, float* scores, int I, int S, int C, int H, int W, int fh,
+                          int fw, void* stream) {
+  if (!feat || !w || !scores || bad_dims(I, S, C, H, W, fh, fw)) return MMT_E_ARG;
+  DimpFilter a{};
+  a.feat = feat;
+  a.w = w;
+  a.I = I; a.S = S; a.C = C; a.H = H; a.W = W; a.fh = fh; a.fw = fw;
+  a.Ho = H + 2 * (fh / 2) - fh + 1;
+  a.Wo = W + 2 * (fw / 2) - fw + 1;
+  a.mode = 0;
+  a.out = scores;
+  dimp_filter(a, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_dimp_feat_transpose(const float* feat, const float* r, float* grad, int I, int S, int C, int H, int W, int fh,
+                            int fw, void* stream) {
+  if (!feat || !r || !grad || bad_dims(I, S, C, H, W, fh, fw)) return MMT_E_ARG;
+  DimpTranspose a{};
+  a.feat = feat;
+  a.r = r;
+  a.I = I; a.S = S; a.C = C; a.H = H; a.W = W; a.fh = fh; a.fw = fw;
+  a.Ho = H + 2 * (fh / 2) - fh + 1;
+  a.Wo = W + 2 * (fw / 2) - fw + 1;
+  a.grad = grad;
+  dimp_transpose(a, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
+                      const float* bb, const float* sample_weight, const mmt_dimp_params* p, int num_iter,
+                      void* workspace, size_t ws_bytes, float* losses, void* stream_) {
+  if (!feat || !weights || !bb || !p || !workspace || num_iter < 0 || bad_dims(I, S, C, H, W, fh, fw) ||
+      p->num_dist_bins <= 0 || p->num_dist_bins > 32)
+    return MMT_E_ARG;
+  const WsLayout L = layout(I, S, C, H, W, fh, fw, num_iter);
+  if (ws_bytes < L.total) return MMT_E_ARG;
+  hipStream_t st = (hipStream_t)stream_;
+  char* ws = static_cast<char*>(workspace);
+  auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
+  const int IS = I * S;
+  const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, n = Ho * Wo, nby = (n + 255) / 256;
+  // host-side per-sample constants (optimizer.py:108-125, same fp32 arithmetic)
+  std::vector<float> centers(2 * IS), sqrtsw(IS), params(96, 0.f);
+  const float off0 = (float)(fh % 2) / 2.0f, off1 = (float)(fw % 2) / 2.0f;
+  for (int k = 0; k < IS; ++k) {
+    const float* b = bb + 4 * k;
+    centers[2 * k] = (b[1] + b[3] / 2) / p->feat_stride - off0;       // flip((1,)) -> (y, x)
+    centers[2 * k + 1] = (b[0] + b[2] / 2) / p->feat_stride - off1;
+    sqrtsw[k] = sample_weight ? std::sqrt(sample_weight[k]) : (float)std::sqrt(1.0 / I);
+  }
+  std::memcpy(params.data(), p->label_w, 32 * 4);
+  std::memcpy(params.data() + 32, p->mask_w, 32 * 4);
+  std::memcpy(params.data() + 64, p->spatial_w, 32 * 4);
+  if (hipMemcpyAsync(F(L.centers), centers.data(), centers.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(F(L.sqrtsw), sqrtsw.data(), sqrtsw.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(F(L.params), params.data(), params.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess)
+    return MMT_E_HIP;
+  const float step = std::exp(p->log_step_length);
+  const float reg = std::fmax(p->filter_reg * p->filter_reg, p->min_filter_reg * p->min_filter_reg);
+
+  DimpMaps m{IS, Ho, Wo, p->num_dist_bins, p->bin_displacement, F(L.centers), F(L.sqrtsw), F(L.params),
+             F(L.params) + 32, F(L.params) + 64, F(L.label), F(L.mask), F(L.sw)};
+  dimp_maps(m, st);
+
+  DimpFilter fa{};
+  fa.feat = feat;
+  fa.I = I; fa.S = S; fa.C = C; fa.H = H; fa.W = W; fa.fh = fh; fa.fw = fw; fa.Ho = Ho; fa.Wo = Wo;
+  fa.label = F(L.label);
+  fa.mask = F(L.mask);
+  fa.sw = F(L.sw);
+  fa.smask = F(L.smask);
+  DimpTranspose ta{};
+  ta.feat = feat;
+  ta.r = F(L.rm);
+  ta.w = weights;
+  ta.reg = reg;
+  ta.I = I; ta.S = S; ta.C = C; ta.H = H; ta.W = W; ta.fh = fh; ta.fw = fw; ta.Ho = Ho; ta.Wo = Wo;
+  ta.grad = F(L.grad);
+  ta.gsq = F(L.gsq);
+  DimpUpdate ua{weights, F(L.grad), F(L.gsq), F(L.sgsq), I, S, C, fh, fw, nby, reg, p->alpha_eps, step};
+  const int nw = S * C * fh * fw;
+  for (int it = 0; it < num_iter; ++it) {
+    fa.mode = 1;               // residuals at the current filter
+    fa.w = weights;
+    fa.out = F(L.rm);
+    fa.partial = F(L.rsq);
+    dimp_filter(fa, st);
+    if (losses) dimp_loss(F(L.rsq), IS * nby, weights, nw, reg, S, F(L.loss) + it, st);
+    dimp_transpose(ta, st);    // gradient
+    fa.mode = 2;               // |J g|^2
+    fa.w = F(L.grad);
+    fa.out = nullptr;
+    fa.partial = F(L.sgsq);
+    dimp_filter(fa, st);
+    dimp_update(ua, st);       // Gauss-Newton step
+  }
+  if (losses) {
+    fa.mode = 1;
+    fa.w = weights;
+    fa.out = F(L.scratch);
+    fa.smask = F(L.scratch);
+    fa.partial = F(L.rsq);
+    dimp_filter(fa, st);
+    dimp_loss(F(L.rsq), IS * nby, weights, nw, reg, S, F(L.loss) + num_iter, st);
+    if (hipMemcpyAsync(losses, F(L.loss), (num_iter + 1) * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return MMT_E_HIP;
+  }
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+}  // extern "C"

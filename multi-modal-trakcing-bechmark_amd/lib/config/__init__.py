@@ -1,0 +1,1 @@
+"""Reference-layout mirror (ViPT/lib) over the MI355X engine."""

@@ -37,6 +37,21 @@ class MmtConfig(ctypes.Structure):
     ]
 
 
+class MmtDimpParams(ctypes.Structure):
+    _fields_ = [
+        ("feat_stride", ctypes.c_float),
+        ("log_step_length", ctypes.c_float),
+        ("filter_reg", ctypes.c_float),
+        ("min_filter_reg", ctypes.c_float),
+        ("alpha_eps", ctypes.c_float),
+        ("bin_displacement", ctypes.c_float),
+        ("num_dist_bins", ctypes.c_int),
+        ("label_w", ctypes.c_float * 32),
+        ("mask_w", ctypes.c_float * 32),
+        ("spatial_w", ctypes.c_float * 32),
+    ]
+
+
 # every symbol include/mmtrack.h declares: name -> (restype, argtypes)
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -62,6 +77,11 @@ SIGNATURES = {
     "mmt_timing_enable": (_I, [_P, ctypes.c_char_p]),
     "mmt_timing_read": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_D), ctypes.POINTER(_D), ctypes.POINTER(_D)]),
     "mmt_xcorr": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P]),
+    "mmt_dimp_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I]),
+    "mmt_dimp_apply_filter": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "mmt_dimp_feat_transpose": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "mmt_dimp_optimize": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, ctypes.POINTER(MmtDimpParams), _I, _P,
+                               ctypes.c_size_t, _P, _P]),
     "mmt_op_gemm": (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_gemm_force_config": (_I, [_I]),
     "mmt_op_attention": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),

@@ -98,3 +98,17 @@ def test_gelu_erfc_form_accuracy():
     assert (err <= 2e-7 * np.maximum(1.0, np.abs(x))).all()       # absolute, everywhere
     big = np.abs(ref) > 1e-4
     assert (err[big] / np.abs(ref[big])).max() < 5e-6            # relative, where it matters
+
+
+def test_oracle_dimp_matches_reference():
+    """DiMP filter / transposed filter / steepest-descent GN iterates vs the DeT reference (golden)."""
+    from oracle import dimp as od
+    g = np.load(os.path.join(GOLDEN, "dimp.npz"))
+    feat, filt, bb = (torch.from_numpy(g[k]) for k in ("feat", "filt", "bb"))
+    np.testing.assert_allclose(od.apply_filter(feat, filt).numpy(), g["scores"], rtol=1e-5, atol=1e-5)
+    ft = od.apply_feat_transpose(feat, torch.from_numpy(g["resid"]), (4, 4)).numpy()
+    np.testing.assert_allclose(ft, g["feat_t"], rtol=1e-4, atol=1e-3)
+    sd = {k[4:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("opt.")}
+    w, iters, losses = od.steepest_descent_gn(filt, feat, bb, sd, num_iter=5)
+    np.testing.assert_allclose(torch.stack(iters).numpy(), g["iterates"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(torch.stack(losses).numpy().ravel(), g["losses"], rtol=1e-4)
