@@ -68,6 +68,14 @@ def cpu_baseline(workload, frames_np, gts, seconds=12.0):
                       f"(crop+net+decode, torch {threads} threads, {dt:.1f}s)"}
 
 
+def aggregate_throughput(batch, steps, elapsed):
+    """(whole-job frames/s, max-over-ranks elapsed): every rank tracked batch x steps frames."""
+    from mmtrack_amd.sharding import max_over_ranks, rank_world
+    _, world = rank_world()
+    elapsed = max_over_ranks(elapsed)
+    return world * batch * steps / elapsed, elapsed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,13 +132,7 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    frames_total = world * B * args.steps
-    value = frames_total / elapsed
+    value, elapsed = aggregate_throughput(B, args.steps, t1 - t0)
 
     # roofline probe: the same steps again, launched eagerly (HIP cannot time event nodes captured in a
     # graph), with HIP events on the engine stream around every launch of the dominant kernel class

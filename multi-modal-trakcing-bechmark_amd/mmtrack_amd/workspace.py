@@ -32,23 +32,27 @@ def gen_config(seq_path, set_type):
     if set_type in ('RGBT234', 'LasHeR', 'lasher'):
         rgb = sorted(join(seq_path, 'visible', p) for p in os.listdir(join(seq_path, 'visible')) if p.endswith('.jpg'))
         aux = sorted(join(seq_path, 'infrared', p) for p in os.listdir(join(seq_path, 'infrared')) if p.endswith('.jpg'))
-        gt = np.loadtxt(join(seq_path, 'visible.txt'), delimiter=',')
+        gt = np.loadtxt(join(seq_path, 'visible.txt'), delimiter=',', ndmin=2)
     elif set_type == 'GTOT':
         rgb = sorted(join(seq_path, 'v', p) for p in os.listdir(join(seq_path, 'v')) if p.endswith('.png'))
         aux = sorted(join(seq_path, 'i', p) for p in os.listdir(join(seq_path, 'i')) if p.endswith('.png'))
-        g = np.loadtxt(join(seq_path, 'groundTruth_v.txt'), delimiter=' ')
+        g = np.loadtxt(join(seq_path, 'groundTruth_v.txt'), delimiter=' ', ndmin=2)
         x0, y0 = g[:, [0, 2]].min(1), g[:, [1, 3]].min(1)
         x1, y1 = g[:, [0, 2]].max(1), g[:, [1, 3]].max(1)
         gt = np.stack([x0, y0, x1 - x0, y1 - y0], axis=1)
     elif 'VTUAV' in set_type:
         rgb = sorted(join(seq_path, 'rgb', p) for p in os.listdir(join(seq_path, 'rgb')) if p.endswith('.jpg'))
         aux = sorted(join(seq_path, 'ir', p) for p in os.listdir(join(seq_path, 'ir')) if p.endswith('.jpg'))
-        gt = np.loadtxt(join(seq_path, 'rgb.txt'), delimiter=' ')
+        gt = np.loadtxt(join(seq_path, 'rgb.txt'), delimiter=' ', ndmin=2)
+    elif set_type in ('DepthTrack', 'depthtrack', 'CDTB', 'cdtb'):   # VOT-RGBD layout: color/, depth/
+        rgb = sorted(join(seq_path, 'color', p) for p in os.listdir(join(seq_path, 'color')) if p.endswith('.jpg'))
+        aux = sorted(join(seq_path, 'depth', p) for p in os.listdir(join(seq_path, 'depth')) if p.endswith('.png'))
+        gt = np.loadtxt(join(seq_path, 'groundtruth.txt'), delimiter=',', ndmin=2)
     elif set_type in ('VisEvent', 'visevent'):
         rgb = sorted(join(seq_path, 'vis_imgs', p) for p in os.listdir(join(seq_path, 'vis_imgs')) if p.endswith('.bmp'))
         aux = sorted(join(seq_path, 'event_imgs', p) for p in os.listdir(join(seq_path, 'event_imgs'))
                      if p.endswith('.bmp'))
-        gt = np.loadtxt(join(seq_path, 'groundtruth.txt'), delimiter=',')
+        gt = np.loadtxt(join(seq_path, 'groundtruth.txt'), delimiter=',', ndmin=2)
         absent = np.loadtxt(join(seq_path, 'absent_label.txt'))
         if absent[0] == 0:   # first frame absent (test_rgbe_mgpus.py:56-61)
             k = int(absent.argmax())
@@ -66,6 +70,21 @@ def synthetic_sequences(n, frames, H=480, W=640, C=6, seed=0):
         fr, gt = synth.make_frames(seed + i, frames, H, W, C, box=box)
         out.append((f"synthetic_{i:03d}", fr, gt))
     return out
+
+
+def default_xtype(dataset_name, script_name='vipt'):
+    """Frame assembly per modality: RGB-T/E aux read as RGB ('rgbrgb', test_rgbt_mgpus.py:98),
+    RGB-D depth JET-colormapped ('rgbcolormap', vipt_class.py:70); the RGB-only OSTrack reads 'color'."""
+    if script_name == 'ostrack':
+        return 'color'
+    return 'rgbcolormap' if dataset_name in ('DepthTrack', 'depthtrack', 'CDTB', 'cdtb') else 'rgbrgb'
+
+
+def synthetic_state_dict(script_name, yaml_name):
+    from mmtrack_amd import synth
+    if script_name == 'ostrack':
+        return synth.make_state_dict(0, kind='ostrack', search_size=384, template_size=192)
+    return synth.make_state_dict(0, kind='vipt', prompt_type='vipt_' + yaml_name.split('_')[0])
 
 
 # ------------------------------------------------------------------ one sequence through the reference-shaped tracker
@@ -92,12 +111,11 @@ def run_sequence(seq_name, seq_home, dataset_name, yaml_name, num_gpu=1, epoch=6
         torch.cuda.set_device(worker_id % num_gpu)
     except Exception:
         pass
-    import lib.test.parameter.vipt as vipt_params
-    from lib.test.tracker.vipt import ViPTTrack
-    params = vipt_params.parameters(yaml_name, epoch)
+    import importlib
+    params = importlib.import_module(f'lib.test.parameter.{script_name}').parameters(yaml_name, epoch)
     for k, v in (params_overrides or {}).items():
         setattr(params, k, v)
-    tracker = ViPTTrack(params)
+    tracker = importlib.import_module(f'lib.test.tracker.{script_name}').get_tracker_class()(params)
     if synthetic is not None:
         frames, gt = synthetic
         get = lambda i: frames[i]
@@ -105,7 +123,7 @@ def run_sequence(seq_name, seq_home, dataset_name, yaml_name, num_gpu=1, epoch=6
     else:
         from lib.train.dataset.depth_utils import get_x_frame
         rgb, aux, gt = gen_config(join(seq_home, seq_name), dataset_name)
-        xtype = getattr(params.cfg.DATA, 'XTYPE', 'rgbrgb')
+        xtype = default_xtype(dataset_name, script_name)
         get = lambda i: get_x_frame(rgb[i], aux[i], dtype=xtype)
         n = len(rgb)
     result = np.zeros((n, 4), dtype=np.float64)
@@ -126,13 +144,14 @@ def run_sequence(seq_name, seq_home, dataset_name, yaml_name, num_gpu=1, epoch=6
 
 
 # ------------------------------------------------------------------ batched engine path
-def run_batched_dataset(seqs, yaml_name, batch, modality, out_root, dataset_name, params_overrides=None):
-    """seqs: list of (name, frames-or-None, gt, loader) ; one engine, `batch` sequences per launch."""
-    import lib.test.parameter.vipt as vipt_params
+def run_batched_dataset(seqs, yaml_name, batch, modality, out_root, dataset_name, params_overrides=None,
+                        script_name='vipt'):
+    """seqs: list of (name, n_frames, frame getter, gt); one engine, `batch` sequences per launch."""
+    import importlib
     from lib.test.tracker.basetracker import current_device, load_net
     from mmtrack_amd import Engine, EngineConfig
     from mmtrack_amd.runner import SeqJob, run_batched
-    params = vipt_params.parameters(yaml_name)
+    params = importlib.import_module(f'lib.test.parameter.{script_name}').parameters(yaml_name)
     for k, v in (params_overrides or {}).items():
         setattr(params, k, v)
     ecfg = EngineConfig.from_cfg(params.cfg, max_batch=batch, precision=getattr(params, 'precision', 'bf16'))
@@ -177,20 +196,20 @@ def main(modality='rgbt', argv=None):
     num_gpus = args.num_gpus if args.num_gpus is not None else max(torch.cuda.device_count(), 1)
     overrides = {'precision': args.precision}
     if args.synthetic_weights:
-        from mmtrack_amd import synth
-        overrides['state_dict'] = synth.make_state_dict(0, kind='vipt', prompt_type='vipt_' + args.yaml_name.split('_')[0])
+        overrides['state_dict'] = synthetic_state_dict(args.script_name, args.yaml_name)
     # sequences
     if args.synthetic:
-        syn = synthetic_sequences(args.synthetic, args.frames)
+        syn = synthetic_sequences(args.synthetic, args.frames, C=3 if args.script_name == 'ostrack' else 6)
         names = [s[0] for s in syn]
     else:
         names = sorted(f for f in os.listdir(args.seq_home) if isdir(join(args.seq_home, f)))
         if args.video:
             names = [args.video]
-    rank, world = int(os.environ.get('RANK', 0)), int(os.environ.get('WORLD_SIZE', 1))
-    if world > 1:
+    from mmtrack_amd.sharding import rank_world, shard_indices
+    rank, world = rank_world()
+    if world > 1 and torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', 0)))
-    mine = [i for i in range(len(names)) if i % world == rank]
+    mine = shard_indices(len(names), rank, world)
     start = time.time()
     if args.batch > 0:
         seqs = []
@@ -201,8 +220,10 @@ def main(modality='rgbt', argv=None):
             else:
                 from lib.train.dataset.depth_utils import get_x_frame
                 rgb, aux, gt = gen_config(join(args.seq_home, names[i]), args.dataset_name)
-                seqs.append((names[i], len(rgb), (lambda r, a: (lambda k: get_x_frame(r[k], a[k], dtype='rgbrgb')))(rgb, aux), gt))
-        run_batched_dataset(seqs, args.yaml_name, args.batch, modality, args.out_root, args.dataset_name, overrides)
+                xt = default_xtype(args.dataset_name, args.script_name)
+                seqs.append((names[i], len(rgb), (lambda r, a: (lambda k: get_x_frame(r[k], a[k], dtype=xt)))(rgb, aux), gt))
+        run_batched_dataset(seqs, args.yaml_name, args.batch, modality, args.out_root, args.dataset_name, overrides,
+                            script_name=args.script_name)
     else:
         jobs = [(names[i], args.seq_home, args.dataset_name, args.yaml_name, num_gpus, args.epoch, args.debug,
                  args.script_name, modality, args.out_root, (syn[i][1], syn[i][2]) if args.synthetic else None, overrides)

@@ -1,0 +1,182 @@
+"""Host-side logic on CPU: config/yaml loading, tracker discovery, result formats, batched-slot
+compaction, dataset layouts, benchmark dispatch (no GPU, no compute calls)."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "multi-modal-trakcing-bechmark_amd")
+
+
+def test_yaml_configs_load():
+    from lib.config.vipt.config import cfg, reset_config, update_config_from_file
+    for name in ("deep_rgbt", "deep_rgbd", "deep_rgbe", "shaw_rgbt", "shaw_rgbd", "shaw_rgbe"):
+        reset_config()
+        update_config_from_file(os.path.join(PKG, "experiments", "vipt", name + ".yaml"))
+        assert cfg.TEST.SEARCH_SIZE == 256 and cfg.TEST.TEMPLATE_SIZE == 128
+        assert cfg.TEST.SEARCH_FACTOR == 4.0 and cfg.TEST.TEMPLATE_FACTOR == 2.0
+        assert cfg.TRAIN.PROMPT.TYPE == "vipt_" + name.split("_")[0]
+        assert list(cfg.MODEL.BACKBONE.CE_LOC) == [3, 6, 9]
+    reset_config()
+    update_config_from_file(os.path.join(PKG, "experiments", "ostrack", "vitb_384_mae_ce_32x4_ep300.yaml"))
+    assert cfg.TEST.SEARCH_SIZE == 384 and cfg.TEST.TEMPLATE_SIZE == 192
+    reset_config()
+
+
+def test_yaml_unknown_key_raises(tmp_path):
+    from lib.config.vipt.config import reset_config, update_config_from_file
+    p = tmp_path / "bad.yaml"
+    p.write_text("MODEL:\n  NOT_A_KEY: 1\n")
+    with pytest.raises(ValueError):
+        update_config_from_file(str(p))
+    reset_config()
+
+
+def test_parameters_and_engine_config():
+    import lib.test.parameter.vipt as vp
+    from mmtrack_amd import EngineConfig
+    p = vp.parameters("deep_rgbt")
+    assert p.search_size == 256 and p.template_factor == 2.0
+    assert p.checkpoint.endswith("ViPT_deep_rgbt.pth")
+    ec = EngineConfig.from_cfg(p.cfg, max_batch=4)
+    assert ec.prompt_type == "deep" or ec.prompt_type in (2, "vipt_deep")
+    assert ec.max_batch == 4
+
+
+def test_tracker_discovery():
+    from lib.test.evaluation.tracker import Tracker
+    t = Tracker("vipt", "deep_rgbt", "LasHeR")
+    assert t.tracker_class is not None and t.tracker_class.__name__ == "ViPTTrack"
+    assert t.results_dir.endswith(os.path.join("vipt", "deep_rgbt"))
+    assert Tracker("no_such_tracker", "x", "LasHeR").tracker_class is None
+
+
+def test_result_writers(tmp_path):
+    from lib.test.evaluation.running import _save_tracker_output
+
+    class Seq:
+        dataset, name = "lasher", "seqA"
+
+    class Tr:
+        results_dir = str(tmp_path / "res")
+
+    out = {"target_bbox": [[1.7, 2.2, 30.9, 40.1], [3.0, 4.0, 5.5, 6.5]], "time": [0.5, 0.25],
+           "all_scores": [1, 0.876]}
+    _save_tracker_output(Seq(), Tr(), out)
+    assert (tmp_path / "res" / "seqA.txt").read_text() == "1\t2\t30\t40\n3\t4\t5\t6\n"
+    assert (tmp_path / "res" / "seqA_time.txt").read_text() == "0.500000\n0.250000\n"
+    assert (tmp_path / "res" / "seqA_all_scores.txt").read_text() == "1.00\n0.88\n"
+
+
+def test_workspace_result_formats(tmp_path):
+    from mmtrack_amd.workspace import save_result
+    r = np.array([[1.5, 2.25, 3.0, 4.125]])
+    save_result(tmp_path / "t.txt", r, "rgbt")
+    assert (tmp_path / "t.txt").read_text() == "1.500000000000000000e+00 2.250000000000000000e+00 " \
+                                               "3.000000000000000000e+00 4.125000000000000000e+00\n"
+    save_result(tmp_path / "e.txt", r, "rgbe")
+    assert (tmp_path / "e.txt").read_text() == "1.50000000000000,2.25000000000000,3.00000000000000,4.12500000000000\n"
+
+
+def test_gen_config_layouts(tmp_path):
+    from mmtrack_amd.workspace import gen_config
+    s = tmp_path / "lasher_seq"
+    (s / "visible").mkdir(parents=True)
+    (s / "infrared").mkdir()
+    for i in range(3):
+        (s / "visible" / f"{i:05d}.jpg").write_bytes(b"")
+        (s / "infrared" / f"{i:05d}.jpg").write_bytes(b"")
+    np.savetxt(s / "visible.txt", np.ones((3, 4)), delimiter=",")
+    rgb, aux, gt = gen_config(str(s), "LasHeR")
+    assert len(rgb) == len(aux) == 3 and gt.shape == (3, 4)
+    g = tmp_path / "gtot_seq"
+    (g / "v").mkdir(parents=True)
+    (g / "i").mkdir()
+    (g / "v" / "a.png").write_bytes(b"")
+    (g / "i" / "a.png").write_bytes(b"")
+    np.savetxt(g / "groundTruth_v.txt", np.array([[10, 20, 50, 80]]), delimiter=" ")
+    _, _, gt = gen_config(str(g), "GTOT")
+    assert gt.tolist() == [[10, 20, 40, 60]]          # x1 y1 x2 y2 -> x y w h
+    v = tmp_path / "ve_seq"
+    (v / "vis_imgs").mkdir(parents=True)
+    (v / "event_imgs").mkdir()
+    for i in range(4):
+        (v / "vis_imgs" / f"{i:04d}.bmp").write_bytes(b"")
+        (v / "event_imgs" / f"{i:04d}.bmp").write_bytes(b"")
+    np.savetxt(v / "groundtruth.txt", np.arange(16).reshape(4, 4), delimiter=",")
+    np.savetxt(v / "absent_label.txt", np.array([0, 0, 1, 1]))
+    rgb, aux, gt = gen_config(str(v), "VisEvent")   # leading absent frames dropped
+    assert len(rgb) == 2 and gt[0].tolist() == [8, 9, 10, 11]
+    with pytest.raises(ValueError):
+        gen_config(str(v), "NoSuchSet")
+
+
+class _FakeEngine:
+    """Records slot occupancy; box(t) = init + t so results show whether slots were mixed up."""
+
+    def __init__(self):
+        self.slot = {}
+
+    def initialize(self, slot, frame, box):
+        name, t = frame
+        assert t == 0
+        self.slot[slot] = [name, list(box)]
+
+    def set_state(self, slot, state):
+        self.slot[slot][1] = list(state)
+
+    def track_batch(self, first, frames):
+        boxes, scores = [], []
+        for k, (name, t) in enumerate(frames):
+            entry = self.slot[first + k]
+            assert entry[0] == name, "frame routed to the wrong slot"
+            entry[1] = [entry[1][0] + 1.0] + entry[1][1:]
+            boxes.append(list(entry[1]))
+            scores.append(0.5)
+        return np.array(boxes), np.array(scores, dtype=np.float32)
+
+
+@pytest.mark.parametrize("batch", [1, 2, 3, 8])
+def test_run_batched_slot_compaction(batch):
+    from mmtrack_amd.runner import SeqJob, run_batched
+    lens = [5, 2, 9, 3, 3, 7, 1 + 1, 4]
+    jobs = [SeqJob(f"s{i}", n, (lambda nm: (lambda t: (nm, t)))(f"s{i}"), [float(i), 0, 10, 10])
+            for i, n in enumerate(lens)]
+    done = []
+    run_batched(_FakeEngine(), jobs, batch, on_done=lambda j: done.append(j.name))
+    assert sorted(done) == sorted(j.name for j in jobs)
+    for i, j in enumerate(jobs):
+        assert j.boxes[:, 0].tolist() == [i + t for t in range(j.n_frames)]
+
+
+def test_sharding():
+    from mmtrack_amd.sharding import shard, shard_indices
+    assert shard_indices(10, 1, 4) == [1, 5, 9]
+    items = list("abcdefg")
+    parts = [shard(items, r, 3) for r in range(3)]
+    assert sorted(sum(parts, [])) == items
+    with pytest.raises(ValueError):
+        shard_indices(3, 2, 2)
+
+
+def test_benchmark_dispatch(tmp_path):
+    from mmtrack_amd.benchmark import run
+    reg = {"ok": (".", [sys.executable, "-c", "import sys; open('ran.txt','w').write(' '.join(sys.argv[1:]))"]),
+           "fail": (".", [sys.executable, "-c", "raise SystemExit(3)"])}
+    tc = run(str(tmp_path), reg, ["--out", str(tmp_path / "tc.json"), "--", "--x", "1"])
+    assert set(tc) == {"ok", "fail"} and all(v >= 0 for v in tc.values())
+    assert (tmp_path / "ran.txt").read_text() == "--x 1"
+    assert json.load(open(tmp_path / "tc.json")).keys() == tc.keys()
+    with pytest.raises(ValueError):
+        run(str(tmp_path), reg, ["--trackers", "nope"])
+
+
+@pytest.mark.parametrize("mod", ["RGBT", "RGBE", "RGBD"])
+def test_benchmark_scripts_dry_run(mod):
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(PKG, mod, "benchmark.py"), "--dry_run"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "[benchmark]" in r.stdout
