@@ -112,6 +112,18 @@ int mmt_timing_read(mmt_engine* e, int* launches, double* total_ms, double* flop
 int mmt_xcorr(const float* z, const float* x, float* out, int B, int C, int hz, int wz, int hx, int wx,
               float scale, float bias, void* hip_stream);
 
+/* SiamFC per-frame steps around the correlation (TrackerSiamFC.init/update, published SiamFC; the
+ * reference's RGBE/models/siamfc is an empty submodule):
+ *   mmt_siamfc_crop: n <= 8 square windows (top-left y0/x0, side) of a device H x W x C uint8 frame,
+ *     constant border pad[3], cv2 INTER_LINEAR resize to out_sz -> out [n][3][out_sz][out_sz] float;
+ *   mmt_siamfc_response: resp [n][r][r] -> INTER_CUBIC to up x up, scale penalty on scales != n/2,
+ *     best scale, normalise, blend with outer(hann1d, hann1d)/hann_sum by window_influence, argmax;
+ *     result (device) [4] = scale id, row, col, value; scratch: n*up*up floats (device).           */
+int mmt_siamfc_crop(const uint8_t* frame, int H, int W, int C, int64_t row_stride, int n, const int* y0,
+                    const int* x0, const int* size, const int pad[3], int out_sz, float* out, void* hip_stream);
+int mmt_siamfc_response(const float* resp, int n, int r, int up, float scale_penalty, double window_influence,
+                        const double* hann1d, double hann_sum, float* scratch, float* result, void* hip_stream);
+
 /* ---- DiMP / mfDiMP target classifier (device pointers, fp32) ------------------------------------
  *  feat [I][S][C][H][W] (I training images x S sequences), filter [S][C][fh][fw] (fh*fw <= 25).
  *  mmt_dimp_optimize runs num_iter steepest-descent Gauss-Newton steps in place on `weights`

@@ -1126,6 +1126,51 @@ int mmt_xcorr(const float* z, const float* x, float* out, int B, int Cc, int hz,
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 
+int mmt_siamfc_crop(const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride, int n, const int* y0,
+                    const int* x0, const int* size, const int pad[3], int out_sz, float* out, void* stream) {
+  if (!frame || !out || !y0 || !x0 || !size || !pad || n <= 0 || n > 8 || Hh <= 0 || Ww <= 0 || Cc < 3 ||
+      row_stride < (int64_t)Ww * Cc || out_sz <= 0)
+    return MMT_E_ARG;
+  SiamCropArgs a{};
+  a.frame = frame;
+  a.stride = row_stride;
+  a.H = Hh;
+  a.W = Ww;
+  a.C = Cc;
+  a.n = n;
+  a.out_sz = out_sz;
+  for (int i = 0; i < n; ++i) {
+    if (size[i] < 1) return MMT_E_ARG;
+    a.y0[i] = y0[i];
+    a.x0[i] = x0[i];
+    a.size[i] = size[i];
+  }
+  for (int c = 0; c < 3; ++c) a.pad[c] = std::min(std::max(pad[c], 0), 255);
+  a.out = out;
+  siamfc_crop(a, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_siamfc_response(const float* resp, int n, int r, int up, float scale_penalty, double window_influence,
+                        const double* hann1d, double hann_sum, float* scratch, float* result, void* stream) {
+  if (!resp || !hann1d || !scratch || !result || n <= 0 || n > 8 || r <= 1 || up < 2 || hann_sum <= 0)
+    return MMT_E_ARG;
+  SiamRespArgs a{};
+  a.resp = resp;
+  a.n = n;
+  a.r = r;
+  a.up = up;
+  a.penalty = scale_penalty;
+  a.one_minus_wi = (float)(1.0 - window_influence);
+  a.wi = window_influence;
+  a.hann_sum = hann_sum;
+  a.hann1d = hann1d;
+  a.scratch = scratch;
+  a.result = result;
+  siamfc_response(a, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
 int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, void* Cp, int64_t ldc,
                 const float* R, int64_t ldr, int M, int N, int K, int epi, int conv_hw, int conv_cin, int pos_rows,
                 void* stream) {

@@ -6,8 +6,7 @@
 //  * decode: the CENTER head's conv5 1x1 + sigmoid/clamp (head.py:110-124, 177-201), the Hann window
 //    (vipt.py:79-80) and cal_bbox's first-occurrence argmax + gather (head.py:142-160);
 //  * xcorr: SiamFC / DiMP per-sequence cross-correlation (grouped conv2d).
-#include <float.h>
-
+#include "cvresize.h"
 #include "kernels.h"
 
 namespace mmt {
@@ -30,36 +29,8 @@ __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= O * O) return;
   const int oy = idx / O, ox = idx - oy * O;
-  const int S = p.crop_sz;
-  const double scale = 1.0 / ((double)O / (double)S);
   int u8[6];
-  if (fabs(scale - 2.0) < DBL_EPSILON) {
-    // cv::resize reroutes an exact 2x down-scale to INTER_AREA's fast path
-    for (int c = 0; c < a.C; ++c) {
-      const int s = crop_px(p, 2 * oy, 2 * ox, c) + crop_px(p, 2 * oy, 2 * ox + 1, c) +
-                    crop_px(p, 2 * oy + 1, 2 * ox, c) + crop_px(p, 2 * oy + 1, 2 * ox + 1, c);
-      u8[c] = (s + 2) >> 2;
-    }
-  } else {
-    float fx = (float)((ox + 0.5) * scale - 0.5);
-    int sx = (int)floorf(fx);
-    fx -= (float)sx;
-    if (sx < 0) { fx = 0.f; sx = 0; }
-    if (sx >= S - 1) { fx = 0.f; sx = S - 1; }
-    const int a0 = __float2int_rn((1.f - fx) * 2048.f), a1 = __float2int_rn(fx * 2048.f);
-    float fy = (float)((oy + 0.5) * scale - 0.5);
-    const int sy = (int)floorf(fy);
-    fy -= (float)sy;
-    const int b0 = __float2int_rn((1.f - fy) * 2048.f), b1 = __float2int_rn(fy * 2048.f);
-    const int r0 = min(max(sy, 0), S - 1), r1 = min(max(sy + 1, 0), S - 1);
-    const int sx1 = min(sx + 1, S - 1);
-    for (int c = 0; c < a.C; ++c) {
-      const int d0 = crop_px(p, r0, sx, c) * a0 + crop_px(p, r0, sx1, c) * a1;
-      const int d1 = crop_px(p, r1, sx, c) * a0 + crop_px(p, r1, sx1, c) * a1;
-      const int v = (((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16);
-      u8[c] = min(max((v + 2) >> 2, 0), 255);
-    }
-  }
+  cv_linear_u8([&](int r, int x, int c) { return crop_px(p, r, x, c); }, p.crop_sz, O, oy, ox, a.C, u8);
   const int np = O / 16;
   const int patch = (oy >> 4) * np + (ox >> 4);
   const int within = (oy & 15) * 16 + (ox & 15);

@@ -154,4 +154,27 @@ void decode(const DecodeArgs& a, hipStream_t s);
 void xcorr(const float* Z, const float* X, float* out, int B, int C, int hz, int wz, int hx, int wx, float scale,
            float bias, hipStream_t s);
 
+// ---- SiamFC (siamfc.hip)
+struct SiamCropArgs {
+  const uint8_t* frame;            // H x W x C uint8 (C >= 3; the first 3 channels are used)
+  int64_t stride;
+  int H, W, C;
+  int n, out_sz;                   // crops, output side
+  int y0[8], x0[8], size[8];       // window corner (may lie outside the frame) and side, per crop
+  int pad[3];                      // border colour (cv2 Scalar -> uint8)
+  float* out;                      // [n][3][out_sz][out_sz]
+};
+void siamfc_crop(const SiamCropArgs& a, hipStream_t s);
+
+struct SiamRespArgs {
+  const float* resp;               // [n][r][r]
+  int n, r, up;                    // scales, response side, upsampled side
+  float penalty, one_minus_wi;
+  double wi, hann_sum;             // cosine window = outer(hann1d, hann1d) / hann_sum (np.hanning, float64)
+  const double* hann1d;            // [up] (device)
+  float* scratch;                  // [n][up][up]
+  float* result;                   // [4] scale id, row, col, windowed response max
+};
+void siamfc_response(const SiamRespArgs& a, hipStream_t s);
+
 }  // namespace mmt

@@ -187,6 +187,43 @@ def make_state_dict(seed: int = 0, **shape_kw) -> "OrderedDict[str, torch.Tensor
     return sd
 
 
+SIAMFC_LAYERS = [  # AlexNetV1 (siamfc backbone): (name, out, in/groups, k, has_bn)
+    ("conv1", 96, 3, 11, True), ("conv2", 256, 48, 5, True), ("conv3", 384, 256, 3, True),
+    ("conv4", 384, 192, 3, True), ("conv5", 256, 192, 3, False)]
+
+
+def siamfc_shapes():
+    """TrackerSiamFC Net(backbone=AlexNetV1, head=SiamFC) state_dict layout (head has no parameters)."""
+    shp = OrderedDict()
+    for name, co, ci, k, bn in SIAMFC_LAYERS:
+        shp[f"backbone.{name}.0.weight"] = (co, ci, k, k)
+        shp[f"backbone.{name}.0.bias"] = (co,)
+        if bn:
+            for t in ("weight", "bias", "running_mean", "running_var"):
+                shp[f"backbone.{name}.1.{t}"] = (co,)
+            shp[f"backbone.{name}.1.num_batches_tracked"] = ()
+    return shp
+
+
+def make_siamfc_state_dict(seed: int = 0) -> "OrderedDict[str, torch.Tensor]":
+    sd = OrderedDict()
+    for k, shp in siamfc_shapes().items():
+        g = _gen(seed, k)
+        if k.endswith("num_batches_tracked"):
+            v = torch.tensor(0, dtype=torch.int64)
+        elif k.endswith(".0.weight"):
+            fan_in = shp[1] * shp[2] * shp[3]
+            v = torch.randn(shp, generator=g) * math.sqrt(2.0 / fan_in) * (0.02 if "conv1." in k else 1.0)
+        elif k.endswith(".1.weight"):
+            v = torch.rand(shp, generator=g) * 0.4 + 0.8
+        elif k.endswith("running_var"):
+            v = torch.rand(shp, generator=g) + 0.5
+        else:
+            v = torch.randn(shp, generator=g) * 0.05
+        sd[k] = v.contiguous()
+    return sd
+
+
 # ----------------------------------------------------------------------------- frames
 def make_frames(seed: int, n: int, H: int = 480, W: int = 640, C: int = 6,
                 box=(300.0, 200.0, 40.0, 30.0), drift=(1.5, 0.75)):

@@ -112,3 +112,35 @@ def test_oracle_dimp_matches_reference():
     w, iters, losses = od.steepest_descent_gn(filt, feat, bb, sd, num_iter=5)
     np.testing.assert_allclose(torch.stack(iters).numpy(), g["iterates"], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(torch.stack(losses).numpy().ravel(), g["losses"], rtol=1e-4)
+
+
+def test_cubic_resize_oracle_properties():
+    """cv2 INTER_CUBIC restatement (oracle/siamfc.py): constants stay constant (the A = -0.75 kernel is a
+    partition of unity) and the float32 result
+    matches an independent float64 evaluation of the same separable kernel."""
+    from oracle import siamfc as osf
+    c = np.full((17, 17), 3.25, np.float32)
+    np.testing.assert_allclose(osf.cv2_resize_cubic_f32(c, 272), 3.25, rtol=1e-6)
+    rng = np.random.default_rng(0)
+    src = rng.standard_normal((17, 17)).astype(np.float32)
+
+    def kern(t):
+        a = -0.75
+        t = abs(t)
+        return ((a + 2) * t - (a + 3)) * t * t + 1 if t <= 1 else (((t - 5) * t + 8) * t - 4) * a if t < 2 else 0.0
+
+    ref = np.zeros((272, 272))
+    for oy in range(0, 272, 7):
+        fy = (oy + 0.5) / 16 - 0.5
+        sy = int(np.floor(fy))
+        for ox in range(0, 272, 5):
+            fx = (ox + 0.5) / 16 - 0.5
+            sx = int(np.floor(fx))
+            v = 0.0
+            for i in range(4):
+                for j in range(4):
+                    yy, xx = min(max(sy + i - 1, 0), 16), min(max(sx + j - 1, 0), 16)
+                    v += src[yy, xx] * kern(fy - (sy + i - 1)) * kern(fx - (sx + j - 1))
+            ref[oy, ox] = v
+    got = osf.cv2_resize_cubic_f32(src, 272)
+    np.testing.assert_allclose(got[::7, ::5], ref[::7, ::5], atol=2e-5)
