@@ -31,7 +31,7 @@ __device__ __forceinline__ float wave_max(float v) {
 // with erfc from the Chebyshev-fitted form of Numerical Recipes' erfcc (fractional error < 1.2e-7
 // everywhere).  For x < 0 it is x * erfc(|x|/sqrt2) / 2 directly, so there is no cancellation.
 __device__ __forceinline__ float erfc_pos(float z) {   // z >= 0
-  const float t = __frcp_rn(1.0f + 0.5f * z);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * z);   // v_rcp_f32 (1 ulp); __frcp_rn is a full IEEE divide
   const float p = -1.26551223f + t * (1.00002368f + t * (0.37409196f + t * (0.09678418f + t * (-0.18628806f +
                   t * (0.27886807f + t * (-1.13520398f + t * (1.48851587f + t * (-0.82215223f + t * 0.17087277f))))))));
   return t * __expf(-z * z + p);

@@ -7,7 +7,7 @@
 // token map) all have this shape: activations [tokens x K] and weights [out x K], K-contiguous.
 //
 // * tiles BM x BN x 64; 4 or 8 waves, each a 64x64 (or smaller) block of v_mfma_f32_16x16x32_bf16;
-// * operands move HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR staging); each wave-
+// * operands move HBM/L2 -> LDS with buffer_load_dwordx4 ... lds (no VGPR staging); each wave-
 //   instruction fills 8 LDS rows of 128 B; the 16-B chunks are XOR-swizzled by row (chunk ^ (row&7))
 //   by pre-swizzling the per-lane SOURCE address, so the fragment ds_read_b128s are conflict-free;
 // * two LDS stages: the loads of K-tile k+1 are in flight while tile k is multiplied;
@@ -24,7 +24,6 @@ namespace mmt {
 
 __device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((c ^ (r & 7)) << 3); }
 
-typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
 template <int BM, int BN, int WMW, int WNW, bool SPLIT, int STAGES = 0>
@@ -41,13 +40,22 @@ struct Tile {
   static_assert(GROUPS % NW == 0, "row groups must divide over waves");
 };
 
-// logical tile id -> (tm, tn): column-group-major with Wc tile columns per group, tm-major inside
-__device__ __forceinline__ void tile_of(int id, int tiles_m, int tiles_n, int wc, int& tm, int& tn) {
-  const int per = tiles_m * wc;
+// logical tile id -> (tm, tn): super-tiles of gm tile-rows x all tile-columns, column-major inside,
+// so any 64 consecutive ids cover a ~8 x 8 block of output tiles (A and W slices that fit one L2)
+__device__ __forceinline__ void tile_of(int id, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  const int per = gm * tiles_n;
   const int grp = id / per, rem = id - grp * per;
-  const int width = min(wc, tiles_n - grp * wc);
-  tm = rem / width;
-  tn = grp * wc + (rem - tm * width);
+  const int first = grp * gm;
+  const int h = min(gm, tiles_m - first);
+  tn = rem / h;
+  tm = first + (rem - tn * h);
+}
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
+  // raw buffer: stride 0, num_records = bytes (loads past it return 0), gfx9 dword3
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)min(bytes, (int64_t)0x7fffffff),
+                                           0x00020000);
 }
 
 template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int STAGES>
@@ -56,79 +64,90 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   __shared__ __attribute__((aligned(16))) bf16_t smem[T::NSTAGE * T::STAGE];
 
   const GemmGroup& g = args.g[blockIdx.z];
-  const int M = args.M, N = args.N, K = args.K;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN, ntiles = tiles_m * tiles_n;
+  const int M = args.M, K = args.K;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = args.N / BN, ntiles = tiles_m * tiles_n;
   // XCD-aware remap (bijective): blocks b, b+8, ... (one XCD) take a contiguous logical range
   const int b = blockIdx.x, x = b & 7, j = b >> 3;
   const int q = ntiles >> 3, r8 = ntiles & 7;
   const int id = (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + j;
   int tm, tn;
-  tile_of(id, tiles_m, tiles_n, args.wc, tm, tn);
+  tile_of(id, tiles_m, tiles_n, args.gm, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WNW, wn = wave % WNW;
 
-  // ---- per-lane source rows of this wave's load groups (fixed over K)
+  // ---- loads: buffer_load ... lds with per-lane VGPR offsets fixed over K and the K advance in the
+  // SGPR soffset; rows past M fall outside the A resource and read as zero.  Row block i of the
+  // tile (rows [i*RPI, (i+1)*RPI)) lies in one operand region, known at compile time.
   constexpr int GPW = T::GROUPS / T::NW;
-  const bf16_t* src[GPW];
-  int64_t conv_pix[GPW];   // A_CONV3: base pixel row (b*plane + y*hw + x) or -1, y/x packed
-  int conv_yx[GPW];
+  constexpr int RPI = T::NW * 8;
+  static_assert(BM % RPI == 0 && BN % RPI == 0, "row blocks must not straddle operands");
+  const int chunk = ((lane & 7) ^ (lane >> 3)) * 16;   // XOR swizzle of the 16-B chunk (row & 7 == lane >> 3)
+  const int64_t a_rows = AM == A_DENSE ? (int64_t)(M - m0) : (int64_t)M;
+  const rsrc_t rA = make_rsrc(AM == A_DENSE ? g.A + (int64_t)m0 * g.lda : g.A, a_rows * g.lda * 2);
+  const rsrc_t rAl = SPLIT ? make_rsrc(AM == A_DENSE ? g.A_lo + (int64_t)m0 * g.lda : g.A_lo, a_rows * g.lda * 2) : rA;
+  const rsrc_t rW = make_rsrc(g.W + (int64_t)n0 * g.ldw, (int64_t)BN * g.ldw * 2);
+  const rsrc_t rWl = SPLIT ? make_rsrc(g.W_lo + (int64_t)n0 * g.ldw, (int64_t)BN * g.ldw * 2) : rW;
+  uint32_t voff[GPW];
+  int conv_b[GPW], conv_y[GPW], conv_x[GPW];   // A_CONV3: map index, pixel of the output row (-1: tail)
 #pragma unroll
   for (int i = 0; i < GPW; ++i) {
-    const int grp = wave + i * T::NW;
-    const int row = grp * 8 + (lane >> 3);
-    const bf16_t* p = args.zero;
-    conv_pix[i] = -1;
-    conv_yx[i] = 0;
-    if (row < T::AROWS) {
-      const int lr = SPLIT ? (row % BM) : row;
-      const bool lo = SPLIT && row >= BM;
-      const int m = m0 + lr;
-      if (m < M) {
-        if (AM == A_DENSE) {
-          p = (lo ? g.A_lo : g.A) + (int64_t)m * g.lda;
-        } else {
+    const int r0 = i * RPI;                              // compile-time after unrolling
+    const int row = r0 + wave * 8 + (lane >> 3);
+    conv_b[i] = -1;
+    conv_y[i] = conv_x[i] = 0;
+    if (r0 < T::AROWS) {
+      const int lr = (SPLIT && r0 >= BM) ? row - BM : row;
+      voff[i] = (uint32_t)(lr * g.lda * 2 + chunk);
+      if (AM == A_CONV3) {
+        const int m = m0 + lr;
+        if (m < M) {
           const int hw = args.conv_hw, plane = hw * hw;
-          const int bi = m / plane, pp = m - bi * plane;
-          const int y = pp / hw, xx = pp - y * hw;
-          conv_pix[i] = (int64_t)bi * plane;
-          conv_yx[i] = (y << 16) | xx;
-          p = lo ? g.A_lo : g.A;
+          conv_b[i] = m / plane;
+          const int pp = m - conv_b[i] * plane;
+          conv_y[i] = pp / hw;
+          conv_x[i] = pp - conv_y[i] * hw;
         }
       }
     } else {
       const int wr = row - T::AROWS;
-      const int lr = SPLIT ? (wr % BN) : wr;
-      const bool lo = SPLIT && wr >= BN;
-      p = (lo ? g.W_lo : g.W) + (int64_t)(n0 + lr) * g.ldw;
+      const int lr = (SPLIT && wr >= BN) ? wr - BN : wr;
+      voff[i] = (uint32_t)(lr * g.ldw * 2 + chunk);
     }
-    src[i] = p;
   }
 
   auto issue = [&](int kt, int stage) {
     const int k0 = kt * 64;
     bf16_t* sbase = smem + stage * T::STAGE;
+    int tap = 0, ch = 0, dy = 0, dx = 0;
+    if (AM == A_CONV3) {
+      tap = k0 / args.conv_cin;
+      ch = k0 - tap * args.conv_cin;
+      dy = tap / 3 - 1;
+      dx = tap % 3 - 1;
+    }
 #pragma unroll
     for (int i = 0; i < GPW; ++i) {
-      const int grp = wave + i * T::NW;
-      const int row = grp * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (row & 7);
-      const bf16_t* p = src[i];
-      if (p != args.zero) {
-        if (AM == A_CONV3 && row < T::AROWS) {
-          const int hw = args.conv_hw, cin = args.conv_cin;
-          const int tap = k0 / cin, ch = k0 - tap * cin;
-          const int ky = tap / 3, kx = tap - ky * 3;
-          const int y = (conv_yx[i] >> 16) + ky - 1, xx = (conv_yx[i] & 0xffff) + kx - 1;
-          if (y >= 0 && y < hw && xx >= 0 && xx < hw)
-            p = p + (conv_pix[i] + y * hw + xx) * g.lda + ch + c * 8;
-          else
-            p = args.zero;
+      const int r0 = i * RPI;
+      lptr_t dst = (lptr_t)(sbase + (r0 + wave * 8) * 64);
+      if (r0 < T::AROWS) {
+        const rsrc_t rs = (SPLIT && r0 >= BM) ? rAl : rA;
+        if (AM == A_CONV3) {
+          const int hw = args.conv_hw;
+          const int y = conv_y[i] + dy, xx = conv_x[i] + dx;
+          const bool ok = conv_b[i] >= 0 && y >= 0 && y < hw && xx >= 0 && xx < hw;
+          const uint32_t vo = ok ? (uint32_t)((((conv_b[i] * hw + y) * hw + xx) * g.lda + ch) * 2 + chunk)
+                                 : 0x80000000u;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, vo, 0, 0, 0);
         } else {
-          p = p + k0 + c * 8;
+          const uint32_t vo = voff[i];   // (a subscript directly in the builtin drops the host stub)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, vo, k0 * 2, 0, 0);
         }
+      } else {
+        const rsrc_t rs = (SPLIT && r0 >= T::AROWS + BN) ? rWl : rW;
+        const uint32_t vo = voff[i];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, vo, k0 * 2, 0, 0);
       }
-      __builtin_amdgcn_global_load_lds((gptr_t)p, (lptr_t)(sbase + grp * 8 * 64), 16, 0, 0);
     }
   };
 
@@ -244,13 +263,8 @@ template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int ST>
 static void launch_one(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.N / BN;
-  // column-group width: ~tiles_n/8 columns per XCD when there are enough W tiles, else whole rows
-  int wc = tiles_n;
-  if (tiles_n >= 8) {
-    wc = tiles_n / 8;
-    while (tiles_n % wc) --wc;
-  }
-  a.wc = wc;
+  (void)tiles_n;
+  a.gm = tiles_m < 8 ? tiles_m : 8;
   dim3 grid(tiles_m * tiles_n, 1, a.groups);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI, AM, SPLIT, ST>), grid, dim3(WMW * WNW * 64), 0, s, a);
 }

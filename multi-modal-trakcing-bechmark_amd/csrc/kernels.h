@@ -37,8 +37,8 @@ struct GemmArgs {
   int conv_cin;     // A_CONV3: input channels (multiple of 64)
   int pos_rows;     // EPI_POS_F32
   int split;        // 1: fp32-faithful bf16x3 products
-  int wc;           // (set by the launcher) tile columns per XCD group
-  const bf16_t* zero;   // >= 16 zero bytes (source of padding / tail rows)
+  int gm;           // (set by the launcher) tile rows per super-tile group of the tile order
+  const bf16_t* zero;   // unused by the buffer-load kernels (kept for ABI stability of the struct)
 };
 
 void gemm(const GemmArgs& a, int epi, hipStream_t s);

@@ -6,7 +6,22 @@ from mmtrack_amd import _lib
 lib = _lib.load()
 B = int(os.environ.get("B", "32"))
 shapes = {"fc1": (B * 320, 3072, 768, 1), "qkv": (B * 320, 2304, 768, 0), "fc2": (B * 320, 768, 3072, 2),
-          "proj": (B * 320, 768, 768, 2)}
+          "proj": (B * 320, 768, 768, 2), "sq4k": (4096, 4096, 4096, 0)}
+if os.environ.get("SHAPES"):
+    shapes = {k: v for k, v in shapes.items() if k in os.environ["SHAPES"].split(",")}
+CFGS = [int(c) for c in os.environ.get("CFGS", "-1,1,2,3,4,5,6,7,8").split(",")]
+
+
+def time_it(fn, n=20):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3
 s = torch.cuda.current_stream().cuda_stream
 for name, (M, N, K, epi) in shapes.items():
     A = torch.randn(M, K, device="cuda").bfloat16()
@@ -14,7 +29,11 @@ for name, (M, N, K, epi) in shapes.items():
     bias = torch.randn(N, device="cuda")
     C = torch.empty(M, N, device="cuda", dtype=torch.float32 if epi == 2 else torch.bfloat16)
     ref = None
-    for cfg in [-1, 1, 2, 3, 4, 5, 6, 7, 8]:
+    # library reference on the same operands (hipBLASLt through torch; bias, no fused epilogue)
+    us = 0.0 if os.environ.get("NO_TORCH") else time_it(lambda: torch.nn.functional.linear(A, W, bias.bfloat16()))
+    if us > 0:
+        print(f"{name:5s} M={M} N={N} K={K} torch/hipBLASLt: {us:8.1f} us  {2*M*N*K/us/1e6:7.1f} TFLOP/s", flush=True)
+    for cfg in CFGS:
         lib.mmt_gemm_force_config(cfg)
         def run():
             lib.mmt_op_gemm(A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr(), C.data_ptr(), N,
