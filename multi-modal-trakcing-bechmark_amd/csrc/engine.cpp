@@ -1195,6 +1195,8 @@ int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const fl
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 
+int mmt_gemm_stamps(void* dev_buf) { return gemm_set_stamps(dev_buf) == 0 ? MMT_OK : MMT_E_HIP; }
+
 int mmt_gemm_force_config(int cfg) {
   gemm_force_config(cfg);
   return MMT_OK;

@@ -18,6 +18,8 @@
 //   acc += Wh*Ah + Wl*Ah + Wh*Al  (relative error ~1e-5, vs ~2e-3 for plain bf16);
 // * the MFMA is issued W-fragment x A-fragment, so a lane ends with 4 consecutive output columns
 //   of one row: 8-B (bf16) / 16-B (fp32) epilogue stores.
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace mmt {
@@ -51,12 +53,124 @@ __device__ __forceinline__ void tile_of(int id, int tiles_m, int tiles_n, int gm
   tm = first + (rem - tn * h);
 }
 
+// optional per-block cycle stamps (tuning: mmt_gemm_stamps); null in production
+__device__ unsigned long long* g_gemm_stamps = nullptr;
+#define GEMM_STAMP(k)                                                                      \
+  do {                                                                                     \
+    if (g_gemm_stamps && threadIdx.x == 0)                                                 \
+      g_gemm_stamps[(size_t)blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memtime();          \
+  } while (0)
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
   // raw buffer: stride 0, num_records = bytes (loads past it return 0), gfx9 dword3
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)min(bytes, (int64_t)0x7fffffff),
                                            0x00020000);
 }
+
+// fused epilogue for one lane's 4 consecutive outputs C[m][n..n+3]
+template <int EPI, bool SPLIT>
+__device__ __forceinline__ void store4(const GemmGroup& g, const GemmArgs& args, int m, int n, const f32x4& a) {
+  const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float v[4] = {a[0] + bv.x, a[1] + bv.y, a[2] + bv.z, a[3] + bv.w};
+  if (EPI == EPI_GELU_BF16)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+  if (EPI == EPI_RELU_BF16 || EPI == EPI_RELU_F32)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+  const int64_t off = (int64_t)m * g.ldc + n;
+  if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
+    bf16_t h[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) h[e] = f2bf(v[e]);
+    uint2 o;
+    o.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+    o.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+    *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C) + off) = o;
+    if (SPLIT && g.C_lo) {
+      uint2 lo;
+      lo.x = (uint32_t)f2bf(v[0] - bf2f(h[0])) | ((uint32_t)f2bf(v[1] - bf2f(h[1])) << 16);
+      lo.y = (uint32_t)f2bf(v[2] - bf2f(h[2])) | ((uint32_t)f2bf(v[3] - bf2f(h[3])) << 16);
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C_lo) + off) = lo;
+    }
+  } else {
+    float4 o = make_float4(v[0], v[1], v[2], v[3]);
+    if (EPI == EPI_RESID_F32) {
+      const float4 rr = *reinterpret_cast<const float4*>(g.R + (int64_t)m * g.ldr + n);
+      o = make_float4(rr.x + v[0], rr.y + v[1], rr.z + v[2], rr.w + v[3]);
+    } else if (EPI == EPI_POS_F32) {
+      const float4 rr = *reinterpret_cast<const float4*>(g.R + (int64_t)(m % args.pos_rows) * g.ldr + n);
+      o = make_float4(v[0] + rr.x, v[1] + rr.y, v[2] + rr.z, v[3] + rr.w);
+    }
+    *reinterpret_cast<float4*>(static_cast<float*>(g.C) + off) = o;
+  }
+}
+
+
+// ---- LDS-staged epilogue: bias + activation per lane, the tile goes through LDS ([rows][COLS],
+// 16-B chunks XOR-swizzled by row so the fragment-shaped writes are conflict-free), then every lane
+// stores 16 contiguous bytes of a row (whole 128-B lines per wave instruction) -- fragment-shaped
+// 8-B stores scattered over 16 rows are store-issue bound.  The fp32 epilogues add R while streaming.
+constexpr bool epi_is_bf16(int e) { return e == EPI_BF16 || e == EPI_GELU_BF16 || e == EPI_RELU_BF16; }
+
+template <int EPI>
+__device__ __forceinline__ void epi_values(const GemmGroup& g, int n, const f32x4& a, float* v) {
+  const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  v[0] = a[0] + bv.x;
+  v[1] = a[1] + bv.y;
+  v[2] = a[2] + bv.z;
+  v[3] = a[3] + bv.w;
+  if (EPI == EPI_GELU_BF16)   // the LDS epilogue serves the bf16 mode only (split keeps store4 + gelu_erf)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gelu_erf_bf16out(v[e]);
+  if (EPI == EPI_RELU_BF16 || EPI == EPI_RELU_F32)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+}
+
+template <int EPI, int COLS>
+struct LdsTile {
+  static constexpr int ESZ = epi_is_bf16(EPI) ? 2 : 4;
+  static constexpr int CH = 16 / ESZ;                 // elements per 16-B chunk
+  static constexpr int NCH = COLS / CH;               // chunks per row
+  static constexpr int MASK = (NCH < 16 ? NCH : 16) - 1;
+  __device__ static int off(int row, int col) {       // byte offset of (row, col), col % 4 == 0
+    return row * COLS * ESZ + ((((col / CH) ^ (row & MASK))) << 4) + (col % CH) * ESZ;
+  }
+  __device__ static void put(char* lds, int row, int col, const float* v) {
+    if (ESZ == 2) {
+      uint2 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(lds + off(row, col)) = o;
+    } else {
+      *reinterpret_cast<float4*>(lds + off(row, col)) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  // rows [0, ROWS) of the LDS tile -> C rows m_base + r (< M), columns n0 ..
+  template <int ROWS, int NT>
+  __device__ static void drain(const char* lds, const GemmGroup& g, const GemmArgs& args, int m_base, int n0, int M) {
+    for (int idx = threadIdx.x; idx < ROWS * NCH; idx += NT) {
+      const int r = idx / NCH, c = idx - r * NCH;
+      const int m = m_base + r;
+      if (m >= M) continue;
+      const int n = n0 + c * CH;
+      const uint4 d = *reinterpret_cast<const uint4*>(lds + r * COLS * ESZ + ((c ^ (r & MASK)) << 4));
+      if (ESZ == 2) {
+        *reinterpret_cast<uint4*>(static_cast<bf16_t*>(g.C) + (int64_t)m * g.ldc + n) = d;
+      } else {
+        float4 o = make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
+        if (EPI == EPI_RESID_F32 || EPI == EPI_POS_F32) {
+          const int64_t rr = EPI == EPI_POS_F32 ? (int64_t)(m % args.pos_rows) : (int64_t)m;
+          const float4 R = *reinterpret_cast<const float4*>(g.R + rr * g.ldr + n);
+          o = make_float4(R.x + o.x, R.y + o.y, R.z + o.z, R.w + o.w);
+        }
+        *reinterpret_cast<float4*>(static_cast<float*>(g.C) + (int64_t)m * g.ldc + n) = o;
+      }
+    }
+  }
+};
 
 template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int STAGES>
 __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args) {
@@ -73,6 +187,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   int tm, tn;
   tile_of(id, tiles_m, tiles_n, args.gm, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
+  GEMM_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WNW, wn = wave % WNW;
 
@@ -199,6 +314,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   if (nk > 1 && D > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  GEMM_STAMP(1);
   int stage = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = kt + D;
@@ -213,49 +329,239 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
     __builtin_amdgcn_s_barrier();
   }
 
+  GEMM_STAMP(2);
   // ---- epilogue: lane owns C[m][n..n+3]
+  using LT = LdsTile<EPI, BN>;
+  if constexpr (!SPLIT && BM * BN * LT::ESZ <= T::NSTAGE * T::STAGE * 2) {
+    char* lds = reinterpret_cast<char*>(smem);
 #pragma unroll
-  for (int i = 0; i < T::FM; ++i) {
-    const int m = m0 + wm * T::WM + i * 16 + (lane & 15);
-    if (m >= M) continue;
+    for (int i = 0; i < T::FM; ++i)
 #pragma unroll
-    for (int jj = 0; jj < T::FN; ++jj) {
-      const int n = n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4;
-      const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-      float v[4] = {acc[i][jj][0] + bv.x, acc[i][jj][1] + bv.y, acc[i][jj][2] + bv.z, acc[i][jj][3] + bv.w};
-      if (EPI == EPI_GELU_BF16)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
-      if (EPI == EPI_RELU_BF16 || EPI == EPI_RELU_F32)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      const int64_t off = (int64_t)m * g.ldc + n;
-      if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
-        bf16_t h[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) h[e] = f2bf(v[e]);
-        uint2 o;
-        o.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-        o.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C) + off) = o;
-        if (SPLIT && g.C_lo) {
-          uint2 lo;
-          lo.x = (uint32_t)f2bf(v[0] - bf2f(h[0])) | ((uint32_t)f2bf(v[1] - bf2f(h[1])) << 16);
-          lo.y = (uint32_t)f2bf(v[2] - bf2f(h[2])) | ((uint32_t)f2bf(v[3] - bf2f(h[3])) << 16);
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C_lo) + off) = lo;
-        }
-      } else {
-        float4 o = make_float4(v[0], v[1], v[2], v[3]);
-        if (EPI == EPI_RESID_F32) {
-          const float4 rr = *reinterpret_cast<const float4*>(g.R + (int64_t)m * g.ldr + n);
-          o = make_float4(rr.x + v[0], rr.y + v[1], rr.z + v[2], rr.w + v[3]);
-        } else if (EPI == EPI_POS_F32) {
-          const float4 rr = *reinterpret_cast<const float4*>(g.R + (int64_t)(m % args.pos_rows) * g.ldr + n);
-          o = make_float4(v[0] + rr.x, v[1] + rr.y, v[2] + rr.z, v[3] + rr.w);
-        }
-        *reinterpret_cast<float4*>(static_cast<float*>(g.C) + off) = o;
+      for (int jj = 0; jj < T::FN; ++jj) {
+        const int col = wn * T::WN + jj * 16 + (lane >> 4) * 4;
+        float v[4];
+        epi_values<EPI>(g, n0 + col, acc[i][jj], v);
+        LT::put(lds, wm * T::WM + i * 16 + (lane & 15), col, v);
       }
+    __syncthreads();
+    LT::template drain<BM, T::NT>(lds, g, args, m0, n0, M);
+  } else {
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i) {
+      const int m = m0 + wm * T::WM + i * 16 + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj)
+        store4<EPI, SPLIT>(g, args, m, n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4, acc[i][jj]);
     }
+  }
+  GEMM_STAMP(3);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// 256 x 256 tile, 8 waves (2 x 4), four phases per 64-deep K-tile (one 128 x 128 C quadrant per
+// phase; each wave owns a 64 x 32 piece of every quadrant).
+//
+// LDS holds 8 half-tile slots of 128 rows x 64 k (16 KB): {A rows 0-127, W rows 0-127, W rows
+// 128-255, A rows 128-255} x 2 K-tile buffers.  Half-tile loads are numbered L = 4 kt + pos and
+// load L is issued at global phase L - 6 (5-6 phases ahead of its first read, >= 2 phases after the
+// last read of the slot it overwrites).  Phase reads (register reuse): p0 A rows 0-127 + W rows
+// 0-127, p1 W rows 128-255, p2 A rows 128-255, p3 none (12 / 4 / 8 / 0 ds_read_b128).  Each phase: fragment reads, counted vmcnt for what the
+// next phase reads, one half-tile load (2 x buffer_load_dwordx4 ... lds per lane), s_barrier, 16
+// MFMAs at raised priority, s_barrier.  Waves 4-7 run one barrier behind waves 0-3, so on every
+// SIMD one wave multiplies while its partner reads fragments and issues loads.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm256_kernel(const GemmArgs args) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 128 * 64];
+  const GemmGroup& g = args.g[blockIdx.z];
+  const int M = args.M, K = args.K;
+  const int tiles_m = (M + 255) / 256, tiles_n = args.N / 256, ntiles = tiles_m * tiles_n;
+  const int b = blockIdx.x, x = b & 7, j = b >> 3;
+  const int q = ntiles >> 3, r8 = ntiles & 7;
+  const int id = (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + j;
+  int tm, tn;
+  tile_of(id, tiles_m, tiles_n, args.gm, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  GEMM_STAMP(0);
+
+  const int chunk = ((lane & 7) ^ (lane >> 3)) * 16;
+  const rsrc_t rA = make_rsrc(g.A + (int64_t)m0 * g.lda, (int64_t)(M - m0) * g.lda * 2);
+  const rsrc_t rW = make_rsrc(g.W + (int64_t)n0 * g.ldw, (int64_t)256 * g.ldw * 2);
+  const uint32_t va = (uint32_t)((wave * 8 + (lane >> 3)) * g.lda * 2 + chunk);
+  const uint32_t vw = (uint32_t)((wave * 8 + (lane >> 3)) * g.ldw * 2 + chunk);
+  const uint32_t a64 = 64u * g.lda * 2, w64 = 64u * g.ldw * 2;
+  const int nk = K / 64, NL = 4 * nk;
+
+  // half-tile L (pos = L & 3: 0 A rows 0-127, 1 W rows 0-127, 2 W rows 128-255, 3 A rows 128-255)
+  auto issue = [&](int L, auto pos_c) {
+    constexpr int pos = decltype(pos_c)::value;
+    const int kt = L >> 2;
+    bf16_t* dst = smem + ((kt & 1) * 4 + pos) * 8192 + wave * 512;
+    const int soff = kt * 128;
+    const rsrc_t rs = (pos == 0 || pos == 3) ? rA : rW;
+    const uint32_t v0 = pos == 0 ? va : pos == 3 ? va + 2 * a64 : pos == 1 ? vw : vw + 2 * w64;
+    const uint32_t v1 = v0 + ((pos == 0 || pos == 3) ? a64 : w64);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lptr_t)dst, 16, v0, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lptr_t)(dst + 4096), 16, v1, soff, 0, 0);
+  };
+  auto wait_vm = [&](int n) {   // n half-tiles (2 loads each) may stay in flight
+    if (n >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x4 acc[4][4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[a][i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 Ar[4][2], B0r[2][2], B1r[2][2];
+
+  auto read_a = [&](const bf16_t* S) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int row = wr * 64 + i * 16 + (lane & 15), c = 4 * s2 + (lane >> 4);
+        Ar[i][s2] = *reinterpret_cast<const bf16x8*>(S + swz(row, c));
+      }
+  };
+  auto read_b = [&](const bf16_t* S, bf16x8 (&Br)[2][2]) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int row = wc * 32 + jj * 16 + (lane & 15), c = 4 * s2 + (lane >> 4);
+        Br[jj][s2] = *reinterpret_cast<const bf16x8*>(S + swz(row, c));
+      }
+  };
+  auto mma = [&](f32x4 (&C)[4][2], bf16x8 (&Br)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          C[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Br[jj][s2], Ar[i][s2], C[i][jj], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // half-tiles that may stay in flight at phase P's wait (before its own load): everything issued
+  // after the last one phase P + 1 reads (p0: B1 = P+2, p1: A1 = P+2, p2: A1 = P+1, p3: B0' = P+2)
+  auto n_after = [&](int P, int p) {
+    const int need = P + (p == 2 ? 1 : 2);
+    return max(min(P + 6, NL) - need - 1, 0);
+  };
+
+  auto ktile = [&](int kt, auto steady_c) {
+    constexpr bool STEADY = decltype(steady_c)::value;   // every load of this K-tile's phases exists
+    const bf16_t* S = smem + (kt & 1) * 4 * 8192;
+    const int P0 = 4 * kt;
+    // phase 0: quadrant (A rows 0-127, W rows 0-127)
+    read_b(S + 8192, B0r);
+    read_a(S);
+    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0, 0));
+    if (STEADY || P0 + 6 < NL) issue(P0 + 6, std::integral_constant<int, 2>{});
+    __builtin_amdgcn_s_barrier();
+    mma(acc[0], B0r);
+    __builtin_amdgcn_s_barrier();
+    // phase 1: (A rows 0-127, W rows 128-255)
+    read_b(S + 2 * 8192, B1r);
+    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 1, 1));
+    if (STEADY || P0 + 7 < NL) issue(P0 + 7, std::integral_constant<int, 3>{});
+    __builtin_amdgcn_s_barrier();
+    mma(acc[1], B1r);
+    __builtin_amdgcn_s_barrier();
+    // phase 2: (A rows 128-255, W rows 128-255)
+    read_a(S + 3 * 8192);
+    if (STEADY) asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); else wait_vm(n_after(P0 + 2, 2));
+    if (STEADY || P0 + 8 < NL) issue(P0 + 8, std::integral_constant<int, 0>{});
+    __builtin_amdgcn_s_barrier();
+    mma(acc[2], B1r);
+    __builtin_amdgcn_s_barrier();
+    // phase 3: (A rows 128-255, W rows 0-127)
+    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 3, 3));
+    if (STEADY || P0 + 9 < NL) issue(P0 + 9, std::integral_constant<int, 1>{});
+    __builtin_amdgcn_s_barrier();
+    mma(acc[3], B0r);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  // prologue: half-tiles 0..5 (tile 0 and the first half of tile 1), wait for A0(0) and B0(0)
+  issue(0, std::integral_constant<int, 0>{});
+  issue(1, std::integral_constant<int, 1>{});
+  issue(2, std::integral_constant<int, 2>{});
+  issue(3, std::integral_constant<int, 3>{});
+  if (nk > 1) {
+    issue(4, std::integral_constant<int, 0>{});
+    issue(5, std::integral_constant<int, 1>{});
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  GEMM_STAMP(1);
+  if (wr) __builtin_amdgcn_s_barrier();   // stagger: waves 4-7 one barrier behind
+
+  // steady K-tiles: all of their phase loads (up to half-tile P+9 < 4 nk) exist
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) ktile(kt, std::true_type{});
+  for (; kt < nk; ++kt) ktile(kt, std::false_type{});
+  if (!wr) __builtin_amdgcn_s_barrier();  // balance the stagger
+  GEMM_STAMP(2);
+
+  // epilogue: quadrant order (0,0), (0,1), (1,1), (1,0); through LDS (bf16: the whole 256 x 256 tile,
+  // fp32: two 128-row halves)
+  constexpr int QA[4] = {0, 0, 1, 1}, QB[4] = {0, 1, 1, 0};
+  using LT = LdsTile<EPI, 256>;
+  char* lds = reinterpret_cast<char*>(smem);
+  constexpr int HALVES = LT::ESZ == 2 ? 1 : 2;
+#pragma unroll
+  for (int h = 0; h < HALVES; ++h) {
+    if (h) __syncthreads();
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      if (HALVES == 2 && QA[qd] != h) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int col = QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4;
+          const int row = (HALVES == 2 ? 0 : QA[qd] * 128) + wr * 64 + i * 16 + (lane & 15);
+          float v[4];
+          epi_values<EPI>(g, n0 + col, acc[qd][i][jj], v);
+          LT::put(lds, row, col, v);
+        }
+    }
+    __syncthreads();
+    LT::template drain<256 / HALVES, 512>(lds, g, args, m0 + h * 128, n0, M);
+  }
+  GEMM_STAMP(3);
+}
+
+template <int EPI>
+static void launch256(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  const int tiles_m = (a.M + 255) / 256;
+  a.gm = tiles_m < 4 ? tiles_m : 4;
+  dim3 grid(tiles_m * (a.N / 256), 1, a.groups);
+  hipLaunchKernelGGL(gemm256_kernel<EPI>, grid, dim3(512), 0, s, a);
+}
+
+static void launch256_epi(const GemmArgs& a, int epi, hipStream_t s) {
+  switch (epi) {
+    case EPI_BF16: return launch256<EPI_BF16>(a, s);
+    case EPI_GELU_BF16: return launch256<EPI_GELU_BF16>(a, s);
+    case EPI_RESID_F32: return launch256<EPI_RESID_F32>(a, s);
+    case EPI_F32: return launch256<EPI_F32>(a, s);
+    case EPI_POS_F32: return launch256<EPI_POS_F32>(a, s);
+    default: break;
   }
 }
 
@@ -301,6 +607,7 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         case 6: return launch_cfg<256, 256, 4, 2, false, 2>(a, epi, s);
         case 7: return launch_cfg<128, 256, 2, 4, false, 2>(a, epi, s);
         case 8: return launch_cfg<64, 128, 2, 2, false, 2>(a, epi, s);
+        case 9: if (a.N % 256 == 0) return launch256_epi(a, epi, s); break;
         default: break;
       }
     }
@@ -327,5 +634,10 @@ void gemm(const GemmArgs& a, int epi, hipStream_t s) {
 }
 
 void gemm_force_config(int cfg) { g_force_cfg = cfg; }
+
+int gemm_set_stamps(void* dev_buf) {
+  unsigned long long* p = static_cast<unsigned long long*>(dev_buf);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
 
 }  // namespace mmt

@@ -43,6 +43,7 @@ struct GemmArgs {
 
 void gemm(const GemmArgs& a, int epi, hipStream_t s);
 void gemm_force_config(int cfg);   // tuning override, -1 = heuristic
+int gemm_set_stamps(void* dev_buf);  // tuning: per-block cycle stamps [blocks][4] (null: off)
 
 // ---------------------------------------------------------------- attention
 struct AttnArgs {

@@ -84,6 +84,7 @@ SIGNATURES = {
     "mmt_dimp_feat_transpose": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_dimp_optimize": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, ctypes.POINTER(MmtDimpParams), _I, _P,
                                ctypes.c_size_t, _P, _P]),
+    "mmt_gemm_stamps": (_I, [_P]),
     "mmt_op_gemm": (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_gemm_force_config": (_I, [_I]),
     "mmt_op_attention": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),

@@ -58,6 +58,31 @@ def test_gemm_dense(lib, M, N, K, epi):
         torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,N,K", [(4896, 3072, 768), (10240, 2304, 768), (300, 256, 128), (7808, 768, 3072),
+                                   (256, 512, 64)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm256_forced(lib, M, N, K, epi):
+    """The 256x256 eight-phase kernel (forced) on the path's shapes, M tails and K = 64 / 128."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 100 * epi)
+    A = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    ref = A.float() @ W.float().t() + bias
+    lib.mmt_gemm_force_config(9)
+    try:
+        if epi in (0, 1):
+            C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            _gemm(lib, A, W, bias, C, epi=epi)
+            torch.testing.assert_close(C.float(), F.gelu(ref) if epi == 1 else ref, rtol=1e-2, atol=1e-2)
+        else:
+            R = torch.randn(M, N, device="cuda", generator=g)
+            C = R.clone()
+            _gemm(lib, A, W, bias, C, R=C, epi=2)
+            torch.testing.assert_close(C, R + ref, rtol=1e-4, atol=1e-3)
+    finally:
+        lib.mmt_gemm_force_config(-1)
+
+
 def test_gemm_pos_epilogue(lib):
     g = torch.Generator(device="cuda").manual_seed(5)
     M, N, K, L = 2 * 720, 768, 768, 720
