@@ -68,6 +68,27 @@ def cpu_baseline(workload, frames_np, gts, seconds=12.0):
                       f"(crop+net+decode, torch {threads} threads, {dt:.1f}s)"}
 
 
+def pmc_traffic(probe, path=None):
+    """HBM bytes per launch of the probed kernel class from the committed PMC summary
+    (tests/pmc_bench.sh + tests/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes)."""
+    import glob
+    import re
+    epi = {"fc1": 1, "qkv": 0, "fc2": 2, "proj": 2}.get(probe)
+    files = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")))
+    if epi is None or not files or not os.path.exists(files[-1]):
+        return None, None
+    ks = json.load(open(files[-1]))["kernels"]
+    best = None
+    for name, d in ks.items():
+        m = re.match(r"gemm_kernel<\d+, \d+, \d+, \d+, (\d+), 0, false", name) or re.match(r"gemm256_kernel<(\d+)>", name)
+        if m and int(m.group(1)) == epi and "traffic_bytes_per_dispatch" in d:
+            if best is None or d["dispatches"] > best[1]["dispatches"]:
+                best = (name, d)
+    if best is None:
+        return None, None
+    return best[1]["traffic_bytes_per_dispatch"], os.path.relpath(files[-1], REPO) + ":" + best[0]
+
+
 def aggregate_throughput(batch, steps, elapsed):
     """(whole-job frames/s, max-over-ranks elapsed): every rank tracked batch x steps frames."""
     from mmtrack_amd.sharding import max_over_ranks, rank_world
@@ -85,7 +106,7 @@ def main():
     ap.add_argument("--workload", default="vipt_deep_rgbt", choices=list(WORKLOADS))
     ap.add_argument("--frames", type=int, default=8, help="distinct synthetic frames per sequence (cycled)")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--probe", default="fc1", help="kernel class timed with HIP events for the roofline")
+    ap.add_argument("--probe", default="fc1", help="kernel class timed with HIP events for the roofline ('none': off)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -137,7 +158,7 @@ def main():
     # roofline probe: the same steps again, launched eagerly (HIP cannot time event nodes captured in a
     # graph), with HIP events on the engine stream around every launch of the dominant kernel class
     roof = None
-    if args.probe:
+    if args.probe and args.probe != "none":
         eng.timing_enable(args.probe)
         for k in range(min(args.steps, 20)):
             step(args.warmup + k)
@@ -147,10 +168,12 @@ def main():
             avg_ms = tr["total_ms"] / tr["launches"]
             fl = tr["flops"] / tr["launches"]
             achieved = fl / (avg_ms * 1e-3) / 1e12
+            traffic, src = pmc_traffic(args.probe) if B == 32 and args.workload == "vipt_deep_rgbt" else (None, None)
             roof = {"bound": "mfma", "kernel": f"gemm[{args.probe}]", "achieved": round(achieved, 1),
                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                    "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 2), "flop_per_launch": fl,
-                    "launches": tr["launches"]}
+                    "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (HBM, PMC)",
+                    "traffic_source": src, "algorithmic_bytes_per_launch": tr["bytes"] / tr["launches"],
+                    "avg_launch_us": round(avg_ms * 1e3, 2), "flop_per_launch": fl, "launches": tr["launches"]}
 
     if rank == 0:
         cpu = None

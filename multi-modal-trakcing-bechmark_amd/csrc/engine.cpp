@@ -490,7 +490,11 @@ GemmArgs dense(mmt_engine* e, const bf16_t* A, const bf16_t* Al, int64_t lda, co
 
 void run_gemm(mmt_engine* e, const char* cls, const GemmArgs& a, int epi) {
   const double flops = 2.0 * a.M * a.N * (double)a.K * a.groups;
-  const double bytes = ((double)a.M * a.K + (double)a.N * a.K) * 2.0 * a.groups;
+  // algorithmic HBM bytes: A and W once, C once (bf16 or fp32), R once for the residual epilogues
+  const bool out16 = epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RELU_BF16;
+  const double outb = (double)a.M * a.N * (out16 ? 2.0 : 4.0) * (a.split && out16 ? 2.0 : 1.0);
+  const double rb = (epi == EPI_RESID_F32) ? (double)a.M * a.N * 4.0 : 0.0;
+  const double bytes = (((double)a.M * a.K + (double)a.N * a.K) * 2.0 * (a.split ? 2.0 : 1.0) + outb + rb) * a.groups;
   probe_begin(e, cls, flops, bytes);
   gemm(a, epi, e->stream);
   probe_end(e, cls);
