@@ -47,6 +47,7 @@ struct LayerW {
 };
 struct PromptW {
   float *w00, *b00, *w01, *b01, *w1, *b1, *nw, *nb;
+  float* fold;   // deep layers: PromptFold (kernels.h) of LN_B + conv0_1 over the previous s8
   float smooth;
 };
 
@@ -106,7 +107,7 @@ struct mmt_engine {
   bf16_t *A_rgb_l = nullptr, *A_aux_l = nullptr, *Hn_l = nullptr, *QKV_l = nullptr, *O_l = nullptr, *Hm_l = nullptr,
          *feat_l = nullptr, *h1_l = nullptr, *h2_l = nullptr, *h3_l = nullptr, *zero = nullptr;
   bool split = false;
-  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *P = nullptr, *a8 = nullptr,
+  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *s8 = nullptr, *a8 = nullptr,
         *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
   int *gidx0 = nullptr, *gidx1 = nullptr, *slot2pos = nullptr, *gather = nullptr, *removed = nullptr;
@@ -307,6 +308,56 @@ int pack_weights(mmt_engine* e) {
     w.smooth = H(e, p + "fovea.smooth")[0];
     TRY(upload_f32(e, &w.nw, H(e, "backbone.prompt_norms." + std::to_string(i) + ".weight")));
     TRY(upload_f32(e, &w.nb, H(e, "backbone.prompt_norms." + std::to_string(i) + ".bias")));
+    w.fold = nullptr;
+    if (i >= 1) {   // PromptFold, in double (kernels.h)
+      const auto& W = H(e, p + "conv0_1.weight");            // [8][768]
+      const auto& w0 = H(e, p + "conv0_1.bias");
+      const auto& g = H(e, "backbone.prompt_norms." + std::to_string(i) + ".weight");
+      const auto& bb = H(e, "backbone.prompt_norms." + std::to_string(i) + ".bias");
+      const std::string pp = "backbone.prompt_blocks." + std::to_string(i - 1) + ".";
+      const auto& V = H(e, pp + "conv1x1.weight");            // [768][8]
+      const auto& v0 = H(e, pp + "conv1x1.bias");
+      double cm[8] = {0}, bm = 0;
+      for (int c = 0; c < C; ++c) {
+        for (int j = 0; j < 8; ++j) cm[j] += V[c * 8 + j];
+        bm += v0[c];
+      }
+      for (int j = 0; j < 8; ++j) cm[j] /= C;
+      bm /= C;
+      std::vector<double> Vc((size_t)C * 8), vc(C);
+      for (int c = 0; c < C; ++c) {
+        for (int j = 0; j < 8; ++j) Vc[c * 8 + j] = V[c * 8 + j] - cm[j];
+        vc[c] = v0[c] - bm;
+      }
+      std::vector<float> f(FOLD_N, 0.f);
+      for (int k = 0; k < 8; ++k) {
+        double mc = 0, cb = w0[k];
+        double Mk[8] = {0};
+        for (int c = 0; c < C; ++c) {
+          const double wg = (double)W[k * C + c] * g[c];
+          for (int j = 0; j < 8; ++j) Mk[j] += wg * Vc[c * 8 + j];
+          mc += wg * vc[c];
+          cb += (double)W[k * C + c] * bb[c];
+        }
+        for (int j = 0; j < 8; ++j) f[FOLD_MC + k * 8 + j] = (float)Mk[j];
+        f[FOLD_mc + k] = (float)mc;
+        f[FOLD_cb + k] = (float)cb;
+      }
+      double gb = 0;
+      for (int j = 0; j < 8; ++j) {
+        double gj = 0;
+        for (int l = 0; l < 8; ++l) {
+          double G = 0;
+          for (int c = 0; c < C; ++c) G += Vc[c * 8 + j] * Vc[c * 8 + l];
+          f[FOLD_G + j * 8 + l] = (float)(G / C);
+        }
+        for (int c = 0; c < C; ++c) gj += Vc[c * 8 + j] * vc[c];
+        f[FOLD_g + j] = (float)(gj / C);
+      }
+      for (int c = 0; c < C; ++c) gb += vc[c] * vc[c];
+      f[FOLD_gb] = (float)(gb / C);
+      TRY(upload_f32(e, &w.fold, f));
+    }
   }
   for (int i = 0; i < DEPTH; ++i) {
     const std::string p = "backbone.blocks." + std::to_string(i) + ".";
@@ -370,7 +421,7 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->A_rgb, (size_t)B * L * C * 2},      {(void**)&e->A_aux, (size_t)B * L * C * 2},
       {(void**)&e->tok_rgb, (size_t)B * L * C * 4},    {(void**)&e->tok_aux, (size_t)B * L * C * 4},
       {(void**)&e->X, (size_t)B * L * C * 4},          {(void**)&e->X2, (size_t)B * L * C * 4},
-      {(void**)&e->P, (size_t)B * L * C * 4},          {(void**)&e->a8, (size_t)B * L * 8 * 4},
+      {(void**)&e->s8, (size_t)B * L * 8 * 4},         {(void**)&e->a8, (size_t)B * L * 8 * 4},
       {(void**)&e->c8, (size_t)B * L * 8 * 4},         {(void**)&e->Hn, (size_t)B * L * C * 2},
       {(void**)&e->QKV, (size_t)B * L * 3 * C * 2},    {(void**)&e->O, (size_t)B * L * C * 2},
       {(void**)&e->Hm, (size_t)B * L * MLPD * 2},      {(void**)&e->feat, (size_t)B * Lx * C * 2},
@@ -555,7 +606,7 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
   pa.Lx = Lx;
   pa.a8 = e->a8;
   pa.c8 = e->c8;
-  pa.P = e->P;
+  pa.s8 = e->s8;
   auto set_prompt = [&](int i, int lnA) {
     pa.layer = i;
     pa.lnA_w = e->pw[lnA].nw;
@@ -566,8 +617,7 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
     pa.b00 = e->pw[i].b00;
     pa.w01 = e->pw[i].w01;
     pa.b01 = e->pw[i].b01;
-    pa.w1 = e->pw[i].w1;
-    pa.b1 = e->pw[i].b1;
+    pa.fold = e->pw[i].fold;
     pa.smooth = e->pw[i].smooth;
   };
   if (prompted) {  // layer-0 prompt: vit_ce_prompt.py:205-219
@@ -576,10 +626,6 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
     pa.srcA_rows = L;
     pa.srcB = e->tok_aux;
     pa.slot2pos = nullptr;
-    pa.X = X;
-    pa.X_rows = L;
-    pa.tok_rgb = e->tok_rgb;
-    pa.pos = e->pos;
     prompt_reduce(pa, s);
     prompt_expand(pa, s);   // P; X = tok_rgb + P + pos is formed by block 0's fused LN1
   }
@@ -596,10 +642,8 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       set_prompt(i, i - 1);
       pa.srcA = X;
       pa.srcA_rows = Na;
-      pa.srcB = e->P;
+      pa.srcB = nullptr;
       pa.slot2pos = e->slot2pos;
-      pa.X = X;
-      pa.X_rows = Na;
       prompt_reduce(pa, s);
       prompt_expand(pa, s);
       ln_mode = 2;
@@ -612,7 +656,9 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       la.Lz = Lz;
       la.Lx = Lx;
       la.X = X;
-      la.P = e->P;
+      la.s8 = e->s8;
+      la.w1 = e->pw[i].w1;
+      la.b1 = e->pw[i].b1;
       la.tok_rgb = e->tok_rgb;
       la.pos = e->pos;
       la.gidx = gin;

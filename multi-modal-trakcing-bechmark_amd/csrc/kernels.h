@@ -69,31 +69,36 @@ struct PromptArgs {
   int B, Lz, Lx;             // slots per sequence = Lz + Lx
   const float* srcA;         // layer 0: tok_rgb [B][L][768]; else residual X [B][Nrows][768] (compact)
   int srcA_rows;             // rows per sequence of srcA
-  const float* srcB;         // layer 0: tok_aux [B][L][768]; else previous prompt P [B][L][768]
+  const float* srcB;         // layer 0: tok_aux [B][L][768]; deep layers: unused (the previous prompt is s8)
   const int* slot2pos;       // [B][Lx] compact position (or -1) of search slots; null at layer 0
   const float* lnA_w; const float* lnA_b;   // prompt_norms[i-1] (layer 0: prompt_norms[0])
-  const float* lnB_w; const float* lnB_b;   // prompt_norms[i]
+  const float* lnB_w; const float* lnB_b;   // prompt_norms[i] (layer 0 only; deep layers use fold)
   const float* w00; const float* b00;       // conv0_0 [8][768]
-  const float* w01; const float* b01;       // conv0_1 [8][768]
-  const float* w1; const float* b1;         // conv1x1 [768][8]
-  float smooth;                             // fovea.smooth (device scalar copied to host at load)
+  const float* w01; const float* b01;       // conv0_1 [8][768] (layer 0 only)
+  const float* fold;         // deep layers: LN_B + conv0_1 folded onto the previous s8 (PromptFold)
+  float smooth;              // fovea.smooth (device scalar copied to host at load)
   float* a8;                 // scratch [B][L][8]
   float* c8;                 // scratch [B][L][8]
-  float* P;                  // out prompt [B][L][768] (full slot layout)
-  float* X;                  // residual (layer 0: written [B][L][768]; else += at compact positions)
-  int X_rows;                // rows per sequence of X
-  const float* tok_rgb;      // layer 0: the RGB tokens added to the prompt
-  const float* pos;          // layer 0: pos_embed [L][768]
+  float* s8;                 // prompt block output before conv1x1 [B][L][8]: P = conv1x1(s8) is
+                             // never materialised (ln_prompt expands it, the next layer folds it)
 };
+// PromptFold (float[160]) for deep layer i, from prompt_norms[i] (g, b), conv0_1 of block i (W, w0)
+// and conv1x1 of block i-1 (V [768][8], v0): with V' / v0' the column-centred V / v0,
+//   c8 = rstd * (Mc s + mc) + cb,  rstd = 1/sqrt(s'G s + 2 g.s + gb + eps),
+//   Mc = (W diag g) V', mc = (W diag g) v0', cb = W b + w0, G = V'^T V' / 768, g = V'^T v0' / 768,
+//   gb = |v0'|^2 / 768   (LN_B(P_prev) -> conv0_1, vit_ce_prompt.py:292-300, without forming P_prev)
+enum { FOLD_MC = 0, FOLD_mc = 64, FOLD_cb = 72, FOLD_G = 80, FOLD_g = 144, FOLD_gb = 152, FOLD_N = 160 };
 void prompt_reduce(const PromptArgs& a, hipStream_t s);
 void prompt_expand(const PromptArgs& a, hipStream_t s);
 
-// LN1 of a block with the prompt residual fused in (writes the updated residual X and LN(X))
+// LN1 of a block with the prompt residual fused in (writes the updated residual X and LN(X));
+// the prompt P = conv1x1(s8) + bias is expanded on the fly (conv1x1 weights held in registers)
 struct LnPromptArgs {
   int mode;                  // 1: layer 0 (X = tok_rgb + P + pos), 2: deep layer (X += P[slot])
   int rows, rows_per_seq, Lz, Lx;
   float* X;
-  const float* P;            // [B][Lz+Lx][768]
+  const float* s8;           // [B][Lz+Lx][8]
+  const float* w1; const float* b1;   // conv1x1 of this layer's prompt block [768][8], [768]
   const float* tok_rgb;      // mode 1
   const float* pos;          // mode 1: [Lz+Lx][768]
   const int* gidx;           // mode 2: [B][rows_per_seq - Lz] slot of each compact search token
