@@ -2,9 +2,11 @@
 // elimination side output (attn_blocks.py:44-53), gfx950.
 //
 // One workgroup = WAVES waves, each wave 16 query rows of one (sequence, head).
-// K/V tiles of 64 keys are staged in LDS (K row-major, XOR-swizzled; V
-// transposed, rows padded to 136 B so the 8-B fragment reads are
-// conflict-free).  Scores are computed swapped, S^T = K Q^T, with
+// K/V tiles of 64 keys are staged in LDS as 16-B chunks, both row-major with
+// the chunk XOR-swizzled by row; V^T fragments come from ds_read_b64_tr_b16
+// (the hardware transposed read), so staging is a straight copy.  Workgroups
+// of one (sequence, head) are mapped to one XCD (their K/V tiles are shared
+// through that XCD's L2).  Scores are computed swapped, S^T = K Q^T, with
 // v_mfma_f32_16x16x32_bf16: a lane holds 16 keys of ONE query, so the online
 // softmax needs only two cross-lane shuffles per row statistic, and the
 // accumulator is already the B operand (P^T) of O^T = V^T P^T.
@@ -18,10 +20,13 @@
 namespace mmt {
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4* lds_bf16x4_t;
 
 constexpr int KB = 64;         // keys per LDS tile
-constexpr int VT_PITCH = 68;   // bf16 per transposed-V row (136 B)
 constexpr int CE_MAX = 1024;   // max tokens for the exported CE row
+
+// byte offset of 16-B chunk c of row r in a [64][64] bf16 tile (128-B rows, chunk XOR row)
+__device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 
 template <int WAVES, bool SPLIT>
 __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
@@ -29,14 +34,22 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
   // hi*hi + lo*hi + hi*lo; the LDS images of K and V^T are held for both halves.
   constexpr int NH = SPLIT ? 2 : 1;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NH][KB * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[NH][64 * VT_PITCH];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[NH][KB * 64];
   __shared__ float ce_row[CE_MAX];
 
-  const int b = blockIdx.z, h = blockIdx.y;
+  // XCD-aware order: logical id = (b * heads + h) * nqt + qt; blocks bid, bid + 8, ... (one XCD) take a
+  // contiguous logical range, so the query tiles of one (b, h) share an L2
+  const int nqt = (a.N + 16 * WAVES - 1) / (16 * WAVES);
+  const int nblk = nqt * a.heads * a.B;
+  const int bid = blockIdx.x, xcd = bid & 7, jx = bid >> 3;
+  const int q8 = nblk >> 3, r8 = nblk & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + jx;
+  const int qt = lid % nqt, bh = lid / nqt;
+  const int b = bh / a.heads, h = bh - b * a.heads;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N = a.N, Cd = 64 * a.heads, C3 = 3 * Cd;
   const bf16_t* base = a.qkv + (int64_t)b * N * C3;
-  const int q0 = blockIdx.x * (16 * WAVES) + wave * 16;
+  const int q0 = qt * (16 * WAVES) + wave * 16;
   const int qi = q0 + (lane & 15);
   const int g = lane >> 4;
 
@@ -71,10 +84,8 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
         kv = *reinterpret_cast<const uint4*>(row + Cd);
         vv = *reinterpret_cast<const uint4*>(row + 2 * Cd);
       }
-      *reinterpret_cast<uint4*>(Ks[hl] + r * 64 + ((c ^ (r & 7)) << 3)) = kv;
-      const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[hl][(c * 8 + e) * VT_PITCH + r] = ve[e];
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Ks[hl]) + tile_off(r, c)) = kv;
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Vs[hl]) + tile_off(r, c)) = vv;
     }
     __syncthreads();
 
@@ -85,10 +96,11 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int r = 16 * t + (lane & 15), c = 4 * s + g;
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks[0] + r * 64 + ((c ^ (r & 7)) << 3));
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(Ks[0]) + tile_off(r, c));
         sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][s], sc[t], 0, 0, 0);
         if (SPLIT) {
-          const bf16x8 kl = *reinterpret_cast<const bf16x8*>(Ks[NH - 1] + r * 64 + ((c ^ (r & 7)) << 3));
+          const bf16x8 kl =
+              *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(Ks[NH - 1]) + tile_off(r, c));
           sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qf[0][s], sc[t], 0, 0, 0);
           sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[NH - 1][s], sc[t], 0, 0, 0);
         }
@@ -145,16 +157,24 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
           pl[4 + r] = (__bf16)(sc[2 * u + 1][r] - (float)pf[4 + r]);
         }
       }
+      // V^T fragment of keys {32u + 4g + 0..3} and {32u + 16 + 4g + 0..3} (the P element order) at
+      // dim 16 dt + (lane & 15): two transposed reads; lane 4q + p of a 16-lane group addresses key
+      // row q, dims 16 dt + 4p .. + 3
+      const int qq = (lane & 15) >> 2, pp = lane & 3;
+      const int vrow = 32 * u + 4 * g + qq;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const int vo = (16 * dt + (lane & 15)) * VT_PITCH + 32 * u + 4 * g;
-        const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(Vt[0] + vo);
-        const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(Vt[0] + vo + 16);
+        const int c = 2 * dt + (pp >> 1), half = (pp & 1) * 8;
+        const int oA = tile_off(vrow, c) + half, oB = tile_off(vrow + 16, c) + half;
+        const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[0]) + oA));
+        const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[0]) + oB));
         const bf16x8 vf = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
         if (SPLIT) {
-          const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(Vt[NH - 1] + vo);
-          const bf16x4 w1 = *reinterpret_cast<const bf16x4*>(Vt[NH - 1] + vo + 16);
+          const bf16x4 w0 =
+              __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[NH - 1]) + oA));
+          const bf16x4 w1 =
+              __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[NH - 1]) + oB));
           const bf16x8 vl = __builtin_shufflevector(w0, w1, 0, 1, 2, 3, 4, 5, 6, 7);
           o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, pf, o[dt], 0, 0, 0);
           o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl, o[dt], 0, 0, 0);
@@ -200,15 +220,13 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
 template <bool SPLIT>
 static void attention_t(const AttnArgs& a, hipStream_t s) {
   const int per4 = a.B * a.heads * ((a.N + 63) / 64);
+  const int bh = a.B * a.heads;
   if (per4 >= 240) {
-    dim3 grid((a.N + 63) / 64, a.heads, a.B);
-    hipLaunchKernelGGL((attn_kernel<4, SPLIT>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_kernel<4, SPLIT>), dim3((a.N + 63) / 64 * bh), dim3(256), 0, s, a);
   } else if (per4 * 2 >= 240) {
-    dim3 grid((a.N + 31) / 32, a.heads, a.B);
-    hipLaunchKernelGGL((attn_kernel<2, SPLIT>), grid, dim3(128), 0, s, a);
+    hipLaunchKernelGGL((attn_kernel<2, SPLIT>), dim3((a.N + 31) / 32 * bh), dim3(128), 0, s, a);
   } else {
-    dim3 grid((a.N + 15) / 16, a.heads, a.B);
-    hipLaunchKernelGGL((attn_kernel<1, SPLIT>), grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL((attn_kernel<1, SPLIT>), dim3((a.N + 15) / 16 * bh), dim3(64), 0, s, a);
   }
 }
 

@@ -107,7 +107,8 @@ struct mmt_engine {
   bf16_t *A_rgb_l = nullptr, *A_aux_l = nullptr, *Hn_l = nullptr, *QKV_l = nullptr, *O_l = nullptr, *Hm_l = nullptr,
          *feat_l = nullptr, *h1_l = nullptr, *h2_l = nullptr, *h3_l = nullptr, *zero = nullptr;
   bool split = false;
-  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *s8 = nullptr, *a8 = nullptr,
+  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *P = nullptr, *s8 = nullptr,
+        *a8 = nullptr,
         *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
   int *gidx0 = nullptr, *gidx1 = nullptr, *slot2pos = nullptr, *gather = nullptr, *removed = nullptr;
@@ -422,6 +423,7 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->tok_rgb, (size_t)B * L * C * 4},    {(void**)&e->tok_aux, (size_t)B * L * C * 4},
       {(void**)&e->X, (size_t)B * L * C * 4},          {(void**)&e->X2, (size_t)B * L * C * 4},
       {(void**)&e->s8, (size_t)B * L * 8 * 4},         {(void**)&e->a8, (size_t)B * L * 8 * 4},
+      {(void**)&e->P, (size_t)B * L * C * 4},
       {(void**)&e->c8, (size_t)B * L * 8 * 4},         {(void**)&e->Hn, (size_t)B * L * C * 2},
       {(void**)&e->QKV, (size_t)B * L * 3 * C * 2},    {(void**)&e->O, (size_t)B * L * C * 2},
       {(void**)&e->Hm, (size_t)B * L * MLPD * 2},      {(void**)&e->feat, (size_t)B * Lx * C * 2},
@@ -607,6 +609,7 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
   pa.a8 = e->a8;
   pa.c8 = e->c8;
   pa.s8 = e->s8;
+  pa.P = e->P;
   auto set_prompt = [&](int i, int lnA) {
     pa.layer = i;
     pa.lnA_w = e->pw[lnA].nw;
@@ -618,6 +621,8 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
     pa.w01 = e->pw[i].w01;
     pa.b01 = e->pw[i].b01;
     pa.fold = e->pw[i].fold;
+    pa.w1 = e->pw[i].w1;
+    pa.b1 = e->pw[i].b1;
     pa.smooth = e->pw[i].smooth;
   };
   if (prompted) {  // layer-0 prompt: vit_ce_prompt.py:205-219
@@ -626,8 +631,7 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
     pa.srcA_rows = L;
     pa.srcB = e->tok_aux;
     pa.slot2pos = nullptr;
-    prompt_reduce(pa, s);
-    prompt_expand(pa, s);   // P; X = tok_rgb + P + pos is formed by block 0's fused LN1
+    prompt_reduce(pa, s);   // fovea, P and X = tok_rgb + P + pos are formed with block 0's LN1
   }
 
   int* gin = e->gidx0;
@@ -645,7 +649,6 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       pa.srcB = nullptr;
       pa.slot2pos = e->slot2pos;
       prompt_reduce(pa, s);
-      prompt_expand(pa, s);
       ln_mode = 2;
     }
     if (ln_mode) {
@@ -656,9 +659,7 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       la.Lz = Lz;
       la.Lx = Lx;
       la.X = X;
-      la.s8 = e->s8;
-      la.w1 = e->pw[i].w1;
-      la.b1 = e->pw[i].b1;
+      la.P = e->P;
       la.tok_rgb = e->tok_rgb;
       la.pos = e->pos;
       la.gidx = gin;
@@ -666,7 +667,7 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       la.b = w.n1b;
       la.out = e->Hn;
       la.out_lo = e->Hn_l;
-      ln_prompt(la, s);
+      prompt_expand_ln(pa, la, s);
     } else {
       layernorm(X, w.n1w, w.n1b, e->Hn, e->Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
     }

@@ -79,8 +79,10 @@ struct PromptArgs {
   float smooth;              // fovea.smooth (device scalar copied to host at load)
   float* a8;                 // scratch [B][L][8]
   float* c8;                 // scratch [B][L][8]
-  float* s8;                 // prompt block output before conv1x1 [B][L][8]: P = conv1x1(s8) is
-                             // never materialised (ln_prompt expands it, the next layer folds it)
+  float* s8;                 // prompt block output before conv1x1 [B][L][8] (the next layer folds
+                             // LN_B + conv0_1 onto it instead of reading P)
+  const float* w1; const float* b1;         // conv1x1 [768][8]
+  float* P;                  // out prompt [B][L][768] (full slot layout)
 };
 // PromptFold (float[160]) for deep layer i, from prompt_norms[i] (g, b), conv0_1 of block i (W, w0)
 // and conv1x1 of block i-1 (V [768][8], v0): with V' / v0' the column-centred V / v0,
@@ -89,23 +91,22 @@ struct PromptArgs {
 //   gb = |v0'|^2 / 768   (LN_B(P_prev) -> conv0_1, vit_ce_prompt.py:292-300, without forming P_prev)
 enum { FOLD_MC = 0, FOLD_mc = 64, FOLD_cb = 72, FOLD_G = 80, FOLD_g = 144, FOLD_gb = 152, FOLD_N = 160 };
 void prompt_reduce(const PromptArgs& a, hipStream_t s);
-void prompt_expand(const PromptArgs& a, hipStream_t s);
 
-// LN1 of a block with the prompt residual fused in (writes the updated residual X and LN(X));
-// the prompt P = conv1x1(s8) + bias is expanded on the fly (conv1x1 weights held in registers)
+// LN1 of a block with the prompt residual fused in (writes the updated residual X and LN(X))
 struct LnPromptArgs {
   int mode;                  // 1: layer 0 (X = tok_rgb + P + pos), 2: deep layer (X += P[slot])
   int rows, rows_per_seq, Lz, Lx;
   float* X;
-  const float* s8;           // [B][Lz+Lx][8]
-  const float* w1; const float* b1;   // conv1x1 of this layer's prompt block [768][8], [768]
+  const float* P;            // [B][Lz+Lx][768]
   const float* tok_rgb;      // mode 1
   const float* pos;          // mode 1: [Lz+Lx][768]
   const int* gidx;           // mode 2: [B][rows_per_seq - Lz] slot of each compact search token
   const float* w; const float* b;
   bf16_t* out; bf16_t* out_lo;
 };
-void ln_prompt(const LnPromptArgs& a, hipStream_t s);
+void prompt_expand(const PromptArgs& a, hipStream_t s);
+// prompt_expand (s8 + P for every slot), then the prompt residual and LN1 for the compact rows
+void prompt_expand_ln(const PromptArgs& pa, const LnPromptArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- candidate elimination
 struct CEArgs {

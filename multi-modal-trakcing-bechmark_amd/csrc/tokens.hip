@@ -257,17 +257,28 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ prompt block, part 2
-// Fovea (vit_ce_prompt.py:33-47): per channel, softmax over the part's h*w positions of x*smooth,
-// times x; + the conv0_1 branch -> s8 (one block per (part, sequence)).  conv1x1 (8 -> 768) is applied
-// where the prompt is consumed (ln_prompt) and folded into the next layer's LN_B + conv0_1.
+// Fovea (vit_ce_prompt.py:33-47): per channel, softmax over the part's h*w positions of
+// x*smooth, times x; + conv0_1 branch -> s8 (kept: the next layer folds LN_B + conv0_1 onto it);
+// conv1x1 8 -> 768 (+bias) -> prompt P (full slot layout, each thread holding the conv1x1 rows of its
+// 3 columns across the block's 16 tokens).  The residual update that consumes P is fused into the
+// next LayerNorm (ln_prompt below).
+constexpr int PCHUNK = 16;
+
 __global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) {
-  __shared__ float red[4][8];
+  __shared__ float red[256];
   __shared__ float smax[8], ssum[8];
+  __shared__ float f[PCHUNK][8];
   const int L = a.Lz + a.Lx, b = blockIdx.y, tid = threadIdx.x;
-  const int lo = blockIdx.x == 0 ? 0 : a.Lz, n = blockIdx.x == 0 ? a.Lz : a.Lx;
+  const int nbz = (a.Lz + PCHUNK - 1) / PCHUNK;
+  int lo, n, t0;
+  if ((int)blockIdx.x < nbz) {
+    lo = 0; n = a.Lz; t0 = blockIdx.x * PCHUNK;
+  } else {
+    lo = a.Lz; n = a.Lx; t0 = a.Lz + (blockIdx.x - nbz) * PCHUNK;
+  }
+  const int t1 = min(t0 + PCHUNK, lo + n);
   const float* a8 = a.a8 + (int64_t)b * L * 8;
   const float* c8 = a.c8 + (int64_t)b * L * 8;
-  float* s8 = a.s8 + (int64_t)b * L * 8;
   const float sm = a.smooth;
   const int c = tid & 7, stripe = tid >> 3;
   float mx = -INFINITY;
@@ -275,9 +286,9 @@ __global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) 
   mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  if ((tid & 63) < 8) red[tid >> 6][c] = mx;
+  if ((tid & 63) < 8) red[(tid >> 6) * 8 + c] = mx;
   __syncthreads();
-  if (tid < 8) smax[tid] = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
+  if (tid < 8) smax[tid] = fmaxf(fmaxf(red[tid], red[8 + tid]), fmaxf(red[16 + tid], red[24 + tid]));
   __syncthreads();
   const float cm = smax[c];
   float sum = 0.f;
@@ -286,20 +297,44 @@ __global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) 
   sum += __shfl_xor(sum, 16, 64);
   sum += __shfl_xor(sum, 32, 64);
   __syncthreads();
-  if ((tid & 63) < 8) red[tid >> 6][c] = sum;
+  if ((tid & 63) < 8) red[(tid >> 6) * 8 + c] = sum;
   __syncthreads();
-  if (tid < 8) ssum[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+  if (tid < 8) ssum[tid] = (red[tid] + red[8 + tid]) + (red[16 + tid] + red[24 + tid]);
   __syncthreads();
-  for (int i = tid; i < n * 8; i += 256) {
-    const int t = lo + i / 8, ch = i & 7;
+  if (tid < (t1 - t0) * 8) {
+    const int t = t0 + tid / 8, ch = tid & 7;
     const float v = a8[t * 8 + ch];
     const float msk = __expf(v * sm - smax[ch]) / ssum[ch];
-    s8[t * 8 + ch] = msk * v + c8[t * 8 + ch];
+    const float sv = msk * v + c8[t * 8 + ch];
+    f[tid / 8][ch] = sv;
+    a.s8[((int64_t)b * L + t) * 8 + ch] = sv;   // kept for the next layer's folded LN_B + conv0_1
+  }
+  __syncthreads();
+  float w1r[3][8], b1r[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int col = tid + 256 * k;
+    const float4* w4 = reinterpret_cast<const float4*>(a.w1 + col * 8);
+    const float4 p0 = w4[0], p1 = w4[1];
+    w1r[k][0] = p0.x; w1r[k][1] = p0.y; w1r[k][2] = p0.z; w1r[k][3] = p0.w;
+    w1r[k][4] = p1.x; w1r[k][5] = p1.y; w1r[k][6] = p1.z; w1r[k][7] = p1.w;
+    b1r[k] = a.b1[col];
+  }
+  for (int t = t0; t < t1; ++t) {
+    float* prow = a.P + ((int64_t)b * L + t) * C768;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float v = b1r[k];
+#pragma unroll
+      for (int ch = 0; ch < 8; ++ch) v += w1r[k][ch] * f[t - t0][ch];
+      prow[tid + 256 * k] = v;
+    }
   }
 }
 
 void prompt_expand(const PromptArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(prompt_expand_kernel, dim3(2, a.B), dim3(256), 0, s, a);
+  const int nb = (a.Lz + PCHUNK - 1) / PCHUNK + (a.Lx + PCHUNK - 1) / PCHUNK;
+  hipLaunchKernelGGL(prompt_expand_kernel, dim3(nb, a.B), dim3(256), 0, s, a);
 }
 
 // ------------------------------------------------------------------ LN1 with the prompt residual fused
@@ -308,63 +343,37 @@ void prompt_expand(const PromptArgs& a, hipStream_t s) {
 //                    (candidate_elimination_prompt + x_ori add, attn_blocks.py:9-18, vit_ce_prompt.py:310)
 // then out = LN(X[r]) (norm1 of the block).
 __global__ __launch_bounds__(256) void ln_prompt_kernel(const LnPromptArgs a) {
-  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= a.rows) return;
+  const int b = r / a.rows_per_seq, t = r - b * a.rows_per_seq;
   const int L = a.Lz + a.Lx;
-  // conv1x1 rows of this lane's 12 columns (lane*4 + 256*i + e) and their biases
-  float4 w1[3][4][2], b1[3];
+  Row12 x;
+  if (a.mode == 1) {
+    const Row12 tk = load_row(a.tok_rgb + (int64_t)r * C768, lane);
+    const Row12 pp = load_row(a.P + (int64_t)r * C768, lane);
+    const Row12 ps = load_row(a.pos + (int64_t)t * C768, lane);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    b1[i] = reinterpret_cast<const float4*>(a.b1)[lane + 64 * i];
+    for (int i = 0; i < 3; ++i)
+      x.v[i] = make_float4((tk.v[i].x + pp.v[i].x) + ps.v[i].x, (tk.v[i].y + pp.v[i].y) + ps.v[i].y,
+                           (tk.v[i].z + pp.v[i].z) + ps.v[i].z, (tk.v[i].w + pp.v[i].w) + ps.v[i].w);
+  } else {
+    const int slot = t < a.Lz ? t : a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (t - a.Lz)];
+    const Row12 xo = load_row(a.X + (int64_t)r * C768, lane);
+    const Row12 pp = load_row(a.P + ((int64_t)b * L + slot) * C768, lane);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float4* q = reinterpret_cast<const float4*>(a.w1 + ((lane + 64 * i) * 4 + e) * 8);
-      w1[i][e][0] = q[0];
-      w1[i][e][1] = q[1];
-    }
+    for (int i = 0; i < 3; ++i)
+      x.v[i] = make_float4(xo.v[i].x + pp.v[i].x, xo.v[i].y + pp.v[i].y, xo.v[i].z + pp.v[i].z,
+                           xo.v[i].w + pp.v[i].w);
   }
-  const int nw = gridDim.x * 4;
-  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < a.rows; r += nw) {
-    const int b = r / a.rows_per_seq, t = r - b * a.rows_per_seq;
-    const int slot = a.mode == 1 ? t : (t < a.Lz ? t : a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (t - a.Lz)]);
-    const float4* sp = reinterpret_cast<const float4*>(a.s8 + ((int64_t)b * L + slot) * 8);
-    const float4 s0 = sp[0], s1 = sp[1];
-    Row12 pp;   // P = conv1x1(s8) + bias (the order of the reference's 1x1 conv: bias + sum_k w s)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      float pv[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float4 u = w1[i][e][0], v = w1[i][e][1];
-        pv[e] = (&b1[i].x)[e] + u.x * s0.x + u.y * s0.y + u.z * s0.z + u.w * s0.w + v.x * s1.x + v.y * s1.y +
-                v.z * s1.z + v.w * s1.w;
-      }
-      pp.v[i] = make_float4(pv[0], pv[1], pv[2], pv[3]);
-    }
-    Row12 x;
-    if (a.mode == 1) {   // X = (tok_rgb + P) + pos   (vit_ce_prompt.py:218, 240-241)
-      const Row12 tk = load_row(a.tok_rgb + (int64_t)r * C768, lane);
-      const Row12 ps = load_row(a.pos + (int64_t)t * C768, lane);
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        x.v[i] = make_float4((tk.v[i].x + pp.v[i].x) + ps.v[i].x, (tk.v[i].y + pp.v[i].y) + ps.v[i].y,
-                             (tk.v[i].z + pp.v[i].z) + ps.v[i].z, (tk.v[i].w + pp.v[i].w) + ps.v[i].w);
-    } else {             // X = X + P[slot]            (vit_ce_prompt.py:310)
-      const Row12 xo = load_row(a.X + (int64_t)r * C768, lane);
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        x.v[i] = make_float4(xo.v[i].x + pp.v[i].x, xo.v[i].y + pp.v[i].y, xo.v[i].z + pp.v[i].z,
-                             xo.v[i].w + pp.v[i].w);
-    }
-    store_f32(a.X + (int64_t)r * C768, x, lane);
-    const Row12 y = ln_row(x, a.w, a.b, lane);
-    store_bf16(a.out + (int64_t)r * C768, y, lane);
-    if (a.out_lo) store_bf16_lo(a.out_lo + (int64_t)r * C768, y, lane);
-  }
+  store_f32(a.X + (int64_t)r * C768, x, lane);
+  const Row12 y = ln_row(x, a.w, a.b, lane);
+  store_bf16(a.out + (int64_t)r * C768, y, lane);
+  if (a.out_lo) store_bf16_lo(a.out_lo + (int64_t)r * C768, y, lane);
 }
 
-void ln_prompt(const LnPromptArgs& a, hipStream_t s) {
-  const int blocks = min(PD_BLOCKS, (a.rows + 15) / 16);
-  hipLaunchKernelGGL(ln_prompt_kernel, dim3(blocks), dim3(256), 0, s, a);
+void prompt_expand_ln(const PromptArgs& pa, const LnPromptArgs& a, hipStream_t s) {
+  prompt_expand(pa, s);
+  hipLaunchKernelGGL(ln_prompt_kernel, dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
 }
 
 // ------------------------------------------------------------------ candidate elimination
