@@ -155,7 +155,9 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
 /* ---- operator-level entry points (device pointers; used by the parity tests and by hosts that
  *      compose their own pipelines).  epi: 0 bias->bf16, 1 bias+GELU->bf16, 2 C(f32) = R + acc + bias,
  *      3 bias+ReLU->bf16, 4 bias->f32, 5 bias+ReLU->f32, 6 C(f32) = acc + bias + R[m % pos_rows].
- *      conv_hw > 0 selects the implicit 3x3 (pad 1) conv A-operand over an NHWC map.            */
+ *      conv_hw > 0 selects the implicit 3x3 (pad 1) conv A-operand over an NHWC map.  GEMMs with few
+ *      64 x 64 tiles and a long K run split-K here (fp32 partials, fixed-order reduction); the engine
+ *      itself never splits K, so its results do not depend on the batch size.                     */
 int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, void* C, int64_t ldc,
                 const float* R, int64_t ldr, int M, int N, int K, int epi, int conv_hw, int conv_cin, int pos_rows,
                 void* hip_stream);

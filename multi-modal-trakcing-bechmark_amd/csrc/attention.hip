@@ -73,21 +73,38 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
   const bool ce_wave = a.ce_query >= q0 && a.ce_query < q0 + 16;
   const bool ce_lane = ce_wave && (lane & 15) == a.ce_query - q0;
 
-  for (int kb = 0; kb < N; kb += KB) {
-    __syncthreads();
-    for (int q = tid; q < NH * KB * 8; q += WAVES * 64) {
+  // K/V staging, software-pipelined: the next tile's 16-B chunks are loaded into registers while the
+  // current tile is multiplied, then copied to LDS
+  constexpr int NCHT = NH * KB * 8 / (WAVES * 64);   // chunks of K (and of V) per thread per tile
+  uint4 kreg[NCHT], vreg[NCHT];
+  auto fetch = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < NCHT; ++i) {
+      const int q = tid + i * WAVES * 64;
       const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
       const int r = qq >> 3, c = qq & 7, key = kb + r;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      kreg[i] = make_uint4(0, 0, 0, 0);
+      vreg[i] = make_uint4(0, 0, 0, 0);
       if (key < N) {
         const bf16_t* row = (hl ? base_lo : base) + (int64_t)key * C3 + h * 64 + c * 8;
-        kv = *reinterpret_cast<const uint4*>(row + Cd);
-        vv = *reinterpret_cast<const uint4*>(row + 2 * Cd);
+        kreg[i] = *reinterpret_cast<const uint4*>(row + Cd);
+        vreg[i] = *reinterpret_cast<const uint4*>(row + 2 * Cd);
       }
-      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Ks[hl]) + tile_off(r, c)) = kv;
-      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Vs[hl]) + tile_off(r, c)) = vv;
+    }
+  };
+  fetch(0);
+  for (int kb = 0; kb < N; kb += KB) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NCHT; ++i) {
+      const int q = tid + i * WAVES * 64;
+      const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
+      const int r = qq >> 3, c = qq & 7;
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Ks[hl]) + tile_off(r, c)) = kreg[i];
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Vs[hl]) + tile_off(r, c)) = vreg[i];
     }
     __syncthreads();
+    if (kb + KB < N) fetch(kb + KB);
 
     f32x4 sc[4];
 #pragma unroll

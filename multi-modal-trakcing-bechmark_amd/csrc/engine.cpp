@@ -45,6 +45,8 @@ struct LayerW {
   bf16_t *qkv_wl, *proj_wl, *fc1_wl, *fc2_wl;   // low halves (fp32-faithful mode)
   float *qkv_b, *proj_b, *fc1_b, *fc2_b, *n1w, *n1b, *n2w, *n2b;
 };
+constexpr int64_t kSplitKWsElems = 4 << 20;   // 16 MB of fp32 split-K partials (mmt_op_gemm)
+
 struct PromptW {
   float *w00, *b00, *w01, *b01, *w1, *b1, *nw, *nb;
   float* fold;   // deep layers: PromptFold (kernels.h) of LN_B + conv0_1 over the previous s8
@@ -538,6 +540,9 @@ GemmArgs dense(mmt_engine* e, const bf16_t* A, const bf16_t* Al, int64_t lda, co
   a.N = N;
   a.K = K;
   a.amode = A_DENSE;
+  // No split-K inside the engine: it would change the fp32 summation order with the batch size, and a
+  // sequence's boxes must not depend on how many sequences share its launch (test_batch_equals_single).
+  a.ws = nullptr;
   return a;
 }
 
@@ -1230,11 +1235,15 @@ int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const fl
   if (conv_hw > 0 && (conv_cin % 64 || K != 9 * conv_cin || (epi != EPI_RELU_BF16 && epi != EPI_RELU_F32)))
     return MMT_E_ARG;
   static bf16_t* zero = nullptr;
+  static float* ws = nullptr;
   if (!zero && hipMalloc(&zero, 256) == hipSuccess) hipMemset(zero, 0, 256);
+  if (!ws && hipMalloc(&ws, kSplitKWsElems * 4) != hipSuccess) ws = nullptr;
   GemmArgs a{};
   a.g[0] = GemmGroup{(const bf16_t*)A, nullptr, lda, (const bf16_t*)W, nullptr, ldw, bias, Cp, nullptr, ldc, R, ldr};
   a.groups = 1;
   a.zero = zero;
+  a.ws = ws;
+  a.ws_elems = ws ? kSplitKWsElems : 0;
   a.M = M;
   a.N = N;
   a.K = K;

@@ -307,10 +307,14 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   // K loop over an LDS ring of NSTAGE buffers: tiles kt+1 .. kt+NSTAGE-1 are in flight while tile kt
   // is multiplied.  A tile is read only after the issuing waves' counted vmcnt retired it AND a
   // barrier (raw s_barrier: __syncthreads() would drain every in-flight LDS-DMA with vmcnt(0)).
-  const int nk = K / 64;
+  // Split-K (EPI_PARTIAL): workgroup row blockIdx.y takes K-tiles [kbeg, kend) and stores raw sums.
+  const int nk_all = K / 64;
+  const int kbeg = EPI == EPI_PARTIAL ? (int)((int64_t)blockIdx.y * nk_all / args.ksplit) : 0;
+  const int kend = EPI == EPI_PARTIAL ? (int)((int64_t)(blockIdx.y + 1) * nk_all / args.ksplit) : nk_all;
+  const int nk = kend - kbeg;
   constexpr int D = T::NSTAGE - 1;   // tiles in flight ahead of the one being multiplied
   for (int p = 0; p < D; ++p)
-    if (p < nk) issue(p, p);
+    if (p < nk) issue(kbeg + p, p);
   if (nk > 1 && D > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   int stage = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = kt + D;
-    if (ahead < nk) issue(ahead, ahead % T::NSTAGE);
+    if (ahead < nk) issue(kbeg + ahead, ahead % T::NSTAGE);
     compute(stage);
     stage = stage + 1 == T::NSTAGE ? 0 : stage + 1;
     // retire tile kt+1: the loads issued after it (tiles kt+2 .. min(kt+D, nk-1)) may stay in flight
@@ -332,7 +336,22 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   GEMM_STAMP(2);
   // ---- epilogue: lane owns C[m][n..n+3]
   using LT = LdsTile<EPI, BN>;
-  if constexpr (!SPLIT && BM * BN * LT::ESZ <= T::NSTAGE * T::STAGE * 2) {
+  if constexpr (EPI == EPI_PARTIAL) {   // raw partial sums -> workspace slice (blockIdx.z, blockIdx.y)
+    GemmGroup gp{};
+    gp.C = args.ws + ((int64_t)blockIdx.z * args.ksplit + blockIdx.y) * (int64_t)M * args.N;
+    gp.ldc = args.N;
+    char* lds = reinterpret_cast<char*>(smem);
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj) {
+        const int col = wn * T::WN + jj * 16 + (lane >> 4) * 4;
+        const float v[4] = {acc[i][jj][0], acc[i][jj][1], acc[i][jj][2], acc[i][jj][3]};
+        LT::put(lds, wm * T::WM + i * 16 + (lane & 15), col, v);
+      }
+    __syncthreads();
+    LT::template drain<BM, T::NT>(lds, gp, args, m0, n0, M);
+  } else if constexpr (!SPLIT && BM * BN * LT::ESZ <= T::NSTAGE * T::STAGE * 2) {
     char* lds = reinterpret_cast<char*>(smem);
 #pragma unroll
     for (int i = 0; i < T::FM; ++i)
@@ -592,6 +611,41 @@ static void launch_cfg(const GemmArgs& a, int epi, hipStream_t s) {
   }
 }
 
+// split-K reduction: C = epi(sum_s partial_s + bias) in a fixed order (deterministic)
+template <int EPI, bool SPLIT>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args) {
+  const GemmGroup& g = args.g[blockIdx.z];
+  const int64_t MN = (int64_t)args.M * args.N;
+  const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (idx >= MN) return;
+  const int m = (int)(idx / args.N), n = (int)(idx - (int64_t)m * args.N);
+  const float* p = args.ws + (int64_t)blockIdx.z * args.ksplit * MN + idx;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(p);
+  for (int s = 1; s < args.ksplit; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * MN);
+  store4<EPI, SPLIT>(g, args, m, n, acc);
+}
+
+template <int BM, int BN, int WMW, int WNW, int AM, bool SPLIT, int ST>
+static void launch_splitk(const GemmArgs& a0, int epi, int ks, hipStream_t s) {
+  GemmArgs a = a0;
+  a.ksplit = ks;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  a.gm = tiles_m < 8 ? tiles_m : 8;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI_PARTIAL, AM, SPLIT, ST>), dim3(tiles_m * (a.N / BN), ks, a.groups),
+                     dim3(WMW * WNW * 64), 0, s, a);
+  const dim3 rg((unsigned)(((int64_t)a.M * a.N / 4 + 255) / 256), 1, a.groups);
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_BF16, SPLIT>), rg, dim3(256), 0, s, a); break;
+    case EPI_GELU_BF16: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_GELU_BF16, SPLIT>), rg, dim3(256), 0, s, a); break;
+    case EPI_RESID_F32: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_RESID_F32, SPLIT>), rg, dim3(256), 0, s, a); break;
+    case EPI_RELU_BF16: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_RELU_BF16, SPLIT>), rg, dim3(256), 0, s, a); break;
+    case EPI_F32: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_F32, SPLIT>), rg, dim3(256), 0, s, a); break;
+    case EPI_RELU_F32: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_RELU_F32, SPLIT>), rg, dim3(256), 0, s, a); break;
+    case EPI_POS_F32: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_POS_F32, SPLIT>), rg, dim3(256), 0, s, a); break;
+    default: break;
+  }
+}
+
 static int g_force_cfg = -1;   // tuning override (mmt_gemm_force_config), -1 = heuristic
 
 template <bool SPLIT>
@@ -620,6 +674,24 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.N % 128 == 0 && t128 * (a.N / 128) * a.groups >= target) return launch_cfg<128, 128, 4, 2, SPLIT>(a, epi, s);
   if (a.N % 64 == 0) {
     if (t128 * (a.N / 64) * a.groups >= target) return launch_cfg<128, 64, 2, 2, SPLIT>(a, epi, s);
+    // few 64 x 64 tiles and a long K (small batches): split K over workgroups (fp32 partials in the
+    // workspace, fixed-order reduction with the epilogue), at least 4 K-tiles per split
+    const int tiles = t64 * (a.N / 64) * a.groups, nk = a.K / 64;
+    if (a.ws && tiles < 128 && nk >= 8) {
+      int ks = (256 + tiles - 1) / tiles;
+      ks = ks < nk / 4 ? ks : nk / 4;
+      ks = ks < 8 ? ks : 8;
+      while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems) --ks;
+      if (ks > 1) {
+        if (a.amode == A_CONV3) return launch_splitk<64, 64, 2, 2, A_CONV3, SPLIT, 4>(a, epi, ks, s);
+        return launch_splitk<64, 64, 2, 2, A_DENSE, SPLIT, 4>(a, epi, ks, s);
+      }
+    }
+    // few tiles (small batches): each workgroup walks the whole K serially, so keep up to seven
+    // K-tiles in flight (8-deep LDS ring, 128 KB) to cover the L2 / HBM latency of every step
+    if constexpr (!SPLIT)
+      if (a.K >= 12 * 64) return launch_cfg<64, 64, 2, 2, SPLIT, 8>(a, epi, s);
+    if (a.K >= 6 * 64) return launch_cfg<64, 64, 2, 2, SPLIT, 4>(a, epi, s);
     return launch_cfg<64, 64, 2, 2, SPLIT>(a, epi, s);
   }
   if (t64 * (a.N / 32) * a.groups >= target) return launch_cfg<64, 32, 4, 1, SPLIT>(a, epi, s);

@@ -17,6 +17,7 @@ enum Epi : int {
   EPI_F32 = 4,         // bias -> f32
   EPI_RELU_F32 = 5,    // bias, ReLU -> f32
   EPI_POS_F32 = 6,     // C(f32) = (acc + bias) + R[m % pos_rows]  (OSTrack patch-embed + pos_embed)
+  EPI_PARTIAL = 7,     // internal (split-K): raw fp32 partial sums into the workspace
 };
 enum AMode : int { A_DENSE = 0, A_CONV3 = 1 };
 
@@ -38,6 +39,9 @@ struct GemmArgs {
   int pos_rows;     // EPI_POS_F32
   int split;        // 1: fp32-faithful bf16x3 products
   int gm;           // (set by the launcher) tile rows per super-tile group of the tile order
+  int ksplit;       // (set by the launcher) K splits (1: none)
+  float* ws;        // split-K workspace ([groups][ksplit][M][N] fp32) or null: never split
+  int64_t ws_elems; // its capacity in floats
   const bf16_t* zero;   // unused by the buffer-load kernels (kept for ABI stability of the struct)
 };
 

@@ -251,7 +251,7 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
     const int waves = (rows + PR_ROWS - 1) / PR_ROWS;
     hipLaunchKernelGGL(prompt_reduce_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, a);
   } else {
-    const int blocks = min(PD_BLOCKS, (rows + 15) / 16);
+    const int blocks = min(PD_BLOCKS, (rows + 3) / 4);   // small batches: one row per wave
     hipLaunchKernelGGL(prompt_reduce_deep_kernel, dim3(blocks), dim3(256), 0, s, a);
   }
 }
