@@ -687,10 +687,8 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         return launch_splitk<64, 64, 2, 2, A_DENSE, SPLIT, 4>(a, epi, ks, s);
       }
     }
-    // few tiles (small batches): each workgroup walks the whole K serially, so keep up to seven
-    // K-tiles in flight (8-deep LDS ring, 128 KB) to cover the L2 / HBM latency of every step
-    if constexpr (!SPLIT)
-      if (a.K >= 12 * 64) return launch_cfg<64, 64, 2, 2, SPLIT, 8>(a, epi, s);
+    // few tiles (small batches): each workgroup walks the whole K serially, so keep three K-tiles in
+    // flight (4-deep LDS ring; an 8-deep ring measured no better at M = 320)
     if (a.K >= 6 * 64) return launch_cfg<64, 64, 2, 2, SPLIT, 4>(a, epi, s);
     return launch_cfg<64, 64, 2, 2, SPLIT>(a, epi, s);
   }
