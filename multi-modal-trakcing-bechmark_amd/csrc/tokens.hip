@@ -383,50 +383,31 @@ __device__ __forceinline__ bool before(float ka, int va, float kb, int vb) {
   return ka > kb || (ka == kb && va < vb);
 }
 
+// Rank selection instead of a sort network: every search token's position in the descending order
+// (ties -> lower index, the order "before" defines) is the number of tokens before it, counted in
+// one parallel pass over LDS (Ls <= 1024), so there is a single barrier instead of log^2 stages.
 __global__ __launch_bounds__(512) void ce_select_kernel(const CEArgs a) {
   __shared__ float key[1024];
-  __shared__ int val[1024];
   const int b = blockIdx.x, tid = threadIdx.x;
-  int P2 = 1;
-  while (P2 < a.Ls) P2 <<= 1;
   const float* prob = a.prob + (int64_t)b * a.heads * a.Ls;
-  for (int i = tid; i < P2; i += 512) {
-    float s = -INFINITY;
-    if (i < a.Ls) {
-      s = 0.f;
-      for (int h = 0; h < a.heads; ++h) s += prob[h * a.Ls + i];
-      s = s / (float)a.heads;
-    }
-    key[i] = s;
-    val[i] = i;
+  for (int i = tid; i < a.Ls; i += 512) {
+    float s = 0.f;
+    for (int h = 0; h < a.heads; ++h) s += prob[h * a.Ls + i];
+    key[i] = s / (float)a.heads;
   }
   __syncthreads();
-  for (int k = 2; k <= P2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < P2; i += 512) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const bool up = (i & k) == 0;   // this sub-sequence sorted in "before" order
-          const bool ib = before(key[i], val[i], key[ixj], val[ixj]);
-          if (up ? !ib : ib) {
-            const float tk = key[i]; key[i] = key[ixj]; key[ixj] = tk;
-            const int tv = val[i]; val[i] = val[ixj]; val[ixj] = tv;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
   const int Ln = a.Lz + a.keep;
   for (int i = tid; i < a.Ls; i += 512) {
-    const int src = val[i];
-    const int slot = a.gidx_in[b * a.Ls + src];
-    if (i < a.keep) {
-      a.gidx_out[b * a.keep + i] = slot;
-      a.gather[b * Ln + a.Lz + i] = a.Lz + src;
-      a.slot2pos[b * a.Lx + slot] = a.Lz + i;
+    const float ki = key[i];
+    int rank = 0;
+    for (int j = 0; j < a.Ls; ++j) rank += before(key[j], j, ki, i) ? 1 : 0;
+    const int slot = a.gidx_in[b * a.Ls + i];
+    if (rank < a.keep) {
+      a.gidx_out[b * a.keep + rank] = slot;
+      a.gather[b * Ln + a.Lz + rank] = a.Lz + i;
+      a.slot2pos[b * a.Lx + slot] = a.Lz + rank;
     } else {
-      a.removed[b * a.Lx + a.removed_off + (i - a.keep)] = slot;
+      a.removed[b * a.Lx + a.removed_off + (rank - a.keep)] = slot;
       a.slot2pos[b * a.Lx + slot] = -1;
     }
   }
