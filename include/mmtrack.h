@@ -124,6 +124,16 @@ int mmt_siamfc_crop(const uint8_t* frame, int H, int W, int C, int64_t row_strid
 int mmt_siamfc_response(const float* resp, int n, int r, int up, float scale_penalty, double window_influence,
                         const double* hann1d, double hann_sum, float* scratch, float* result, void* hip_stream);
 
+/* RGB-D frame assembly (get_rgbd_frame(..., 'rgbcolormap', depth_clip), depth_utils.py:7-58, as the
+ * RGB-D VOT path calls it, vipt_class.py:79, 92): device RGB (H x W x 3 uint8) + device depth
+ * (H x W uint16) -> device H x W x 6 uint8 frame (R G B | JET colormap in cv2's B G R order).
+ * lut_bgr: device [256][3] colormap, or NULL for the published JET definition; workspace: device
+ * buffer of mmt_rgbd_workspace_bytes() bytes.  Asynchronous on hip_stream.                       */
+size_t mmt_rgbd_workspace_bytes(void);
+int mmt_rgbd_assemble(const uint8_t* rgb, int64_t rgb_stride, const uint16_t* depth, int64_t depth_stride, int H,
+                      int W, int depth_clip, const uint8_t* lut_bgr, uint8_t* out, int64_t out_stride,
+                      void* workspace, size_t ws_bytes, void* hip_stream);
+
 /* ---- DiMP / mfDiMP target classifier (device pointers, fp32) ------------------------------------
  *  feat [I][S][C][H][W] (I training images x S sequences), filter [S][C][fh][fw] (fh*fw <= 25).
  *  mmt_dimp_optimize runs num_iter steepest-descent Gauss-Newton steps in place on `weights`

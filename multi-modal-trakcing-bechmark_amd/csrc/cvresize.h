@@ -44,6 +44,7 @@ __device__ __forceinline__ void cv_linear_u8(const Px& px, int S, int O, int oy,
 
 // interpolateCubic (resize.cpp): coefficients for fractional offset x, A = -0.75
 __device__ __forceinline__ void cv_cubic_coeffs(float x, float* c) {
+#pragma clang fp contract(off)   // separate roundings (HIP's __fmul_rn / __fadd_rn are plain operators)
   const float A = -0.75f;
   const float x1 = __fadd_rn(x, 1.f), omx = __fsub_rn(1.f, x);
   c[0] = __fsub_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fsub_rn(__fmul_rn(A, x1), 5.f * A), x1), 8.f * A), x1), 4.f * A);
@@ -54,6 +55,7 @@ __device__ __forceinline__ void cv_cubic_coeffs(float x, float* c) {
 
 // INTER_CUBIC sample (oy, ox) of the O x O resize of an S x S float map (row pitch S)
 __device__ __forceinline__ float cv_cubic_f32(const float* src, int S, int O, int oy, int ox) {
+#pragma clang fp contract(off)
   const double scale = 1.0 / ((double)O / (double)S);
   float fx = (float)((ox + 0.5) * scale - 0.5), fy = (float)((oy + 0.5) * scale - 0.5);
   const int sx = (int)floorf(fx), sy = (int)floorf(fy);

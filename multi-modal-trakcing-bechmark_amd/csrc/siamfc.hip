@@ -59,6 +59,7 @@ __device__ __forceinline__ float block_reduce_f(float v, float* red, bool is_max
 }
 
 __global__ __launch_bounds__(RT) void siamfc_response_kernel(const SiamRespArgs a) {
+#pragma clang fp contract(off)   // numpy's separate float32 / float64 roundings
   __shared__ float red[RT / 64 + 1];
   __shared__ double dv[RT];
   __shared__ int di[RT];

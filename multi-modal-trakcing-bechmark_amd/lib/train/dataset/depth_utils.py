@@ -18,14 +18,16 @@ def _imread(path, unchanged=False):
 
 
 def normalize_minmax_u8(dp: np.ndarray) -> np.ndarray:
-    """cv2.normalize(dp, None, 0, 255, NORM_MINMAX) followed by the uint8 cast of np.asarray."""
-    d = dp.astype(np.float64)
-    lo, hi = d.min(), d.max()
-    scale = 255.0 / (hi - lo) if hi > lo else 0.0
-    out = (d - lo) * scale
-    if dp.dtype == np.uint8:
-        return np.clip(np.rint(out), 0, 255).astype(np.uint8)
-    return out.astype(dp.dtype).astype(np.uint8) if np.issubdtype(dp.dtype, np.integer) else out.astype(np.uint8)
+    """cv2.normalize(dp, None, 0, 255, NORM_MINMAX) followed by the uint8 cast of np.asarray: scale and
+    shift in double, applied as OpenCV's convertTo does (float multiply-add, round half to even,
+    saturate to the source type), then the low byte (the GPU path, mmt_rgbd_assemble, is identical)."""
+    lo, hi = float(dp.min()), float(dp.max())
+    scale = 255.0 / (hi - lo) if (hi - lo) > np.finfo(np.float64).eps else 0.0
+    shift = 0.0 - lo * scale
+    f = dp.astype(np.float32) * np.float32(scale) + np.float32(shift)
+    top = 255 if dp.dtype == np.uint8 else 65535
+    v = np.clip(np.rint(f), 0, top).astype(np.int64)
+    return (v & 0xFF).astype(np.uint8)
 
 
 def _jet_lut():
@@ -74,3 +76,16 @@ def get_x_frame(color_path, depth_path, dtype='rgbcolormap', depth_clip=False):
 
 def get_rgbd_frame(color_path, depth_path, dtype='rgbcolormap', depth_clip=False):
     return get_x_frame(color_path, depth_path, dtype=dtype, depth_clip=depth_clip)
+
+
+def get_rgbd_frame_device(color_path, depth_path, depth_clip=True, device=None):
+    """get_rgbd_frame(color, depth, 'rgbcolormap', depth_clip) with the clip / NORM_MINMAX / JET / merge
+    done on the GPU (mmtrack_amd.frames.assemble_rgbd): returns the H x W x 6 frame as a CUDA tensor,
+    which the tracker reads in place.  Only the decoded RGB (3 B/pixel) and depth (2 B/pixel) cross PCIe."""
+    from mmtrack_amd.frames import assemble_rgbd
+    rgb = _imread(color_path)
+    dp = _imread(depth_path, unchanged=True)
+    if dp.ndim == 3:
+        dp = dp[..., 0]
+    return assemble_rgbd(rgb, dp.astype(np.uint16, copy=False), depth_clip=depth_clip, device=device)
+

@@ -79,6 +79,9 @@ SIGNATURES = {
     "mmt_xcorr": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P]),
     "mmt_siamfc_crop": (_I, [_P, _I, _I, _I, ctypes.c_int64, _I, _P, _P, _P, _P, _I, _P, _P]),
     "mmt_siamfc_response": (_I, [_P, _I, _I, _I, ctypes.c_float, ctypes.c_double, _P, ctypes.c_double, _P, _P, _P]),
+    "mmt_rgbd_workspace_bytes": (ctypes.c_size_t, []),
+    "mmt_rgbd_assemble": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _I, _I, _I, _P, _P, ctypes.c_int64, _P,
+                               ctypes.c_size_t, _P]),
     "mmt_dimp_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I]),
     "mmt_dimp_apply_filter": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_dimp_feat_transpose": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),

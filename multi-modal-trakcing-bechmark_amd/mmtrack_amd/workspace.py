@@ -121,10 +121,13 @@ def run_sequence(seq_name, seq_home, dataset_name, yaml_name, num_gpu=1, epoch=6
         get = lambda i: frames[i]
         n = len(frames)
     else:
-        from lib.train.dataset.depth_utils import get_x_frame
+        from lib.train.dataset.depth_utils import get_rgbd_frame_device, get_x_frame
         rgb, aux, gt = gen_config(join(seq_home, seq_name), dataset_name)
         xtype = default_xtype(dataset_name, script_name)
-        get = lambda i: get_x_frame(rgb[i], aux[i], dtype=xtype)
+        if xtype == 'rgbcolormap':   # RGB-D: clip / normalise / colormap on the GPU (vipt_class.py:79 flags)
+            get = lambda i: get_rgbd_frame_device(rgb[i], aux[i], depth_clip=True)
+        else:
+            get = lambda i: get_x_frame(rgb[i], aux[i], dtype=xtype)
         n = len(rgb)
     result = np.zeros((n, 4), dtype=np.float64)
     result[0] = np.copy(gt[0])
@@ -218,10 +221,14 @@ def main(modality='rgbt', argv=None):
                 name, fr, gt = syn[i]
                 seqs.append((name, len(fr), (lambda f: (lambda k: f[k]))(fr), gt))
             else:
-                from lib.train.dataset.depth_utils import get_x_frame
+                from lib.train.dataset.depth_utils import get_rgbd_frame_device, get_x_frame
                 rgb, aux, gt = gen_config(join(args.seq_home, names[i]), args.dataset_name)
                 xt = default_xtype(args.dataset_name, args.script_name)
-                seqs.append((names[i], len(rgb), (lambda r, a: (lambda k: get_x_frame(r[k], a[k], dtype=xt)))(rgb, aux), gt))
+                if xt == 'rgbcolormap':
+                    getf = (lambda r, a: (lambda k: get_rgbd_frame_device(r[k], a[k], depth_clip=True)))(rgb, aux)
+                else:
+                    getf = (lambda r, a: (lambda k: get_x_frame(r[k], a[k], dtype=xt)))(rgb, aux)
+                seqs.append((names[i], len(rgb), getf, gt))
         run_batched_dataset(seqs, args.yaml_name, args.batch, modality, args.out_root, args.dataset_name, overrides,
                             script_name=args.script_name)
     else:

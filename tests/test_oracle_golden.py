@@ -172,3 +172,22 @@ def test_cubic_resize_oracle_properties():
             ref[oy, ox] = v
     got = osf.cv2_resize_cubic_f32(src, 272)
     np.testing.assert_allclose(got[::7, ::5], ref[::7, ::5], atol=2e-5)
+
+
+def test_frames_oracle_properties():
+    """oracle/frames.py: NORM_MINMAX spans 0..255, the clip replaces values above 3x the median,
+    the JET table runs blue -> red, and the merged frame keeps the RGB half untouched."""
+    from oracle import frames as ofr
+    rng = np.random.default_rng(0)
+    dp = rng.integers(100, 1000, (40, 50)).astype(np.uint16)
+    d8 = ofr.normalize_minmax_u8(dp)
+    assert d8.min() == 0 and d8.max() == 255
+    lut = ofr.jet_bgr()
+    assert tuple(lut[0]) == (128, 0, 0) and tuple(lut[255]) == (0, 0, 128)   # dark blue .. dark red (BGR)
+    far = dp.copy()
+    far[:5] = 60000
+    rgb = rng.integers(0, 256, (40, 50, 3), dtype=np.uint8)
+    fr = ofr.rgbd_frame(rgb, far, depth_clip=True)
+    np.testing.assert_array_equal(fr[..., :3], rgb)
+    # after the clip the far rows share the top code with the 3x-median clip value
+    assert (fr[:5, :, 3:] == lut[255]).all()
