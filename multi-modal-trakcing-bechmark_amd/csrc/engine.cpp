@@ -50,6 +50,7 @@ constexpr int64_t kSplitKWsElems = 4 << 20;   // 16 MB of fp32 split-K partials 
 struct PromptW {
   float *w00, *b00, *w01, *b01, *w1, *b1, *nw, *nb;
   float* fold;   // deep layers: PromptFold (kernels.h) of LN_B + conv0_1 over the previous s8
+  float *w00f, *b00f;   // deep layers: conv0_0 with the affine of LN_A (prompt_norms[i-1]) folded in
   float smooth;
 };
 
@@ -75,6 +76,9 @@ struct mmt_engine {
   mmt_config cfg{};
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;       // second half of a split launch
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  int overlap_min = 64;                // split launches of >= this many sequences over two streams (0: never)
   std::string err;
   std::map<std::string, std::vector<int64_t>> expected;
   std::vector<std::string> expected_order;
@@ -109,7 +113,7 @@ struct mmt_engine {
   bf16_t *A_rgb_l = nullptr, *A_aux_l = nullptr, *Hn_l = nullptr, *QKV_l = nullptr, *O_l = nullptr, *Hm_l = nullptr,
          *feat_l = nullptr, *h1_l = nullptr, *h2_l = nullptr, *h3_l = nullptr, *zero = nullptr;
   bool split = false;
-  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *P = nullptr, *s8 = nullptr,
+  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *s8 = nullptr,
         *a8 = nullptr,
         *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
@@ -312,6 +316,24 @@ int pack_weights(mmt_engine* e) {
     TRY(upload_f32(e, &w.nw, H(e, "backbone.prompt_norms." + std::to_string(i) + ".weight")));
     TRY(upload_f32(e, &w.nb, H(e, "backbone.prompt_norms." + std::to_string(i) + ".bias")));
     w.fold = nullptr;
+    w.w00f = w.b00f = nullptr;
+    if (i >= 1) {   // conv0_0(LN_A(x)) = (w00 diag gA) xhat + (b00 + w00 bA), in double
+      const auto& W = H(e, p + "conv0_0.weight");
+      const auto& b0 = H(e, p + "conv0_0.bias");
+      const auto& gA = H(e, "backbone.prompt_norms." + std::to_string(i - 1) + ".weight");
+      const auto& bA = H(e, "backbone.prompt_norms." + std::to_string(i - 1) + ".bias");
+      std::vector<float> wf((size_t)8 * C), bf(8);
+      for (int k = 0; k < 8; ++k) {
+        double acc = b0[k];
+        for (int c = 0; c < C; ++c) {
+          wf[(size_t)k * C + c] = (float)((double)W[(size_t)k * C + c] * gA[c]);
+          acc += (double)W[(size_t)k * C + c] * bA[c];
+        }
+        bf[k] = (float)acc;
+      }
+      TRY(upload_f32(e, &w.w00f, wf));
+      TRY(upload_f32(e, &w.b00f, bf));
+    }
     if (i >= 1) {   // PromptFold, in double (kernels.h)
       const auto& W = H(e, p + "conv0_1.weight");            // [8][768]
       const auto& w0 = H(e, p + "conv0_1.bias");
@@ -425,7 +447,6 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->tok_rgb, (size_t)B * L * C * 4},    {(void**)&e->tok_aux, (size_t)B * L * C * 4},
       {(void**)&e->X, (size_t)B * L * C * 4},          {(void**)&e->X2, (size_t)B * L * C * 4},
       {(void**)&e->s8, (size_t)B * L * 8 * 4},         {(void**)&e->a8, (size_t)B * L * 8 * 4},
-      {(void**)&e->P, (size_t)B * L * C * 4},
       {(void**)&e->c8, (size_t)B * L * 8 * 4},         {(void**)&e->Hn, (size_t)B * L * C * 2},
       {(void**)&e->QKV, (size_t)B * L * 3 * C * 2},    {(void**)&e->O, (size_t)B * L * C * 2},
       {(void**)&e->Hm, (size_t)B * L * MLPD * 2},      {(void**)&e->feat, (size_t)B * Lx * C * 2},
@@ -466,7 +487,7 @@ int alloc_acts(mmt_engine* e) {
 }
 
 // ---------------------------------------------------------------- timing probe
-void probe_begin(mmt_engine* e, const char* cls, double flops, double bytes) {
+void probe_begin(mmt_engine* e, hipStream_t st, const char* cls, double flops, double bytes) {
   TimingProbe* p = e->probe.get();
   if (!p || p->cls != cls) return;
   if (p->capture) {
@@ -475,7 +496,7 @@ void probe_begin(mmt_engine* e, const char* cls, double flops, double bytes) {
     hipEventCreate(&b);
     p->capture->ev.push_back({a, b});
     p->capture->work.push_back({flops, bytes});
-    hipEventRecord(a, e->stream);
+    hipEventRecord(a, st);
     return;
   }
   if (p->used == p->ev.size()) {
@@ -484,17 +505,17 @@ void probe_begin(mmt_engine* e, const char* cls, double flops, double bytes) {
     hipEventCreate(&b);
     p->ev.push_back({a, b});
   }
-  hipEventRecord(p->ev[p->used].first, e->stream);
+  hipEventRecord(p->ev[p->used].first, st);
   p->pending_work.push_back({flops, bytes});
 }
-void probe_end(mmt_engine* e, const char* cls) {
+void probe_end(mmt_engine* e, hipStream_t st, const char* cls) {
   TimingProbe* p = e->probe.get();
   if (!p || p->cls != cls) return;
   if (p->capture) {
-    hipEventRecord(p->capture->ev.back().second, e->stream);
+    hipEventRecord(p->capture->ev.back().second, st);
     return;
   }
-  hipEventRecord(p->ev[p->used].second, e->stream);
+  hipEventRecord(p->ev[p->used].second, st);
   p->used++;
 }
 void probe_collect_graph(mmt_engine* e, const GraphEntry& g) {
@@ -546,16 +567,16 @@ GemmArgs dense(mmt_engine* e, const bf16_t* A, const bf16_t* Al, int64_t lda, co
   return a;
 }
 
-void run_gemm(mmt_engine* e, const char* cls, const GemmArgs& a, int epi) {
+void run_gemm(mmt_engine* e, hipStream_t st, const char* cls, const GemmArgs& a, int epi) {
   const double flops = 2.0 * a.M * a.N * (double)a.K * a.groups;
   // algorithmic HBM bytes: A and W once, C once (bf16 or fp32), R once for the residual epilogues
   const bool out16 = epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RELU_BF16;
   const double outb = (double)a.M * a.N * (out16 ? 2.0 : 4.0) * (a.split && out16 ? 2.0 : 1.0);
   const double rb = (epi == EPI_RESID_F32) ? (double)a.M * a.N * 4.0 : 0.0;
   const double bytes = (((double)a.M * a.K + (double)a.N * a.K) * 2.0 * (a.split ? 2.0 : 1.0) + outb + rb) * a.groups;
-  probe_begin(e, cls, flops, bytes);
-  gemm(a, epi, e->stream);
-  probe_end(e, cls);
+  probe_begin(e, st, cls, flops, bytes);
+  gemm(a, epi, st);
+  probe_end(e, st, cls);
 }
 
 // offset a possibly-null low-half pointer
@@ -564,10 +585,44 @@ inline T* off(T* p, size_t o) {
   return p ? p + o : nullptr;
 }
 
-void enqueue_forward(mmt_engine* e, int b0, int n) {
+void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
   const auto& c = e->cfg;
-  hipStream_t s = e->stream;
   const int Lz = e->Lz, Lx = e->Lx, L = e->L;
+  // per-launch activation views: this launch covers launch-relative sequences [r0, r0 + n)
+  auto* const q_X = off(e->X, (size_t)r0 * (size_t)L * C);
+  auto* const q_X2 = off(e->X2, (size_t)r0 * (size_t)L * C);
+  auto* const q_tok_rgb = off(e->tok_rgb, (size_t)r0 * (size_t)L * C);
+  auto* const q_tok_aux = off(e->tok_aux, (size_t)r0 * (size_t)L * C);
+  auto* const q_a8 = off(e->a8, (size_t)r0 * (size_t)L * 8);
+  auto* const q_c8 = off(e->c8, (size_t)r0 * (size_t)L * 8);
+  auto* const q_s8 = off(e->s8, (size_t)r0 * (size_t)L * 8);
+  auto* const q_Hn = off(e->Hn, (size_t)r0 * (size_t)L * C);
+  auto* const q_Hn_l = off(e->Hn_l, (size_t)r0 * (size_t)L * C);
+  auto* const q_QKV = off(e->QKV, (size_t)r0 * (size_t)L * 3 * C);
+  auto* const q_QKV_l = off(e->QKV_l, (size_t)r0 * (size_t)L * 3 * C);
+  auto* const q_O = off(e->O, (size_t)r0 * (size_t)L * C);
+  auto* const q_O_l = off(e->O_l, (size_t)r0 * (size_t)L * C);
+  auto* const q_Hm = off(e->Hm, (size_t)r0 * (size_t)L * MLPD);
+  auto* const q_Hm_l = off(e->Hm_l, (size_t)r0 * (size_t)L * MLPD);
+  auto* const q_ce_prob = off(e->ce_prob, (size_t)r0 * (size_t)HEADS * Lx);
+  auto* const q_feat = off(e->feat, (size_t)r0 * (size_t)Lx * C);
+  auto* const q_feat_l = off(e->feat_l, (size_t)r0 * (size_t)Lx * C);
+  auto* const q_dbg_feat = off(e->dbg_feat, (size_t)r0 * (size_t)L * C);
+  auto* const q_h1 = off(e->h1, (size_t)r0 * (size_t)Lx * 3 * c.head_channels);
+  auto* const q_h1_l = off(e->h1_l, (size_t)r0 * (size_t)Lx * 3 * c.head_channels);
+  auto* const q_h2 = off(e->h2, (size_t)r0 * (size_t)Lx * 3 * (c.head_channels / 2));
+  auto* const q_h2_l = off(e->h2_l, (size_t)r0 * (size_t)Lx * 3 * (c.head_channels / 2));
+  auto* const q_h3 = off(e->h3, (size_t)r0 * (size_t)Lx * 3 * (c.head_channels / 4));
+  auto* const q_h3_l = off(e->h3_l, (size_t)r0 * (size_t)Lx * 3 * (c.head_channels / 4));
+  auto* const q_h4 = off(e->h4, (size_t)r0 * (size_t)Lx * 3 * 32);
+  auto* const q_res = off(e->res, (size_t)r0 * (size_t)8);
+  auto* const q_dbg_maps = off(e->dbg_maps, (size_t)r0 * (size_t)5 * Lx);
+  auto* const q_gidx0 = off(e->gidx0, (size_t)r0 * (size_t)Lx);
+  auto* const q_gidx1 = off(e->gidx1, (size_t)r0 * (size_t)Lx);
+  auto* const q_slot2pos = off(e->slot2pos, (size_t)r0 * (size_t)Lx);
+  auto* const q_gather = off(e->gather, (size_t)r0 * (size_t)L);
+  auto* const q_removed = off(e->removed, (size_t)r0 * (size_t)Lx);
+  auto* const q_dbg_patch = off(e->dbg_patch, (size_t)r0 * (size_t)c.search_size * c.search_size * c.in_chans);
   const bool vipt = c.model == MMT_MODEL_VIPT;
   const bool prompted = vipt && c.prompt_type != MMT_PROMPT_NONE;
   const bool deep = vipt && c.prompt_type == MMT_PROMPT_DEEP;
@@ -578,7 +633,7 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
 
   // 1. crop + normalise + patchify the search region of every sequence
   CropArgs ca{};
-  ca.params = e->params_dev;
+  ca.params = e->params_dev + r0;
   ca.B = n;
   ca.out_sz = c.search_size;
   ca.C = c.in_chans;
@@ -588,59 +643,56 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
   ca.A_aux_lo = A_aux_l;
   ca.rows_per_seq = L;
   ca.row0 = Lz;
-  ca.dbg_patch = e->dbg_patch;
+  ca.dbg_patch = q_dbg_patch;
   crop_patchify(ca, s);
 
   // 2. patch embedding (template rows were written at initialize)
-  float* X = e->X;
-  float* X2 = e->X2;
+  float* X = q_X;
+  float* X2 = q_X2;
   if (vipt) {
-    GemmArgs g = dense(e, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, e->tok_rgb, nullptr, C, nullptr, 0,
+    GemmArgs g = dense(e, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, q_tok_rgb, nullptr, C, nullptr, 0,
                        n * L, C, C);
-    g.g[1] = GemmGroup{A_aux, A_aux_l, C, e->pep_w, e->pep_wl, C, e->pep_b, e->tok_aux, nullptr, C, nullptr, 0};
+    g.g[1] = GemmGroup{A_aux, A_aux_l, C, e->pep_w, e->pep_wl, C, e->pep_b, q_tok_aux, nullptr, C, nullptr, 0};
     g.groups = 2;
-    run_gemm(e, "patch", g, EPI_F32);
+    run_gemm(e, s, "patch", g, EPI_F32);
   } else {
     GemmArgs g = dense(e, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, X, nullptr, C, e->pos, C, n * L, C, C);
     g.pos_rows = L;
-    run_gemm(e, "patch", g, EPI_POS_F32);
+    run_gemm(e, s, "patch", g, EPI_POS_F32);
   }
-  init_indices(e->gidx0, e->slot2pos, n, Lz, Lx, s);
+  init_indices(q_gidx0, q_slot2pos, n, Lz, Lx, s);
 
   PromptArgs pa{};
   pa.B = n;
   pa.Lz = Lz;
   pa.Lx = Lx;
-  pa.a8 = e->a8;
-  pa.c8 = e->c8;
-  pa.s8 = e->s8;
-  pa.P = e->P;
+  pa.a8 = q_a8;
+  pa.c8 = q_c8;
+  pa.s8 = q_s8;
   auto set_prompt = [&](int i, int lnA) {
     pa.layer = i;
     pa.lnA_w = e->pw[lnA].nw;
     pa.lnA_b = e->pw[lnA].nb;
     pa.lnB_w = e->pw[i].nw;
     pa.lnB_b = e->pw[i].nb;
-    pa.w00 = e->pw[i].w00;
-    pa.b00 = e->pw[i].b00;
+    pa.w00 = i ? e->pw[i].w00f : e->pw[i].w00;   // deep layers: LN_A's affine folded in
+    pa.b00 = i ? e->pw[i].b00f : e->pw[i].b00;
     pa.w01 = e->pw[i].w01;
     pa.b01 = e->pw[i].b01;
     pa.fold = e->pw[i].fold;
-    pa.w1 = e->pw[i].w1;
-    pa.b1 = e->pw[i].b1;
     pa.smooth = e->pw[i].smooth;
   };
   if (prompted) {  // layer-0 prompt: vit_ce_prompt.py:205-219
     set_prompt(0, 0);
-    pa.srcA = e->tok_rgb;
+    pa.srcA = q_tok_rgb;
     pa.srcA_rows = L;
-    pa.srcB = e->tok_aux;
+    pa.srcB = q_tok_aux;
     pa.slot2pos = nullptr;
     prompt_reduce(pa, s);   // fovea, P and X = tok_rgb + P + pos are formed with block 0's LN1
   }
 
-  int* gin = e->gidx0;
-  int* gout = e->gidx1;
+  int* gin = q_gidx0;
+  int* gout = q_gidx1;
   int removed_off = 0;
   int Ls = Lx;
   for (int i = 0; i < DEPTH; ++i) {
@@ -652,7 +704,7 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       pa.srcA = X;
       pa.srcA_rows = Na;
       pa.srcB = nullptr;
-      pa.slot2pos = e->slot2pos;
+      pa.slot2pos = q_slot2pos;
       prompt_reduce(pa, s);
       ln_mode = 2;
     }
@@ -664,39 +716,41 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       la.Lz = Lz;
       la.Lx = Lx;
       la.X = X;
-      la.P = e->P;
-      la.tok_rgb = e->tok_rgb;
+      la.s8 = q_s8;
+      la.w1 = e->pw[i].w1;   // conv1x1 of the prompt block that ran for this layer
+      la.b1 = e->pw[i].b1;
+      la.tok_rgb = q_tok_rgb;
       la.pos = e->pos;
       la.gidx = gin;
       la.w = w.n1w;
       la.b = w.n1b;
-      la.out = e->Hn;
-      la.out_lo = e->Hn_l;
+      la.out = q_Hn;
+      la.out_lo = q_Hn_l;
       prompt_expand_ln(pa, la, s);
     } else {
-      layernorm(X, w.n1w, w.n1b, e->Hn, e->Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+      layernorm(X, w.n1w, w.n1b, q_Hn, q_Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
     }
-    run_gemm(e, "qkv",
-             dense(e, e->Hn, e->Hn_l, C, w.qkv_w, w.qkv_wl, C, w.qkv_b, e->QKV, e->QKV_l, 3 * C, nullptr, 0, n * Na,
+    run_gemm(e, s, "qkv",
+             dense(e, q_Hn, q_Hn_l, C, w.qkv_w, w.qkv_wl, C, w.qkv_b, q_QKV, q_QKV_l, 3 * C, nullptr, 0, n * Na,
                    3 * C, C),
              EPI_BF16);
     const bool ce = e->keep_at[i] != e->ls_before[i];
     AttnArgs aa{};
-    aa.qkv = e->QKV;
-    aa.qkv_lo = e->QKV_l;
-    aa.out = e->O;
-    aa.out_lo = e->O_l;
+    aa.qkv = q_QKV;
+    aa.qkv_lo = q_QKV_l;
+    aa.out = q_O;
+    aa.out_lo = q_O_l;
     aa.B = n;
     aa.N = Na;
     aa.heads = HEADS;
     aa.ce_query = ce ? c.ce_template_index : -1;
     aa.ce_lens_t = Lz;
-    aa.ce_prob = e->ce_prob;
-    probe_begin(e, "attn", 4.0 * n * HEADS * (double)Na * Na * 64, (double)n * Na * 4 * C * 2);
+    aa.ce_prob = q_ce_prob;
+    probe_begin(e, s, "attn", 4.0 * n * HEADS * (double)Na * Na * 64, (double)n * Na * 4 * C * 2);
     attention(aa, s);
-    probe_end(e, "attn");
-    run_gemm(e, "proj",
-             dense(e, e->O, e->O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
+    probe_end(e, s, "attn");
+    run_gemm(e, s, "proj",
+             dense(e, q_O, q_O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
              EPI_RESID_F32);
     if (ce) {  // attn_blocks.py:99-101
       const int keep = e->keep_at[i];
@@ -707,42 +761,42 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       ce_a.keep = keep;
       ce_a.heads = HEADS;
       ce_a.Lx = Lx;
-      ce_a.prob = e->ce_prob;
+      ce_a.prob = q_ce_prob;
       ce_a.gidx_in = gin;
       ce_a.gidx_out = gout;
-      ce_a.gather = e->gather;
-      ce_a.slot2pos = e->slot2pos;
-      ce_a.removed = e->removed;
+      ce_a.gather = q_gather;
+      ce_a.slot2pos = q_slot2pos;
+      ce_a.removed = q_removed;
       ce_a.removed_off = removed_off;
       ce_select(ce_a, s);
       removed_off += Ls - keep;
       std::swap(gin, gout);
       Ls = keep;
-      layernorm(X, w.n2w, w.n2b, e->Hn, e->Hn_l, nullptr, n * (Lz + Ls), Lz + Ls, e->gather, Na, X2, s);
+      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, nullptr, n * (Lz + Ls), Lz + Ls, q_gather, Na, X2, s);
       std::swap(X, X2);
     } else {
-      layernorm(X, w.n2w, w.n2b, e->Hn, e->Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
     }
     const int Nm = Lz + Ls;
-    run_gemm(e, "fc1",
-             dense(e, e->Hn, e->Hn_l, C, w.fc1_w, w.fc1_wl, C, w.fc1_b, e->Hm, e->Hm_l, MLPD, nullptr, 0, n * Nm, MLPD,
+    run_gemm(e, s, "fc1",
+             dense(e, q_Hn, q_Hn_l, C, w.fc1_w, w.fc1_wl, C, w.fc1_b, q_Hm, q_Hm_l, MLPD, nullptr, 0, n * Nm, MLPD,
                    C),
              EPI_GELU_BF16);
-    run_gemm(e, "fc2",
-             dense(e, e->Hm, e->Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C, n * Nm, C, MLPD),
+    run_gemm(e, s, "fc2",
+             dense(e, q_Hm, q_Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C, n * Nm, C, MLPD),
              EPI_RESID_F32);
   }
-  final_norm_recover(X, Lz + Ls, e->slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, e->feat, e->feat_l, e->dbg_feat, s);
+  final_norm_recover(X, Lz + Ls, q_slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, q_feat, q_feat_l, q_dbg_feat, s);
 
   // CENTER head: conv1 of the three branches fused (N = 3*hc), then per-branch grouped convs
   const int hc = c.head_channels, fs = e->fs, M = n * Lx;
   {
-    GemmArgs g = dense(e, e->feat, e->feat_l, C, e->hw1, e->hw1l, 9 * C, e->hb1, e->h1, e->h1_l, 3 * hc, nullptr, 0,
+    GemmArgs g = dense(e, q_feat, q_feat_l, C, e->hw1, e->hw1l, 9 * C, e->hb1, q_h1, q_h1_l, 3 * hc, nullptr, 0,
                        M, 3 * hc, 9 * C);
     g.amode = A_CONV3;
     g.conv_hw = fs;
     g.conv_cin = C;
-    run_gemm(e, "conv1", g, EPI_RELU_BF16);
+    run_gemm(e, s, "conv1", g, EPI_RELU_BF16);
   }
   const int ch[4] = {hc, hc / 2, hc / 4, hc / 8};
   for (int j = 0; j < 3; ++j) {   // conv2, conv3, conv4
@@ -753,23 +807,23 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
       const bf16_t *A, *Al;
       int64_t lda;
       if (j == 0) {
-        A = e->h1 + k * hc;
-        Al = off(e->h1_l, (size_t)k * hc);
+        A = q_h1 + k * hc;
+        Al = off(q_h1_l, (size_t)k * hc);
         lda = 3 * hc;
       } else {
-        A = (j == 1 ? e->h2 : e->h3) + (size_t)k * M * ci;
-        Al = off(j == 1 ? e->h2_l : e->h3_l, (size_t)k * M * ci);
+        A = (j == 1 ? q_h2 : q_h3) + (size_t)k * M * ci;
+        Al = off(j == 1 ? q_h2_l : q_h3_l, (size_t)k * M * ci);
         lda = ci;
       }
       void *Cout, *Cl;
       if (j == 0) {
-        Cout = e->h2 + (size_t)k * M * co;
-        Cl = off(e->h2_l, (size_t)k * M * co);
+        Cout = q_h2 + (size_t)k * M * co;
+        Cl = off(q_h2_l, (size_t)k * M * co);
       } else if (j == 1) {
-        Cout = e->h3 + (size_t)k * M * co;
-        Cl = off(e->h3_l, (size_t)k * M * co);
+        Cout = q_h3 + (size_t)k * M * co;
+        Cl = off(q_h3_l, (size_t)k * M * co);
       } else {
-        Cout = e->h4 + (size_t)k * M * co;
+        Cout = q_h4 + (size_t)k * M * co;
         Cl = nullptr;
       }
       g.g[k] = GemmGroup{A, Al, lda, e->hw[j] + (size_t)k * co * 9 * ci, off(e->hwl[j], (size_t)k * co * 9 * ci),
@@ -779,17 +833,17 @@ void enqueue_forward(mmt_engine* e, int b0, int n) {
     g.amode = A_CONV3;
     g.conv_hw = fs;
     g.conv_cin = ci;
-    run_gemm(e, j == 0 ? "conv2" : (j == 1 ? "conv3" : "conv4"), g, j == 2 ? EPI_RELU_F32 : EPI_RELU_BF16);
+    run_gemm(e, s, j == 0 ? "conv2" : (j == 1 ? "conv3" : "conv4"), g, j == 2 ? EPI_RELU_F32 : EPI_RELU_BF16);
   }
   DecodeArgs da{};
   da.B = n;
   da.fs = fs;
-  da.h4 = e->h4;
+  da.h4 = q_h4;
   da.w5 = e->w5;
   da.b5 = e->b5;
   da.hann = e->hann;
-  da.res = e->res;
-  da.maps = e->dbg_maps;
+  da.res = q_res;
+  da.maps = q_dbg_maps;
   decode(da, s);
 }
 
@@ -849,12 +903,30 @@ void update_state(mmt_engine* e, int slot, const float* r, int Hh, int Ww, doubl
   st = {x1, y1, bw, bh};
 }
 
+// One launch over n sequences.  Batches of >= overlap_min sequences run as two independent halves on
+// two streams (fork/join events, also valid inside stream capture): the halves' kernels overlap, so one
+// half's latency-bound kernels (LayerNorm, prompt, CE select, head tails) fill the CUs the other
+// half's GEMM tails leave idle.  Each half owns disjoint activation rows, results are unchanged.
+void enqueue_split(mmt_engine* e, int b0, int n) {
+  if (e->overlap_min <= 0 || n < e->overlap_min || e->probe) {
+    enqueue_forward(e, b0, 0, n, e->stream);
+    return;
+  }
+  const int n1 = n / 2;
+  hipEventRecord(e->fork_ev, e->stream);
+  hipStreamWaitEvent(e->stream2, e->fork_ev, 0);
+  enqueue_forward(e, b0, 0, n1, e->stream);
+  enqueue_forward(e, b0 + n1, n1, n - n1, e->stream2);
+  hipEventRecord(e->join_ev, e->stream2);
+  hipStreamWaitEvent(e->stream, e->join_ev, 0);
+}
+
 int launch(mmt_engine* e, int b0, int n, const GraphEntry** replayed) {
   *replayed = nullptr;
   // HIP does not time event-record nodes captured into a graph, so the kernel timing probe runs the
   // identical launch sequence eagerly, bracketing the probed kernel class with stream events
   if (!e->cfg.use_graphs || e->probe) {
-    enqueue_forward(e, b0, n);
+    enqueue_split(e, b0, n);
     HIPCHECK(e, hipGetLastError());
     return MMT_OK;
   }
@@ -869,14 +941,14 @@ int launch(mmt_engine* e, int b0, int n, const GraphEntry** replayed) {
       p->used = 0;
       p->pending_work.clear();
     }
-    enqueue_forward(e, b0, n);
+    enqueue_split(e, b0, n);
     HIPCHECK(e, hipGetLastError());
     GraphEntry entry;
     if (p) p->capture = &entry;
     hipGraph_t g;
     hipError_t st = hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal);
     if (st == hipSuccess) {
-      enqueue_forward(e, b0, n);
+      enqueue_split(e, b0, n);
       st = hipStreamEndCapture(e->stream, &g);
     }
     if (p) p->capture = nullptr;
@@ -940,6 +1012,11 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   }
   if (hipSetDevice(device) != hipSuccess) return MMT_E_HIP;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
+  if (hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
+  if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess)
+    return MMT_E_HIP;
+  if (const char* ov = std::getenv("MMT_OVERLAP_MIN")) e->overlap_min = std::atoi(ov);
   build_expected(e.get());
   e->frame_dev.assign(c.max_batch, nullptr);
   e->frame_cap.assign(c.max_batch, 0);
@@ -974,6 +1051,9 @@ void mmt_destroy(mmt_engine* e) {
   if (e->params_host) hipHostFree(e->params_host);
   if (e->res_host) hipHostFree(e->res_host);
   if (e->stream) hipStreamDestroy(e->stream);
+  if (e->stream2) hipStreamDestroy(e->stream2);
+  if (e->fork_ev) hipEventDestroy(e->fork_ev);
+  if (e->join_ev) hipEventDestroy(e->join_ev);
   delete e;
 }
 

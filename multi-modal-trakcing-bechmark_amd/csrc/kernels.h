@@ -77,7 +77,7 @@ struct PromptArgs {
   const int* slot2pos;       // [B][Lx] compact position (or -1) of search slots; null at layer 0
   const float* lnA_w; const float* lnA_b;   // prompt_norms[i-1] (layer 0: prompt_norms[0])
   const float* lnB_w; const float* lnB_b;   // prompt_norms[i] (layer 0 only; deep layers use fold)
-  const float* w00; const float* b00;       // conv0_0 [8][768]
+  const float* w00; const float* b00;       // conv0_0 [8][768] (deep layers: LN_A's gamma / beta folded in)
   const float* w01; const float* b01;       // conv0_1 [8][768] (layer 0 only)
   const float* fold;         // deep layers: LN_B + conv0_1 folded onto the previous s8 (PromptFold)
   float smooth;              // fovea.smooth (device scalar copied to host at load)
@@ -85,8 +85,6 @@ struct PromptArgs {
   float* c8;                 // scratch [B][L][8]
   float* s8;                 // prompt block output before conv1x1 [B][L][8] (the next layer folds
                              // LN_B + conv0_1 onto it instead of reading P)
-  const float* w1; const float* b1;         // conv1x1 [768][8]
-  float* P;                  // out prompt [B][L][768] (full slot layout)
 };
 // PromptFold (float[160]) for deep layer i, from prompt_norms[i] (g, b), conv0_1 of block i (W, w0)
 // and conv1x1 of block i-1 (V [768][8], v0): with V' / v0' the column-centred V / v0,
@@ -101,15 +99,16 @@ struct LnPromptArgs {
   int mode;                  // 1: layer 0 (X = tok_rgb + P + pos), 2: deep layer (X += P[slot])
   int rows, rows_per_seq, Lz, Lx;
   float* X;
-  const float* P;            // [B][Lz+Lx][768]
+  const float* s8;           // [B][Lz+Lx][8] fovea output of every slot (PromptArgs::s8)
+  const float* w1; const float* b1;         // conv1x1 [768][8] -> the prompt P = w1 s8 + b1
   const float* tok_rgb;      // mode 1
   const float* pos;          // mode 1: [Lz+Lx][768]
   const int* gidx;           // mode 2: [B][rows_per_seq - Lz] slot of each compact search token
   const float* w; const float* b;
   bf16_t* out; bf16_t* out_lo;
 };
-void prompt_expand(const PromptArgs& a, hipStream_t s);
-// prompt_expand (s8 + P for every slot), then the prompt residual and LN1 for the compact rows
+// fovea (s8 for every slot), then the prompt residual (conv1x1 of s8, formed in registers) and LN1
+// for the compact rows
 void prompt_expand_ln(const PromptArgs& pa, const LnPromptArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- candidate elimination

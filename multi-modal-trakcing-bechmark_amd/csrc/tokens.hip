@@ -49,6 +49,25 @@ __device__ __forceinline__ Row12 ln_row(const Row12& x, const float* w, const fl
   return y;
 }
 
+// (x - mean) * rstd, the affine applied by the caller (or folded into the consumer's weights)
+__device__ __forceinline__ Row12 ln_hat(const Row12& x) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) s += x.v[i].x + x.v[i].y + x.v[i].z + x.v[i].w;
+  const float mean = wave_sum(s) * (1.0f / C768);
+  float q = 0.f;
+  Row12 d;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    d.v[i] = make_float4(x.v[i].x - mean, x.v[i].y - mean, x.v[i].z - mean, x.v[i].w - mean);
+    q += d.v[i].x * d.v[i].x + d.v[i].y * d.v[i].y + d.v[i].z * d.v[i].z + d.v[i].w * d.v[i].w;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / C768) + LN_EPS);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d.v[i] = make_float4(d.v[i].x * rstd, d.v[i].y * rstd, d.v[i].z * rstd, d.v[i].w * rstd);
+  return d;
+}
+
 __device__ __forceinline__ void store_bf16(bf16_t* p, const Row12& y, int lane) {
   uint2* q = reinterpret_cast<uint2*>(p);
 #pragma unroll
@@ -188,55 +207,103 @@ __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) 
   }
 }
 
-// Deep layers: conv0_0(LN_A(recovered X)) with conv0_0 held in registers (each lane keeps its 12
-// columns x 8 outputs) over a grid-strided run of rows; conv0_1(LN_B(P_prev)) from the previous s8 and
-// the folded constants (PromptFold) -- 8 floats per token instead of a 768-float prompt row.
-constexpr int PD_BLOCKS = 512;
+// Deep layers: conv0_0(LN_A(recovered X)) with conv0_0 (LN_A's affine folded in) in LDS;
+// conv0_1(LN_B(P_prev)) from the previous s8 and the folded constants (PromptFold) -- 8 floats per
+// token instead of a 768-float prompt row.
+// Each wave owns R rows (r0, r0 + nw, ...).  Every load the wave needs -- the rows' compact
+// positions, then the R rows -- is issued before the block's weight fill and barrier, so a wave
+// has all of its bytes in flight at once and the kernel runs at HBM rate even though each wave only
+// sees a few rows.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && atoi(v) > 0 ? atoi(v) : dflt;
+}
 
-__global__ __launch_bounds__(256) void prompt_reduce_deep_kernel(const PromptArgs a) {
+constexpr int TOK_THREADS = 512;   // 8 waves per block share one LDS copy of the weights
+
+struct DeepIn {
+  Row12 x;
+  float4 s0, s1;
+};
+
+// compact position of slot row `row` (-1: pruned search slot)
+__device__ __forceinline__ int deep_pos(const PromptArgs& a, int row, int L) {
+  const int b = row / L, s = row - b * L;
+  return s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];
+}
+
+__device__ __forceinline__ DeepIn deep_fetch(const PromptArgs& a, int row, int pos, int L, int lane) {
+  const int b = row / L;
+  DeepIn d;
+  // unconditional load (a pruned slot reads compact row 0 and discards it): branch-free, so the
+  // in-order vmcnt waits count exactly the loads issued
+  d.x = load_row(a.srcA + ((int64_t)b * a.srcA_rows + max(pos, 0)) * C768, lane);
+  if (pos < 0) d.x = zero_row();
+  const float4* sp = reinterpret_cast<const float4*>(a.s8 + (int64_t)row * 8);
+  d.s0 = sp[0];
+  d.s1 = sp[1];
+  return d;
+}
+
+template <int R>
+__global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const PromptArgs a) {
   __shared__ float fold[FOLD_N];
-  for (int i = threadIdx.x; i < FOLD_N; i += 256) fold[i] = a.fold[i];
-  __syncthreads();
-  const int L = a.Lz + a.Lx, lane = threadIdx.x & 63;
-  float4 w[8][3];
+  __shared__ __attribute__((aligned(16))) float W0[8 * C768];   // conv0_0 (LN_A affine folded in)
+  const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, rows = a.B * L;
+  const int nw = gridDim.x * (TOK_THREADS / 64);
+  const int r0 = blockIdx.x * (TOK_THREADS / 64) + (threadIdx.x >> 6);
+  // 1. positions of the wave's rows (lane j: row r0 + j * nw), 2. the weights, 3. the rows
+  const int pr = r0 + lane * nw;
+  const int posv = (lane < R && pr < rows) ? deep_pos(a, pr, L) : -1;
+  constexpr int WV = 8 * C768 / 4 / TOK_THREADS;
+  float4 wst[WV];
 #pragma unroll
-  for (int k = 0; k < 8; ++k)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) w[k][i] = reinterpret_cast<const float4*>(a.w00 + k * C768)[lane + 64 * i];
+  for (int k = 0; k < WV; ++k) wst[k] = reinterpret_cast<const float4*>(a.w00)[threadIdx.x + TOK_THREADS * k];
+  const float fo = threadIdx.x < FOLD_N ? a.fold[threadIdx.x] : 0.f;
   const float ba = lane < 8 ? a.b00[lane] : 0.f;
+  DeepIn in[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int rj = min(r0 + j * nw, rows - 1);
+    in[j] = deep_fetch(a, rj, __shfl(posv, j, 64), L, lane);
+  }
+#pragma unroll
+  for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[threadIdx.x + TOK_THREADS * k] = wst[k];
+  if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
+  __syncthreads();
   const int kk = lane & 7;
-  const int nw = gridDim.x * 4;
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < a.B * L; row += nw) {
-    const int b = row / L, s = row - b * L;
-    const int pos = s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];
-    const Row12 xa = pos >= 0 ? load_row(a.srcA + ((int64_t)b * a.srcA_rows + pos) * C768, lane) : zero_row();
-    const Row12 y = ln_row(xa, a.lnA_w, a.lnA_b, lane);
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int row = r0 + j * nw;
+    if (row >= rows) break;
+    const Row12 y = ln_hat(in[j].x);   // LN_A's affine is folded into w00 / b00 (engine pack_weights)
     float part[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float t = 0.f;
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
-        t += y.v[i].x * w[k][i].x + y.v[i].y * w[k][i].y + y.v[i].z * w[k][i].z + y.v[i].w * w[k][i].w;
+      for (int i = 0; i < 3; ++i) {
+        const float4 w = reinterpret_cast<const float4*>(W0 + k * C768)[lane + 64 * i];
+        t += y.v[i].x * w.x + y.v[i].y * w.y + y.v[i].z * w.z + y.v[i].w * w.w;
+      }
       part[k] = t;
     }
     const float ra = reduce8(part, lane);
     // c8 from the previous prompt's s8
-    const float4* sp = reinterpret_cast<const float4*>(a.s8 + (int64_t)row * 8);
-    const float4 s0 = sp[0], s1 = sp[1];
-    const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sv[8] = {in[j].s0.x, in[j].s0.y, in[j].s0.z, in[j].s0.w,
+                         in[j].s1.x, in[j].s1.y, in[j].s1.z, in[j].s1.w};
     float var = fold[FOLD_gb];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float gj = 2.f * fold[FOLD_g + j];
+    for (int q = 0; q < 8; ++q) {
+      float gj = 2.f * fold[FOLD_g + q];
 #pragma unroll
-      for (int l = 0; l < 8; ++l) gj += fold[FOLD_G + j * 8 + l] * sv[l];
-      var += gj * sv[j];
+      for (int l = 0; l < 8; ++l) gj += fold[FOLD_G + q * 8 + l] * sv[l];
+      var += gj * sv[q];
     }
     const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + LN_EPS);
     float mk = fold[FOLD_mc + kk];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) mk += fold[FOLD_MC + kk * 8 + j] * sv[j];
+    for (int q = 0; q < 8; ++q) mk += fold[FOLD_MC + kk * 8 + q] * sv[q];
     const float rb = rstd * mk + fold[FOLD_cb + kk];
     if (lane < 8) {
       a.a8[(int64_t)row * 8 + lane] = ra + ba;
@@ -245,44 +312,61 @@ __global__ __launch_bounds__(256) void prompt_reduce_deep_kernel(const PromptArg
   }
 }
 
+// rows per wave (tuning knob MMT_TOK_WAVES = the wave count to aim for; R = 1 measured fastest at
+// B = 32 on MI355X, the weights' LDS fill is amortised over the block's 8 waves)
+static int rows_per_wave(int rows) {
+  static const int target = env_int("MMT_TOK_WAVES", 1 << 24);   // default: one row per wave (measured best)
+  return rows >= 3 * target ? 4 : rows >= 2 * target ? 3 : rows >= target ? 2 : 1;
+}
+
+template <typename Args, typename K1, typename K2, typename K3, typename K4>
+static void launch_rows(int rows, K1 k1, K2 k2, K3 k3, K4 k4, const Args& a, hipStream_t s) {
+  const int R = rows_per_wave(rows);
+  const int waves = (rows + R - 1) / R;
+  const dim3 grid((waves + TOK_THREADS / 64 - 1) / (TOK_THREADS / 64));
+  auto k = R == 1 ? k1 : R == 2 ? k2 : R == 3 ? k3 : k4;
+  hipLaunchKernelGGL(k, grid, dim3(TOK_THREADS), 0, s, a);
+}
+
 void prompt_reduce(const PromptArgs& a, hipStream_t s) {
   const int rows = a.B * (a.Lz + a.Lx);
   if (a.layer == 0) {
     const int waves = (rows + PR_ROWS - 1) / PR_ROWS;
     hipLaunchKernelGGL(prompt_reduce_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, a);
   } else {
-    const int blocks = min(PD_BLOCKS, (rows + 3) / 4);   // small batches: one row per wave
-    hipLaunchKernelGGL(prompt_reduce_deep_kernel, dim3(blocks), dim3(256), 0, s, a);
+    launch_rows(rows, prompt_reduce_deep_kernel<1>, prompt_reduce_deep_kernel<2>, prompt_reduce_deep_kernel<3>,
+                prompt_reduce_deep_kernel<4>, a, s);
   }
 }
 
 // ------------------------------------------------------------------ prompt block, part 2
-// Fovea (vit_ce_prompt.py:33-47): per channel, softmax over the part's h*w positions of
-// x*smooth, times x; + conv0_1 branch -> s8 (kept: the next layer folds LN_B + conv0_1 onto it);
-// conv1x1 8 -> 768 (+bias) -> prompt P (full slot layout, each thread holding the conv1x1 rows of its
-// 3 columns across the block's 16 tokens).  The residual update that consumes P is fused into the
-// next LayerNorm (ln_prompt below).
-constexpr int PCHUNK = 16;
+// Fovea (vit_ce_prompt.py:33-47): per channel, softmax over the part's h*w positions of x*smooth,
+// times x; + the conv0_1 branch -> s8 [B][L][8].  One block per (part, sequence) computes the
+// part's per-channel max / sum once and writes s8 for every slot of the part.  The conv1x1
+// 8 -> 768 that turns s8 into the prompt P is fused into the consumer (ln_prompt below), and the
+// next layer folds LN_B + conv0_1 onto s8 (PromptFold), so P is never materialized.
+constexpr int FOVEA_MAX_TOKENS = 1024;
 
-__global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) {
+__global__ __launch_bounds__(256) void fovea_kernel(const PromptArgs a) {
+  __shared__ __attribute__((aligned(16))) float va[FOVEA_MAX_TOKENS * 8];
+  __shared__ __attribute__((aligned(16))) float vc[FOVEA_MAX_TOKENS * 8];
   __shared__ float red[256];
   __shared__ float smax[8], ssum[8];
-  __shared__ float f[PCHUNK][8];
   const int L = a.Lz + a.Lx, b = blockIdx.y, tid = threadIdx.x;
-  const int nbz = (a.Lz + PCHUNK - 1) / PCHUNK;
-  int lo, n, t0;
-  if ((int)blockIdx.x < nbz) {
-    lo = 0; n = a.Lz; t0 = blockIdx.x * PCHUNK;
-  } else {
-    lo = a.Lz; n = a.Lx; t0 = a.Lz + (blockIdx.x - nbz) * PCHUNK;
+  const int lo = blockIdx.x == 0 ? 0 : a.Lz, n = blockIdx.x == 0 ? a.Lz : a.Lx;
+  const float* a8 = a.a8 + ((int64_t)b * L + lo) * 8;
+  const float* c8 = a.c8 + ((int64_t)b * L + lo) * 8;
+  float* s8 = a.s8 + ((int64_t)b * L + lo) * 8;
+  // the part's a8 and c8 into LDS with coalesced 16-byte loads (all issued before the first use)
+  for (int e = tid; e < n * 2; e += 256) {
+    reinterpret_cast<float4*>(va)[e] = reinterpret_cast<const float4*>(a8)[e];
+    reinterpret_cast<float4*>(vc)[e] = reinterpret_cast<const float4*>(c8)[e];
   }
-  const int t1 = min(t0 + PCHUNK, lo + n);
-  const float* a8 = a.a8 + (int64_t)b * L * 8;
-  const float* c8 = a.c8 + (int64_t)b * L * 8;
+  __syncthreads();
   const float sm = a.smooth;
   const int c = tid & 7, stripe = tid >> 3;
   float mx = -INFINITY;
-  for (int t = lo + stripe; t < lo + n; t += 32) mx = fmaxf(mx, a8[t * 8 + c] * sm);
+  for (int t = stripe; t < n; t += 32) mx = fmaxf(mx, va[t * 8 + c] * sm);
   mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -292,7 +376,7 @@ __global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) 
   __syncthreads();
   const float cm = smax[c];
   float sum = 0.f;
-  for (int t = lo + stripe; t < lo + n; t += 32) sum += __expf(a8[t * 8 + c] * sm - cm);
+  for (int t = stripe; t < n; t += 32) sum += __expf(va[t * 8 + c] * sm - cm);
   sum += __shfl_xor(sum, 8, 64);
   sum += __shfl_xor(sum, 16, 64);
   sum += __shfl_xor(sum, 32, 64);
@@ -301,79 +385,144 @@ __global__ __launch_bounds__(256) void prompt_expand_kernel(const PromptArgs a) 
   __syncthreads();
   if (tid < 8) ssum[tid] = (red[tid] + red[8 + tid]) + (red[16 + tid] + red[24 + tid]);
   __syncthreads();
-  if (tid < (t1 - t0) * 8) {
-    const int t = t0 + tid / 8, ch = tid & 7;
-    const float v = a8[t * 8 + ch];
-    const float msk = __expf(v * sm - smax[ch]) / ssum[ch];
-    const float sv = msk * v + c8[t * 8 + ch];
-    f[tid / 8][ch] = sv;
-    a.s8[((int64_t)b * L + t) * 8 + ch] = sv;   // kept for the next layer's folded LN_B + conv0_1
+  // s8 = softmax mask * a8 + c8, four channels per thread, 16-byte loads / stores
+  for (int e = tid; e < n * 2; e += 256) {
+    const int c0 = (e & 1) * 4;
+    const float4 v = reinterpret_cast<const float4*>(va)[e];
+    const float4 cc = reinterpret_cast<const float4*>(vc)[e];
+    float4 o;
+    o.x = (__expf(v.x * sm - smax[c0]) / ssum[c0]) * v.x + cc.x;
+    o.y = (__expf(v.y * sm - smax[c0 + 1]) / ssum[c0 + 1]) * v.y + cc.y;
+    o.z = (__expf(v.z * sm - smax[c0 + 2]) / ssum[c0 + 2]) * v.z + cc.z;
+    o.w = (__expf(v.w * sm - smax[c0 + 3]) / ssum[c0 + 3]) * v.w + cc.w;
+    reinterpret_cast<float4*>(s8)[e] = o;
   }
-  __syncthreads();
-  float w1r[3][8], b1r[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int col = tid + 256 * k;
-    const float4* w4 = reinterpret_cast<const float4*>(a.w1 + col * 8);
-    const float4 p0 = w4[0], p1 = w4[1];
-    w1r[k][0] = p0.x; w1r[k][1] = p0.y; w1r[k][2] = p0.z; w1r[k][3] = p0.w;
-    w1r[k][4] = p1.x; w1r[k][5] = p1.y; w1r[k][6] = p1.z; w1r[k][7] = p1.w;
-    b1r[k] = a.b1[col];
-  }
-  for (int t = t0; t < t1; ++t) {
-    float* prow = a.P + ((int64_t)b * L + t) * C768;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      float v = b1r[k];
-#pragma unroll
-      for (int ch = 0; ch < 8; ++ch) v += w1r[k][ch] * f[t - t0][ch];
-      prow[tid + 256 * k] = v;
-    }
-  }
-}
-
-void prompt_expand(const PromptArgs& a, hipStream_t s) {
-  const int nb = (a.Lz + PCHUNK - 1) / PCHUNK + (a.Lx + PCHUNK - 1) / PCHUNK;
-  hipLaunchKernelGGL(prompt_expand_kernel, dim3(nb, a.B), dim3(256), 0, s, a);
 }
 
 // ------------------------------------------------------------------ LN1 with the prompt residual fused
+// P[slot] = conv1x1(s8[slot]) + b1 (vit_ce_prompt.py:69-71), formed on the fly from the 32 bytes of s8
+// per token and the block's LDS copy of conv1x1 (P is never written to HBM).
 // mode 1 (layer 0):  X[r] = (tok_rgb[r] + P[r]) + pos[t]          (vit_ce_prompt.py:218, 240-241)
 // mode 2 (layer i):  X[r] = X[r] + P[b][slot(t)], slot(t) = t < Lz ? t : gidx[b][t-Lz]
 //                    (candidate_elimination_prompt + x_ori add, attn_blocks.py:9-18, vit_ce_prompt.py:310)
 // then out = LN(X[r]) (norm1 of the block).
-__global__ __launch_bounds__(256) void ln_prompt_kernel(const LnPromptArgs a) {
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (r >= a.rows) return;
+struct LnpIn {
+  Row12 x, q;      // mode 2: x = X row; mode 1: x = tok_rgb row, q = pos row
+  float4 s0, s1;   // s8 of the row's slot
+};
+
+template <int MODE>
+__device__ __forceinline__ int lnp_slot(const LnPromptArgs& a, int r) {
+  const int b = r / a.rows_per_seq, t = r - b * a.rows_per_seq;
+  if (MODE == 1 || t < a.Lz) return t;
+  return a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (t - a.Lz)];
+}
+
+template <int MODE>
+__device__ __forceinline__ LnpIn lnp_fetch(const LnPromptArgs& a, int r, int slot, int lane) {
   const int b = r / a.rows_per_seq, t = r - b * a.rows_per_seq;
   const int L = a.Lz + a.Lx;
-  Row12 x;
-  if (a.mode == 1) {
-    const Row12 tk = load_row(a.tok_rgb + (int64_t)r * C768, lane);
-    const Row12 pp = load_row(a.P + (int64_t)r * C768, lane);
-    const Row12 ps = load_row(a.pos + (int64_t)t * C768, lane);
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-      x.v[i] = make_float4((tk.v[i].x + pp.v[i].x) + ps.v[i].x, (tk.v[i].y + pp.v[i].y) + ps.v[i].y,
-                           (tk.v[i].z + pp.v[i].z) + ps.v[i].z, (tk.v[i].w + pp.v[i].w) + ps.v[i].w);
+  LnpIn d;
+  if (MODE == 1) {
+    d.x = load_row(a.tok_rgb + (int64_t)r * C768, lane);
+    d.q = load_row(a.pos + (int64_t)t * C768, lane);
   } else {
-    const int slot = t < a.Lz ? t : a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (t - a.Lz)];
-    const Row12 xo = load_row(a.X + (int64_t)r * C768, lane);
-    const Row12 pp = load_row(a.P + ((int64_t)b * L + slot) * C768, lane);
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-      x.v[i] = make_float4(xo.v[i].x + pp.v[i].x, xo.v[i].y + pp.v[i].y, xo.v[i].z + pp.v[i].z,
-                           xo.v[i].w + pp.v[i].w);
+    d.x = load_row(a.X + (int64_t)r * C768, lane);
   }
-  store_f32(a.X + (int64_t)r * C768, x, lane);
-  const Row12 y = ln_row(x, a.w, a.b, lane);
-  store_bf16(a.out + (int64_t)r * C768, y, lane);
-  if (a.out_lo) store_bf16_lo(a.out_lo + (int64_t)r * C768, y, lane);
+  const float4* sp = reinterpret_cast<const float4*>(a.s8 + ((int64_t)b * L + slot) * 8);
+  d.s0 = sp[0];
+  d.s1 = sp[1];
+  return d;
+}
+
+// Each wave owns R rows; slots, rows and weights are all requested before the barrier (see
+// prompt_reduce_deep_kernel).  conv1x1 is transposed into LDS, W1t[ch][col], so a lane's float4
+// of columns 4 * (lane + 64 i) for channel ch is one conflict-free ds_read_b128.
+template <int MODE, int R>
+__global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptArgs a) {
+  __shared__ __attribute__((aligned(16))) float W1t[8 * C768];
+  __shared__ __attribute__((aligned(16))) float cst[3 * C768];   // conv1x1 bias, norm1 weight, norm1 bias
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (TOK_THREADS / 64);
+  const int r0 = blockIdx.x * (TOK_THREADS / 64) + (threadIdx.x >> 6);
+  const int pr = r0 + lane * nw;
+  const int slotv = (lane < R && pr < a.rows) ? lnp_slot<MODE>(a, pr) : 0;
+  constexpr int WE = 8 * C768 / TOK_THREADS;   // 12 conv1x1 elements per thread
+  float wst[WE];
+#pragma unroll
+  for (int k = 0; k < WE; ++k) wst[k] = a.w1[threadIdx.x + TOK_THREADS * k];
+  float cs[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int e = threadIdx.x + TOK_THREADS * k;
+    cs[k] = e < C768 ? a.b1[e] : e < 2 * C768 ? a.w[e - C768] : e < 3 * C768 ? a.b[e - 2 * C768] : 0.f;
+  }
+  LnpIn in[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int rj = min(r0 + j * nw, a.rows - 1);
+    in[j] = lnp_fetch<MODE>(a, rj, __shfl(slotv, j, 64), lane);
+  }
+#pragma unroll
+  for (int k = 0; k < WE; ++k) {
+    const int e = threadIdx.x + TOK_THREADS * k;
+    W1t[(e & 7) * C768 + (e >> 3)] = wst[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int e = threadIdx.x + TOK_THREADS * k;
+    if (e < 3 * C768) cst[e] = cs[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int r = r0 + j * nw;
+    if (r >= a.rows) break;
+    const float f[8] = {in[j].s0.x, in[j].s0.y, in[j].s0.z, in[j].s0.w, in[j].s1.x, in[j].s1.y, in[j].s1.z, in[j].s1.w};
+    Row12 x;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float4 b1 = reinterpret_cast<const float4*>(cst)[lane + 64 * i];
+      float pv[4] = {b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int ch = 0; ch < 8; ++ch) {
+        const float4 wv = reinterpret_cast<const float4*>(W1t + ch * C768)[lane + 64 * i];
+        pv[0] += wv.x * f[ch];
+        pv[1] += wv.y * f[ch];
+        pv[2] += wv.z * f[ch];
+        pv[3] += wv.w * f[ch];
+      }
+      const float4 xv = in[j].x.v[i];
+      if (MODE == 1) {
+        const float4 ps = in[j].q.v[i];
+        x.v[i] = make_float4((xv.x + pv[0]) + ps.x, (xv.y + pv[1]) + ps.y, (xv.z + pv[2]) + ps.z,
+                             (xv.w + pv[3]) + ps.w);
+      } else {
+        x.v[i] = make_float4(xv.x + pv[0], xv.y + pv[1], xv.z + pv[2], xv.w + pv[3]);
+      }
+    }
+    store_f32(a.X + (int64_t)r * C768, x, lane);
+    Row12 y = ln_hat(x);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float4 gw = reinterpret_cast<const float4*>(cst + C768)[lane + 64 * i];
+      const float4 gb = reinterpret_cast<const float4*>(cst + 2 * C768)[lane + 64 * i];
+      y.v[i] = make_float4(y.v[i].x * gw.x + gb.x, y.v[i].y * gw.y + gb.y, y.v[i].z * gw.z + gb.z,
+                           y.v[i].w * gw.w + gb.w);
+    }
+    store_bf16(a.out + (int64_t)r * C768, y, lane);
+    if (a.out_lo) store_bf16_lo(a.out_lo + (int64_t)r * C768, y, lane);
+  }
 }
 
 void prompt_expand_ln(const PromptArgs& pa, const LnPromptArgs& a, hipStream_t s) {
-  prompt_expand(pa, s);
-  hipLaunchKernelGGL(ln_prompt_kernel, dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(fovea_kernel, dim3(2, pa.B), dim3(256), 0, s, pa);
+  if (a.mode == 1)
+    launch_rows(a.rows, ln_prompt_kernel<1, 1>, ln_prompt_kernel<1, 2>, ln_prompt_kernel<1, 3>,
+                ln_prompt_kernel<1, 4>, a, s);
+  else
+    launch_rows(a.rows, ln_prompt_kernel<2, 1>, ln_prompt_kernel<2, 2>, ln_prompt_kernel<2, 3>,
+                ln_prompt_kernel<2, 4>, a, s);
 }
 
 // ------------------------------------------------------------------ candidate elimination
