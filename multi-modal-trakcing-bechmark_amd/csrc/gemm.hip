@@ -115,8 +115,7 @@ __device__ __forceinline__ void store4(const GemmGroup& g, const GemmArgs& args,
 constexpr bool epi_is_bf16(int e) { return e == EPI_BF16 || e == EPI_GELU_BF16 || e == EPI_RELU_BF16; }
 
 template <int EPI>
-__device__ __forceinline__ void epi_values(const GemmGroup& g, int n, const f32x4& a, float* v) {
-  const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+__device__ __forceinline__ void epi_values(const float4& bv, const f32x4& a, float* v) {
   v[0] = a[0] + bv.x;
   v[1] = a[1] + bv.y;
   v[2] = a[2] + bv.z;
@@ -148,10 +147,24 @@ struct LdsTile {
       *reinterpret_cast<float4*>(lds + off(row, col)) = make_float4(v[0], v[1], v[2], v[3]);
     }
   }
-  // rows [0, ROWS) of the LDS tile -> C rows m_base + r (< M), columns n0 ..
-  template <int ROWS, int NT>
-  __device__ static void drain(const char* lds, const GemmGroup& g, const GemmArgs& args, int m_base, int n0, int M) {
-    for (int idx = threadIdx.x; idx < ROWS * NCH; idx += NT) {
+  static constexpr bool HAS_R = EPI == EPI_RESID_F32 || EPI == EPI_POS_F32;
+  // the residual chunk this thread's drain iteration k adds (issued early: see gemm_kernel)
+  __device__ static float4 r_chunk(const GemmGroup& g, const GemmArgs& args, int idx, int m_base, int n0, int M) {
+    const int r = idx / NCH, c = idx - r * NCH;
+    const int m = m_base + r;
+    if (m >= M) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t rr = EPI == EPI_POS_F32 ? (int64_t)(m % args.pos_rows) : (int64_t)m;
+    return *reinterpret_cast<const float4*>(g.R + rr * g.ldr + n0 + c * CH);
+  }
+  // rows [0, ROWS) of the LDS tile -> C rows m_base + r (< M), columns n0 ..; RPRE: the residual
+  // chunks were prefetched into rpre[k] (k-th iteration of this thread)
+  template <int ROWS, int NT, int RPRE = 0>
+  __device__ static void drain(const char* lds, const GemmGroup& g, const GemmArgs& args, int m_base, int n0, int M,
+                               const float4* rpre = nullptr) {
+#pragma unroll
+    for (int k = 0; k < (ROWS * NCH + NT - 1) / NT; ++k) {
+      const int idx = threadIdx.x + k * NT;
+      if (idx >= ROWS * NCH) break;
       const int r = idx / NCH, c = idx - r * NCH;
       const int m = m_base + r;
       if (m >= M) continue;
@@ -161,9 +174,8 @@ struct LdsTile {
         *reinterpret_cast<uint4*>(static_cast<bf16_t*>(g.C) + (int64_t)m * g.ldc + n) = d;
       } else {
         float4 o = make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
-        if (EPI == EPI_RESID_F32 || EPI == EPI_POS_F32) {
-          const int64_t rr = EPI == EPI_POS_F32 ? (int64_t)(m % args.pos_rows) : (int64_t)m;
-          const float4 R = *reinterpret_cast<const float4*>(g.R + rr * g.ldr + n);
+        if constexpr (HAS_R) {
+          const float4 R = RPRE ? rpre[k] : r_chunk(g, args, idx, m_base, n0, M);
           o = make_float4(R.x + o.x, R.y + o.y, R.z + o.z, R.w + o.w);
         }
         *reinterpret_cast<float4*>(static_cast<float*>(g.C) + (int64_t)m * g.ldc + n) = o;
@@ -190,6 +202,23 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   GEMM_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WNW, wn = wave % WNW;
+
+  // ---- epilogue operands requested now, so their latency hides under the main loop: the bias of
+  // the lane's columns and (residual epilogues) the residual chunks of the drain
+  using LT = LdsTile<EPI, BN>;
+  constexpr bool LDS_EPI = EPI != EPI_PARTIAL && !SPLIT && BM * BN * LT::ESZ <= T::NSTAGE * T::STAGE * 2;
+  constexpr int RPRE = (LDS_EPI && LT::HAS_R && (BM * LT::NCH) % T::NT == 0) ? BM * LT::NCH / T::NT : 0;
+  float4 bpre[T::FN];
+#pragma unroll
+  for (int jj = 0; jj < T::FN; ++jj) {
+    const int col = n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4;
+    bpre[jj] = (LDS_EPI && g.bias) ? *reinterpret_cast<const float4*>(g.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float4 rpre[RPRE > 0 ? RPRE : 1];
+  if constexpr (RPRE > 0) {
+#pragma unroll
+    for (int k = 0; k < RPRE; ++k) rpre[k] = LT::r_chunk(g, args, tid + k * T::NT, m0, n0, M);
+  }
 
   // ---- loads: buffer_load ... lds with per-lane VGPR offsets fixed over K and the K advance in the
   // SGPR soffset; rows past M fall outside the A resource and read as zero.  Row block i of the
@@ -335,7 +364,6 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
 
   GEMM_STAMP(2);
   // ---- epilogue: lane owns C[m][n..n+3]
-  using LT = LdsTile<EPI, BN>;
   if constexpr (EPI == EPI_PARTIAL) {   // raw partial sums -> workspace slice (blockIdx.z, blockIdx.y)
     GemmGroup gp{};
     gp.C = args.ws + ((int64_t)blockIdx.z * args.ksplit + blockIdx.y) * (int64_t)M * args.N;
@@ -351,7 +379,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
       }
     __syncthreads();
     LT::template drain<BM, T::NT>(lds, gp, args, m0, n0, M);
-  } else if constexpr (!SPLIT && BM * BN * LT::ESZ <= T::NSTAGE * T::STAGE * 2) {
+  } else if constexpr (LDS_EPI) {
     char* lds = reinterpret_cast<char*>(smem);
 #pragma unroll
     for (int i = 0; i < T::FM; ++i)
@@ -359,11 +387,11 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
       for (int jj = 0; jj < T::FN; ++jj) {
         const int col = wn * T::WN + jj * 16 + (lane >> 4) * 4;
         float v[4];
-        epi_values<EPI>(g, n0 + col, acc[i][jj], v);
+        epi_values<EPI>(bpre[jj], acc[i][jj], v);
         LT::put(lds, wm * T::WM + i * 16 + (lane & 15), col, v);
       }
     __syncthreads();
-    LT::template drain<BM, T::NT>(lds, g, args, m0, n0, M);
+    LT::template drain<BM, T::NT, RPRE>(lds, g, args, m0, n0, M, rpre);
   } else {
 #pragma unroll
     for (int i = 0; i < T::FM; ++i) {
@@ -403,6 +431,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const GemmArgs args) {
   const int m0 = tm * 256, n0 = tn * 256;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  float4 bpre[2][2];   // bias of the lane's epilogue columns, requested before the main loop
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+      bpre[qb][jj] = g.bias ? *reinterpret_cast<const float4*>(g.bias + n0 + qb * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
   GEMM_STAMP(0);
 
   const int chunk = ((lane & 7) ^ (lane >> 3)) * 16;
@@ -554,7 +589,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const GemmArgs args) {
           const int col = QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4;
           const int row = (HALVES == 2 ? 0 : QA[qd] * 128) + wr * 64 + i * 16 + (lane & 15);
           float v[4];
-          epi_values<EPI>(g, n0 + col, acc[qd][i][jj], v);
+          epi_values<EPI>(bpre[QB[qd]][jj], acc[qd][i][jj], v);
           LT::put(lds, row, col, v);
         }
     }
