@@ -406,6 +406,168 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Persistent variant for the bf16-output GEMMs of the path (qkv, fc1): a grid of two workgroups per
+// CU walks the output tiles, and the first K-tile of a workgroup's NEXT output tile is loaded while
+// the current one is finishing (issued at the last K-step into the free LDS stage), so the load
+// latency that opens every tile of gemm_kernel (its "prologue") hides under the previous tile's last
+// MFMAs and epilogue.  The epilogue stages C through the LDS stage just consumed; a tile's bias is
+// requested with its second K-tile.  Dense A only (no conv gather), no split mode.
+template <int BM, int BN, int WMW, int WNW, int EPI>
+__global__ __launch_bounds__(WMW* WNW * 64) void gemm_persist_kernel(const GemmArgs args) {
+  using T = Tile<BM, BN, WMW, WNW, false, 2>;
+  using LT = LdsTile<EPI, BN>;
+  static_assert(LT::ESZ == 2 && BM * BN * 2 <= T::STAGE * 2, "C tile must fit one LDS stage");
+  static_assert((BM * LT::NCH) % T::NT == 0, "drain iterations must be uniform");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * T::STAGE];
+  const GemmGroup& g = args.g[0];
+  const int M = args.M, K = args.K;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = args.N / BN, ntiles = tiles_m * tiles_n;
+  // XCD-aware: the workgroups of XCD x (= b % 8) share the contiguous logical range
+  // [x * per, (x + 1) * per) of the super-tile order and take its tiles round-robin
+  const int b = blockIdx.x, x = b & 7, j = b >> 3, nb8 = gridDim.x >> 3;
+  const int per = (ntiles + 7) >> 3;
+  const int lo = x * per, hi = min(ntiles, lo + per);
+  int id = lo + j;
+  if (id >= hi) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+
+  constexpr int GPW = T::GROUPS / T::NW;
+  constexpr int RPI = T::NW * 8;
+  constexpr int NST = BM * LT::NCH / T::NT;   // global stores per thread in a full tile's drain
+  const int chunk = ((lane & 7) ^ (lane >> 3)) * 16;
+  uint32_t voff[GPW];
+#pragma unroll
+  for (int i = 0; i < GPW; ++i) {
+    const int r0 = i * RPI;
+    const int row = r0 + wave * 8 + (lane >> 3);
+    voff[i] = r0 < BM ? (uint32_t)(row * g.lda * 2 + chunk) : (uint32_t)((row - BM) * g.ldw * 2 + chunk);
+  }
+  const int nk = K / 64;
+
+  // tile geometry and buffer resources (plain locals: the rsrc type cannot live in a struct on the host
+  // side of the compile, and the builtin's operands are copied to locals, see gemm_kernel)
+  auto tile_geom = [&](int tid_, int& m0, int& n0) {
+    int tm, tn;
+    tile_of(tid_, tiles_m, tiles_n, args.gm, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  auto issue = [&](int m0, int n0, int kt, int stage) {
+    const rsrc_t rA = make_rsrc(g.A + (int64_t)m0 * g.lda, (int64_t)(M - m0) * g.lda * 2);
+    const rsrc_t rW = make_rsrc(g.W + (int64_t)n0 * g.ldw, (int64_t)BN * g.ldw * 2);
+    bf16_t* sbase = smem + stage * T::STAGE;
+#pragma unroll
+    for (int i = 0; i < GPW; ++i) {
+      const int r0 = i * RPI;
+      lptr_t dst = (lptr_t)(sbase + (r0 + wave * 8) * 64);
+      const uint32_t vo = voff[i];
+      const int so = kt * 128;
+      if (r0 < BM) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, vo, so, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, dst, 16, vo, so, 0, 0);
+    }
+  };
+  auto load_bias = [&](int n0, float4* bp) {
+#pragma unroll
+    for (int jj = 0; jj < T::FN; ++jj) {
+      const int col = n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4;
+      bp[jj] = g.bias ? *reinterpret_cast<const float4*>(g.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+
+  f32x4 acc[T::FM][T::FN];
+  auto compute = [&](int stage) {
+    const bf16_t* S = smem + stage * T::STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 4 * s + (lane >> 4);
+      bf16x8 ah[T::FM], bh[T::FN];
+#pragma unroll
+      for (int i = 0; i < T::FM; ++i) ah[i] = *reinterpret_cast<const bf16x8*>(S + swz(wm * T::WM + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj)
+        bh[jj] = *reinterpret_cast<const bf16x8*>(S + swz(BM + wn * T::WN + jj * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < T::FN; ++jj)
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[jj], ah[i], acc[i][jj], 0, 0, 0);
+    }
+  };
+
+  int cm0, cn0;
+  tile_geom(id, cm0, cn0);
+  float4 bcur[T::FN];
+  issue(cm0, cn0, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int stage = 0;
+  for (;;) {
+    const int nid = id + nb8;
+    const bool has_next = nid < hi;
+    int nm0 = cm0, nn0 = cn0;
+    load_bias(cn0, bcur);   // lands with the K-tile loads of the first step; used in the epilogue
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool last = kt + 1 == nk;
+      if (!last) {
+        issue(cm0, cn0, kt + 1, stage ^ 1);
+      } else if (has_next) {   // the next tile's first K-tile, into the stage freed by K-tile kt-1
+        tile_geom(nid, nm0, nn0);
+        issue(nm0, nn0, 0, stage ^ 1);
+      }
+      compute(stage);
+      if (!last) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stage ^= 1;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    // epilogue through the stage just consumed (every wave passed the barrier after reading it)
+    char* lds = reinterpret_cast<char*>(smem + stage * T::STAGE);
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj) {
+        const int col = wn * T::WN + jj * 16 + (lane >> 4) * 4;
+        float v[4];
+        epi_values<EPI>(bcur[jj], acc[i][jj], v);
+        LT::put(lds, wm * T::WM + i * 16 + (lane & 15), col, v);
+      }
+    // LDS visibility of the C tile without __syncthreads(): its fence would also wait (vmcnt(0)) for
+    // the next tile's K-tile in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    LT::template drain<BM, T::NT>(lds, g, args, cm0, cn0, M);
+    if (!has_next) break;
+    // every wave has read its C rows out of LDS before the next tile's loads land in this stage;
+    // the next tile's first K-tile (issued before the drain's stores) must have landed: with a full
+    // tile exactly NST stores per thread follow it in the in-order vmcnt queue (M-tail tiles: all)
+    if (cm0 + BM <= M) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stage ^= 1;
+    cm0 = nm0;
+    cn0 = nn0;
+    id = nid;
+  }
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+// ---------------------------------------------------------------------------------------------------
 // 256 x 256 tile, 8 waves (2 x 4), four phases per 64-deep K-tile (one 128 x 128 C quadrant per
 // phase; each wave owns a 64 x 32 piece of every quadrant).
 //
@@ -629,6 +791,16 @@ static void launch_one(const GemmArgs& a0, hipStream_t s) {
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI, AM, SPLIT, ST>), grid, dim3(WMW * WNW * 64), 0, s, a);
 }
 
+template <int EPI>
+static void launch_persist(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  const int tiles_m = (a.M + 127) / 128, ntiles = tiles_m * (a.N / 128);
+  a.gm = tiles_m < 8 ? tiles_m : 8;
+  static const int slots = 2 * num_cus();   // two 64-KB-LDS workgroups per CU
+  const int grid = (ntiles < slots ? ntiles : slots) & ~7;
+  hipLaunchKernelGGL((gemm_persist_kernel<128, 128, 4, 2, EPI>), dim3(grid), dim3(512), 0, s, a);
+}
+
 template <int BM, int BN, int WMW, int WNW, bool SPLIT, int ST = 2>
 static void launch_cfg(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.amode == A_CONV3) {
@@ -697,6 +869,10 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         case 7: return launch_cfg<128, 256, 2, 4, false, 2>(a, epi, s);
         case 8: return launch_cfg<64, 128, 2, 2, false, 2>(a, epi, s);
         case 9: if (a.N % 256 == 0) return launch256_epi(a, epi, s); break;
+        case 10:
+          if (a.N % 128 == 0 && a.groups == 1 && (epi == EPI_BF16 || epi == EPI_GELU_BF16))
+            return epi == EPI_BF16 ? launch_persist<EPI_BF16>(a, s) : launch_persist<EPI_GELU_BF16>(a, s);
+          break;
         default: break;
       }
     }
@@ -706,6 +882,14 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
   // overlaps the other's MFMAs) beat 256x128 / 256x256 / 3-deep rings on every K=768/3072 GEMM.
   const int target = 200;   // aim for at least ~one tile per CU of the 256
   const int t128 = (a.M + 127) / 128, t64 = (a.M + 63) / 64;
+  // bf16-output GEMMs with several 128 x 128 tiles per workgroup slot: the persistent kernel (the next
+  // tile's first K-tile loads under the current tile's tail)
+  static const int persist_min = getenv("MMT_PERSIST_MIN") ? atoi(getenv("MMT_PERSIST_MIN")) : 1;
+  if (!SPLIT && persist_min > 0 && a.amode == A_DENSE && a.groups == 1 && a.N % 128 == 0 &&
+      t128 * (a.N / 128) >= persist_min * 2 * num_cus()) {
+    if (epi == EPI_BF16) return launch_persist<EPI_BF16>(a, s);
+    if (epi == EPI_GELU_BF16) return launch_persist<EPI_GELU_BF16>(a, s);
+  }
   if (a.N % 128 == 0 && t128 * (a.N / 128) * a.groups >= target) return launch_cfg<128, 128, 4, 2, SPLIT>(a, epi, s);
   if (a.N % 64 == 0) {
     if (t128 * (a.N / 64) * a.groups >= target) return launch_cfg<128, 64, 2, 2, SPLIT>(a, epi, s);

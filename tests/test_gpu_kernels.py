@@ -83,6 +83,28 @@ def test_gemm256_forced(lib, M, N, K, epi):
         lib.mmt_gemm_force_config(-1)
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(10240, 3072, 768, 1), (10240, 2304, 768, 0), (7808, 2304, 768, 0),
+                                       (4899, 3072, 768, 1), (70000, 256, 64, 0), (9000, 384, 128, 1)])
+def test_gemm_persistent_forced(lib, M, N, K, epi):
+    """The persistent bf16-output kernel (forced): several tiles per workgroup, the next tile's first
+    K-tile in flight across the epilogue, M tails (full/partial tiles mixed), K = 64 / 128."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 7 * epi)
+    A = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    ref = A.float() @ W.float().t() + bias
+    C0 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    _gemm(lib, A, W, bias, C0, epi=epi)   # default dispatch: the non-persistent kernels
+    lib.mmt_gemm_force_config(10)
+    try:
+        C = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        _gemm(lib, A, W, bias, C, epi=epi)
+    finally:
+        lib.mmt_gemm_force_config(-1)
+    torch.testing.assert_close(C.float(), F.gelu(ref) if epi == 1 else ref, rtol=1e-2, atol=1e-2)
+    assert torch.equal(C, C0)   # same K order per output: bit-identical to the per-tile kernels
+
+
 def test_gemm_pos_epilogue(lib):
     g = torch.Generator(device="cuda").manual_seed(5)
     M, N, K, L = 2 * 720, 768, 768, 720
