@@ -80,7 +80,8 @@ def pmc_traffic(probe, path=None):
     ks = json.load(open(files[-1]))["kernels"]
     best = None
     for name, d in ks.items():
-        m = re.match(r"gemm_kernel<\d+, \d+, \d+, \d+, (\d+), 0, false", name) or re.match(r"gemm256_kernel<(\d+)>", name)
+        m = (re.match(r"gemm_kernel<\d+, \d+, \d+, \d+, (\d+), 0, false", name) or re.match(r"gemm256_kernel<(\d+)>", name)
+             or re.match(r"gemm_persist_kernel<\d+, \d+, \d+, \d+, (\d+)>", name))
         if m and int(m.group(1)) == epi and "traffic_bytes_per_dispatch" in d:
             if best is None or d["dispatches"] > best[1]["dispatches"]:
                 best = (name, d)

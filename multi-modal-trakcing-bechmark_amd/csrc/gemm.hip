@@ -25,10 +25,18 @@
 namespace mmt {
 
 __device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((c ^ (r & 7)) << 3); }
+// K-tile depth BK = 64: rows of 128 B, 16-B chunk c of row r at c ^ (r & 7).  BK = 32: rows of 64 B
+// (four rows per 256-B bank sweep), chunk c at c ^ ((r >> 2) & 2) -- conflict-free for the
+// ds_read_b128 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... of the fragment reads
+template <int BK>
+__device__ __forceinline__ int swzk(int r, int c) {
+  if constexpr (BK == 64) return swz(r, c);
+  else return r * 32 + ((c ^ ((r >> 2) & 2)) << 3);
+}
 
 typedef __attribute__((address_space(3))) void* lptr_t;
 
-template <int BM, int BN, int WMW, int WNW, bool SPLIT, int STAGES = 0>
+template <int BM, int BN, int WMW, int WNW, bool SPLIT, int STAGES = 0, int BK = 64>
 struct Tile {
   static constexpr int NW = WMW * WNW;
   static constexpr int NT = NW * 64;
@@ -36,8 +44,9 @@ struct Tile {
   static constexpr int FM = WM / 16, FN = WN / 16;
   static constexpr int AROWS = SPLIT ? 2 * BM : BM;
   static constexpr int ROWS = AROWS + (SPLIT ? 2 * BN : BN);
-  static constexpr int GROUPS = ROWS / 8;           // 8 rows per wave-instruction
-  static constexpr int STAGE = ROWS * 64;           // bf16 elements per stage
+  static constexpr int RPW = 512 / BK;              // rows per 1-KB wave-instruction (8 or 16)
+  static constexpr int GROUPS = ROWS / RPW;
+  static constexpr int STAGE = ROWS * BK;           // bf16 elements per stage
   static constexpr int NSTAGE = STAGES ? STAGES : 2;   // LDS ring depth
   static_assert(GROUPS % NW == 0, "row groups must divide over waves");
 };
@@ -184,9 +193,10 @@ struct LdsTile {
   }
 };
 
-template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int STAGES>
+template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int STAGES, int BK = 64>
 __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args) {
-  using T = Tile<BM, BN, WMW, WNW, SPLIT, STAGES>;
+  static_assert(BK == 64 || (BK == 32 && AM == A_DENSE), "BK 32: dense A only");
+  using T = Tile<BM, BN, WMW, WNW, SPLIT, STAGES, BK>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[T::NSTAGE * T::STAGE];
 
   const GemmGroup& g = args.g[blockIdx.z];
@@ -224,9 +234,10 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   // SGPR soffset; rows past M fall outside the A resource and read as zero.  Row block i of the
   // tile (rows [i*RPI, (i+1)*RPI)) lies in one operand region, known at compile time.
   constexpr int GPW = T::GROUPS / T::NW;
-  constexpr int RPI = T::NW * 8;
+  constexpr int RPI = T::NW * T::RPW;
   static_assert(BM % RPI == 0 && BN % RPI == 0, "row blocks must not straddle operands");
-  const int chunk = ((lane & 7) ^ (lane >> 3)) * 16;   // XOR swizzle of the 16-B chunk (row & 7 == lane >> 3)
+  // XOR swizzle of the 16-B source chunk so it lands at its swizzled LDS position (swzk)
+  const int chunk = (BK == 64 ? ((lane & 7) ^ (lane >> 3)) : ((lane & 3) ^ ((lane >> 4) & 2))) * 16;
   const int64_t a_rows = AM == A_DENSE ? (int64_t)(M - m0) : (int64_t)M;
   const rsrc_t rA = make_rsrc(AM == A_DENSE ? g.A + (int64_t)m0 * g.lda : g.A, a_rows * g.lda * 2);
   const rsrc_t rAl = SPLIT ? make_rsrc(AM == A_DENSE ? g.A_lo + (int64_t)m0 * g.lda : g.A_lo, a_rows * g.lda * 2) : rA;
@@ -237,7 +248,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
 #pragma unroll
   for (int i = 0; i < GPW; ++i) {
     const int r0 = i * RPI;                              // compile-time after unrolling
-    const int row = r0 + wave * 8 + (lane >> 3);
+    const int row = r0 + wave * T::RPW + lane / (BK / 8);
     conv_b[i] = -1;
     conv_y[i] = conv_x[i] = 0;
     if (r0 < T::AROWS) {
@@ -261,7 +272,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   }
 
   auto issue = [&](int kt, int stage) {
-    const int k0 = kt * 64;
+    const int k0 = kt * BK;
     bf16_t* sbase = smem + stage * T::STAGE;
     int tap = 0, ch = 0, dy = 0, dx = 0;
     if (AM == A_CONV3) {
@@ -273,7 +284,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
 #pragma unroll
     for (int i = 0; i < GPW; ++i) {
       const int r0 = i * RPI;
-      lptr_t dst = (lptr_t)(sbase + (r0 + wave * 8) * 64);
+      lptr_t dst = (lptr_t)(sbase + (r0 + wave * T::RPW) * BK);
       if (r0 < T::AROWS) {
         const rsrc_t rs = (SPLIT && r0 >= BM) ? rAl : rA;
         if (AM == A_CONV3) {
@@ -304,21 +315,21 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   auto compute = [&](int stage) {
     const bf16_t* S = smem + stage * T::STAGE;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BK / 32; ++s) {
       const int c = 4 * s + (lane >> 4);
       bf16x8 ah[T::FM], bh[T::FN];
       bf16x8 al[SPLIT ? T::FM : 1], bl[SPLIT ? T::FN : 1];
 #pragma unroll
       for (int i = 0; i < T::FM; ++i) {
         const int row = wm * T::WM + i * 16 + (lane & 15);
-        ah[i] = *reinterpret_cast<const bf16x8*>(S + swz(row, c));
-        if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(S + swz(BM + row, c));
+        ah[i] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(row, c));
+        if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(BM + row, c));
       }
 #pragma unroll
       for (int jj = 0; jj < T::FN; ++jj) {
         const int row = T::AROWS + wn * T::WN + jj * 16 + (lane & 15);
-        bh[jj] = *reinterpret_cast<const bf16x8*>(S + swz(row, c));
-        if (SPLIT) bl[jj] = *reinterpret_cast<const bf16x8*>(S + swz(BN + row, c));
+        bh[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(row, c));
+        if (SPLIT) bl[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(BN + row, c));
       }
 #pragma unroll
       for (int i = 0; i < T::FM; ++i)
@@ -337,7 +348,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   // is multiplied.  A tile is read only after the issuing waves' counted vmcnt retired it AND a
   // barrier (raw s_barrier: __syncthreads() would drain every in-flight LDS-DMA with vmcnt(0)).
   // Split-K (EPI_PARTIAL): workgroup row blockIdx.y takes K-tiles [kbeg, kend) and stores raw sums.
-  const int nk_all = K / 64;
+  const int nk_all = K / BK;
   const int kbeg = EPI == EPI_PARTIAL ? (int)((int64_t)blockIdx.y * nk_all / args.ksplit) : 0;
   const int kend = EPI == EPI_PARTIAL ? (int)((int64_t)(blockIdx.y + 1) * nk_all / args.ksplit) : nk_all;
   const int nk = kend - kbeg;
@@ -781,14 +792,14 @@ static void launch256_epi(const GemmArgs& a, int epi, hipStream_t s) {
   }
 }
 
-template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int ST>
+template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int ST, int BK = 64>
 static void launch_one(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.N / BN;
   (void)tiles_n;
   a.gm = tiles_m < 8 ? tiles_m : 8;
   dim3 grid(tiles_m * tiles_n, 1, a.groups);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI, AM, SPLIT, ST>), grid, dim3(WMW * WNW * 64), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI, AM, SPLIT, ST, BK>), grid, dim3(WMW * WNW * 64), 0, s, a);
 }
 
 template <int EPI>
@@ -801,7 +812,7 @@ static void launch_persist(const GemmArgs& a0, hipStream_t s) {
   hipLaunchKernelGGL((gemm_persist_kernel<128, 128, 4, 2, EPI>), dim3(grid), dim3(512), 0, s, a);
 }
 
-template <int BM, int BN, int WMW, int WNW, bool SPLIT, int ST = 2>
+template <int BM, int BN, int WMW, int WNW, bool SPLIT, int ST = 2, int BK = 64>
 static void launch_cfg(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.amode == A_CONV3) {
     if (epi == EPI_RELU_BF16) return launch_one<BM, BN, WMW, WNW, EPI_RELU_BF16, A_CONV3, SPLIT, ST>(a, s);
@@ -809,11 +820,11 @@ static void launch_cfg(const GemmArgs& a, int epi, hipStream_t s) {
     return;
   }
   switch (epi) {
-    case EPI_BF16: return launch_one<BM, BN, WMW, WNW, EPI_BF16, A_DENSE, SPLIT, ST>(a, s);
-    case EPI_GELU_BF16: return launch_one<BM, BN, WMW, WNW, EPI_GELU_BF16, A_DENSE, SPLIT, ST>(a, s);
-    case EPI_RESID_F32: return launch_one<BM, BN, WMW, WNW, EPI_RESID_F32, A_DENSE, SPLIT, ST>(a, s);
-    case EPI_F32: return launch_one<BM, BN, WMW, WNW, EPI_F32, A_DENSE, SPLIT, ST>(a, s);
-    case EPI_POS_F32: return launch_one<BM, BN, WMW, WNW, EPI_POS_F32, A_DENSE, SPLIT, ST>(a, s);
+    case EPI_BF16: return launch_one<BM, BN, WMW, WNW, EPI_BF16, A_DENSE, SPLIT, ST, BK>(a, s);
+    case EPI_GELU_BF16: return launch_one<BM, BN, WMW, WNW, EPI_GELU_BF16, A_DENSE, SPLIT, ST, BK>(a, s);
+    case EPI_RESID_F32: return launch_one<BM, BN, WMW, WNW, EPI_RESID_F32, A_DENSE, SPLIT, ST, BK>(a, s);
+    case EPI_F32: return launch_one<BM, BN, WMW, WNW, EPI_F32, A_DENSE, SPLIT, ST, BK>(a, s);
+    case EPI_POS_F32: return launch_one<BM, BN, WMW, WNW, EPI_POS_F32, A_DENSE, SPLIT, ST, BK>(a, s);
     default: break;
   }
 }
@@ -869,6 +880,9 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         case 7: return launch_cfg<128, 256, 2, 4, false, 2>(a, epi, s);
         case 8: return launch_cfg<64, 128, 2, 2, false, 2>(a, epi, s);
         case 9: if (a.N % 256 == 0) return launch256_epi(a, epi, s); break;
+        case 11: return launch_cfg<128, 128, 4, 2, false, 4, 32>(a, epi, s);
+        case 12: return launch_cfg<128, 128, 4, 2, false, 3, 32>(a, epi, s);
+        case 13: return launch_cfg<128, 64, 2, 2, false, 4, 32>(a, epi, s);
         case 10:
           if (a.N % 128 == 0 && a.groups == 1 && (epi == EPI_BF16 || epi == EPI_GELU_BF16))
             return epi == EPI_BF16 ? launch_persist<EPI_BF16>(a, s) : launch_persist<EPI_GELU_BF16>(a, s);

@@ -61,14 +61,18 @@ def test_gemm_dense(lib, M, N, K, epi):
 @pytest.mark.parametrize("M,N,K", [(4896, 3072, 768), (10240, 2304, 768), (300, 256, 128), (7808, 768, 3072),
                                    (256, 512, 64)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
-def test_gemm256_forced(lib, M, N, K, epi):
-    """The 256x256 eight-phase kernel (forced) on the path's shapes, M tails and K = 64 / 128."""
+@pytest.mark.parametrize("cfg", [9, 11, 12, 13])
+def test_gemm_forced_configs(lib, M, N, K, epi, cfg):
+    """Forced tile configurations on the path's shapes, M tails and K = 64 / 128: 9 = the 256x256
+    eight-phase kernel, 11-13 = 32-deep K-tiles (BK 32) with 3-4 deep LDS rings."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K + 100 * epi)
     A = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
     bias = torch.randn(N, device="cuda", generator=g)
     ref = A.float() @ W.float().t() + bias
-    lib.mmt_gemm_force_config(9)
+    if cfg == 9 and N % 256:
+        pytest.skip("256 x 256 tiles need N % 256 == 0")
+    lib.mmt_gemm_force_config(cfg)
     try:
         if epi in (0, 1):
             C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
@@ -138,9 +142,11 @@ def test_gemm_conv3x3(lib, B, hw, cin, cout, epi):
     torch.testing.assert_close(out, ref, rtol=1e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("B,N", [(1, 320), (3, 244), (2, 153), (1, 720), (5, 190), (1, 17)])
+@pytest.mark.parametrize("B,N", [(1, 320), (3, 244), (2, 153), (1, 720), (5, 190), (1, 17),
+                                 (12, 320), (16, 244), (11, 190), (12, 153), (16, 64), (11, 17)])
 def test_attention(lib, B, N):
-    """attn.py:33-59 with the CE probability row of template token 27 (attn_blocks.py:44-53)."""
+    """attn.py:33-59 with the CE probability row of template token 27 (attn_blocks.py:44-53).
+    B * heads >= 128 with N <= 320 takes the whole-K/V-in-LDS kernel, the others the streaming one."""
     heads, C = 12, 768
     g = torch.Generator(device="cuda").manual_seed(N + B)
     qkv = (torch.randn(B, N, 3 * C, device="cuda", generator=g) * 2.0).bfloat16()
