@@ -28,18 +28,22 @@ constexpr int CE_MAX = 1024;   // max tokens for the exported CE row
 // byte offset of 16-B chunk c of row r in a [64][64] bf16 tile (128-B rows, chunk XOR row)
 __device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 
-template <int WAVES, bool SPLIT>
+template <int WAVES, bool SPLIT, int RB = 1>
 __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
   // SPLIT (fp32-faithful): every operand is an (hi, lo) bf16 pair and each product is
   // hi*hi + lo*hi + hi*lo; the LDS images of K and V^T are held for both halves.
+  // RB: 16-query row blocks per wave, multiplied together against each K / V fragment (fragment
+  // reads shared, RB independent softmax chains interleaved).
+  static_assert(RB == 1 || !SPLIT, "split mode uses one row block per wave");
   constexpr int NH = SPLIT ? 2 : 1;
+  constexpr int QW = 16 * RB;   // queries per wave
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NH][KB * 64];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[NH][KB * 64];
   __shared__ float ce_row[CE_MAX];
 
   // XCD-aware order: logical id = (b * heads + h) * nqt + qt; blocks bid, bid + 8, ... (one XCD) take a
   // contiguous logical range, so the query tiles of one (b, h) share an L2
-  const int nqt = (a.N + 16 * WAVES - 1) / (16 * WAVES);
+  const int nqt = (a.N + QW * WAVES - 1) / (QW * WAVES);
   const int nblk = nqt * a.heads * a.B;
   const int bid = blockIdx.x, xcd = bid & 7, jx = bid >> 3;
   const int q8 = nblk >> 3, r8 = nblk & 7;
@@ -49,38 +53,50 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N = a.N, Cd = 64 * a.heads, C3 = 3 * Cd;
   const bf16_t* base = a.qkv + (int64_t)b * N * C3;
-  const int q0 = qt * (16 * WAVES) + wave * 16;
-  const int qi = q0 + (lane & 15);
+  const int q0 = qt * (QW * WAVES) + wave * QW;
   const int g = lane >> 4;
 
   const bf16_t* base_lo = SPLIT ? a.qkv_lo + (int64_t)b * N * C3 : nullptr;
-  bf16x8 qf[NH][2];
+  bf16x8 qf[RB][NH][2];
 #pragma unroll
-  for (int hl = 0; hl < NH; ++hl)
+  for (int rb = 0; rb < RB; ++rb) {
+    const int qi = q0 + 16 * rb + (lane & 15);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16_t* bb = hl ? base_lo : base;
-      if (qi < N)
-        qf[hl][s] = *reinterpret_cast<const bf16x8*>(bb + (int64_t)qi * C3 + h * 64 + 32 * s + 8 * g);
-      else
-        qf[hl][s] = bf16x8{};
-    }
+    for (int hl = 0; hl < NH; ++hl)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16_t* bb = hl ? base_lo : base;
+        if (qi < N)
+          qf[rb][hl][s] = *reinterpret_cast<const bf16x8*>(bb + (int64_t)qi * C3 + h * 64 + 32 * s + 8 * g);
+        else
+          qf[rb][hl][s] = bf16x8{};
+      }
+  }
 
-  f32x4 o[4];
+  f32x4 o[RB][4];
+  float m[RB], l[RB];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
-  const bool ce_wave = a.ce_query >= q0 && a.ce_query < q0 + 16;
-  const bool ce_lane = ce_wave && (lane & 15) == a.ce_query - q0;
+  for (int rb = 0; rb < RB; ++rb) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[rb][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m[rb] = -INFINITY;
+    l[rb] = 0.f;
+  }
+  const bool ce_wave = a.ce_query >= q0 && a.ce_query < q0 + QW;
+  const int ce_rb = ce_wave ? (a.ce_query - q0) >> 4 : -1;
+  const bool ce_lane = ce_wave && (lane & 15) == ((a.ce_query - q0) & 15);
 
   // K/V staging, software-pipelined: the next tile's 16-B chunks are loaded into registers while the
   // current tile is multiplied, then copied to LDS
-  constexpr int NCHT = NH * KB * 8 / (WAVES * 64);   // chunks of K (and of V) per thread per tile
+  constexpr int NCHUNK = NH * KB * 8;                               // 16-B chunks of K (and of V) per tile
+  constexpr int NCHT = (NCHUNK + WAVES * 64 - 1) / (WAVES * 64);    // per thread
+  constexpr bool CH_EXACT = NCHUNK % (WAVES * 64) == 0;
   uint4 kreg[NCHT], vreg[NCHT];
   auto fetch = [&](int kb) {
 #pragma unroll
     for (int i = 0; i < NCHT; ++i) {
       const int q = tid + i * WAVES * 64;
+      if (!CH_EXACT && q >= NCHUNK) break;
       const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
       const int r = qq >> 3, c = qq & 7, key = kb + r;
       kreg[i] = make_uint4(0, 0, 0, 0);
@@ -98,6 +114,7 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < NCHT; ++i) {
       const int q = tid + i * WAVES * 64;
+      if (!CH_EXACT && q >= NCHUNK) break;
       const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
       const int r = qq >> 3, c = qq & 7;
       *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Ks[hl]) + tile_off(r, c)) = kreg[i];
@@ -106,74 +123,81 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
     __syncthreads();
     if (kb + KB < N) fetch(kb + KB);
 
-    f32x4 sc[4];
+    f32x4 sc[RB][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) sc[rb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int r = 16 * t + (lane & 15), c = 4 * s + g;
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(Ks[0]) + tile_off(r, c));
-        sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][s], sc[t], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) sc[rb][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[rb][0][s], sc[rb][t], 0, 0, 0);
         if (SPLIT) {
           const bf16x8 kl =
               *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(Ks[NH - 1]) + tile_off(r, c));
-          sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qf[0][s], sc[t], 0, 0, 0);
-          sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[NH - 1][s], sc[t], 0, 0, 0);
+          sc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qf[0][0][s], sc[0][t], 0, 0, 0);
+          sc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][NH - 1][s], sc[0][t], 0, 0, 0);
         }
       }
     }
-    float bmax = -INFINITY;
+    bf16x8 pf[RB][2], pl[RB][2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb + 16 * t + 4 * g + r;
-        const float v = key < N ? sc[t][r] * 0.125f : -INFINITY;
-        sc[t][r] = v;
-        bmax = fmaxf(bmax, v);
-      }
-    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
-    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
-    if (ce_lane) {
+    for (int rb = 0; rb < RB; ++rb) {
+      float bmax = -INFINITY;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kb + 16 * t + 4 * g + r;
-          if (key < N) ce_row[key] = sc[t][r];
+          const float v = key < N ? sc[rb][t][r] * 0.125f : -INFINITY;
+          sc[rb][t][r] = v;
+          bmax = fmaxf(bmax, v);
+        }
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+      if (ce_lane && rb == ce_rb) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kb + 16 * t + 4 * g + r;
+            if (key < N) ce_row[key] = sc[rb][t][r];
+          }
+      }
+      const float mnew = fmaxf(m[rb], bmax);
+      const float alpha = __expf(m[rb] - mnew);
+      float psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __expf(sc[rb][t][r] - mnew);
+          sc[rb][t][r] = p;
+          psum += p;
+        }
+      psum += __shfl_xor(psum, 16, 64);
+      psum += __shfl_xor(psum, 32, 64);
+      l[rb] = l[rb] * alpha + psum;
+      m[rb] = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[rb][dt] *= alpha;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pf[rb][u][r] = (__bf16)sc[rb][2 * u][r];
+          pf[rb][u][4 + r] = (__bf16)sc[rb][2 * u + 1][r];
+          if (SPLIT) {
+            pl[rb][u][r] = (__bf16)(sc[rb][2 * u][r] - (float)pf[rb][u][r]);
+            pl[rb][u][4 + r] = (__bf16)(sc[rb][2 * u + 1][r] - (float)pf[rb][u][4 + r]);
+          }
         }
     }
-    const float mnew = fmaxf(m, bmax);
-    const float alpha = __expf(m - mnew);
-    float psum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = __expf(sc[t][r] - mnew);
-        sc[t][r] = p;
-        psum += p;
-      }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
-    l = l * alpha + psum;
-    m = mnew;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
 
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      bf16x8 pf, pl;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pf[r] = (__bf16)sc[2 * u][r];
-        pf[4 + r] = (__bf16)sc[2 * u + 1][r];
-        if (SPLIT) {
-          pl[r] = (__bf16)(sc[2 * u][r] - (float)pf[r]);
-          pl[4 + r] = (__bf16)(sc[2 * u + 1][r] - (float)pf[4 + r]);
-        }
-      }
       // V^T fragment of keys {32u + 4g + 0..3} and {32u + 16 + 4g + 0..3} (the P element order) at
       // dim 16 dt + (lane & 15): two transposed reads; lane 4q + p of a 16-lane group addresses key
       // row q, dims 16 dt + 4p .. + 3
@@ -186,48 +210,60 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
         const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[0]) + oA));
         const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[0]) + oB));
         const bf16x8 vf = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) o[rb][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[rb][u], o[rb][dt], 0, 0, 0);
         if (SPLIT) {
           const bf16x4 w0 =
               __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[NH - 1]) + oA));
           const bf16x4 w1 =
               __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[NH - 1]) + oB));
           const bf16x8 vl = __builtin_shufflevector(w0, w1, 0, 1, 2, 3, 4, 5, 6, 7);
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, pf, o[dt], 0, 0, 0);
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl, o[dt], 0, 0, 0);
+          o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, pf[0][u], o[0][dt], 0, 0, 0);
+          o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl[0][u], o[0][dt], 0, 0, 0);
         }
       }
     }
   }
 
-  const float inv = 1.0f / l;
-  if (qi < N) {
-    const int64_t orow = ((int64_t)b * N + qi) * Cd + h * 64;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      float v[4];
-      bf16_t hv[4];
+  for (int rb = 0; rb < RB; ++rb) {
+    const int qi = q0 + 16 * rb + (lane & 15);
+    const float inv = 1.0f / l[rb];
+    if (qi < N) {
+      const int64_t orow = ((int64_t)b * N + qi) * Cd + h * 64;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = o[dt][r] * inv;
-        hv[r] = f2bf(v[r]);
-      }
-      uint2 w;
-      w.x = (uint32_t)hv[0] | ((uint32_t)hv[1] << 16);
-      w.y = (uint32_t)hv[2] | ((uint32_t)hv[3] << 16);
-      *reinterpret_cast<uint2*>(a.out + orow + 16 * dt + 4 * g) = w;
-      if (SPLIT) {
-        uint2 lo;
-        lo.x = (uint32_t)f2bf(v[0] - bf2f(hv[0])) | ((uint32_t)f2bf(v[1] - bf2f(hv[1])) << 16);
-        lo.y = (uint32_t)f2bf(v[2] - bf2f(hv[2])) | ((uint32_t)f2bf(v[3] - bf2f(hv[3])) << 16);
-        *reinterpret_cast<uint2*>(a.out_lo + orow + 16 * dt + 4 * g) = lo;
+      for (int dt = 0; dt < 4; ++dt) {
+        float v[4];
+        bf16_t hv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = o[rb][dt][r] * inv;
+          hv[r] = f2bf(v[r]);
+        }
+        uint2 w;
+        w.x = (uint32_t)hv[0] | ((uint32_t)hv[1] << 16);
+        w.y = (uint32_t)hv[2] | ((uint32_t)hv[3] << 16);
+        *reinterpret_cast<uint2*>(a.out + orow + 16 * dt + 4 * g) = w;
+        if (SPLIT) {
+          uint2 lo;
+          lo.x = (uint32_t)f2bf(v[0] - bf2f(hv[0])) | ((uint32_t)f2bf(v[1] - bf2f(hv[1])) << 16);
+          lo.y = (uint32_t)f2bf(v[2] - bf2f(hv[2])) | ((uint32_t)f2bf(v[3] - bf2f(hv[3])) << 16);
+          *reinterpret_cast<uint2*>(a.out_lo + orow + 16 * dt + 4 * g) = lo;
+        }
       }
     }
   }
   __syncthreads();
   if (ce_wave) {
-    const int src = a.ce_query - q0;
-    const float mm = __shfl(m, src, 64), ll = __shfl(l, src, 64);
+    const int src = (a.ce_query - q0) & 15;
+    float cm = m[0], cl = l[0];
+#pragma unroll
+    for (int rb = 1; rb < RB; ++rb)
+      if (rb == ce_rb) {
+        cm = m[rb];
+        cl = l[rb];
+      }
+    const float mm = __shfl(cm, src, 64), ll = __shfl(cl, src, 64);
     const int Ls = N - a.ce_lens_t;
     float* dst = a.ce_prob + ((int64_t)b * a.heads + h) * Ls;
     for (int j = lane; j < Ls; j += 64) dst[j] = __expf(ce_row[a.ce_lens_t + j] - mm) / ll;
@@ -238,6 +274,14 @@ template <bool SPLIT>
 static void attention_t(const AttnArgs& a, hipStream_t s) {
   const int per4 = a.B * a.heads * ((a.N + 63) / 64);
   const int bh = a.B * a.heads;
+  // long joint sequences (OSTrack-384, N = 720) in bf16: 8 waves x 16 queries per workgroup -- one
+  // K/V staging shared by 128 queries, half the L2 re-reads of 4 waves (-24 % kernel time, +2.5 %
+  // end to end; at the ViPT lengths N <= 320 it measured level in isolation and -0.4 % end to end)
+  static const int w8 = getenv("MMT_ATTN_W") ? atoi(getenv("MMT_ATTN_W")) : 0;
+  if (!SPLIT && bh >= 128 && (w8 == 8 || (w8 == 0 && a.N > 320))) {
+    hipLaunchKernelGGL((attn_kernel<8, false>), dim3((a.N + 127) / 128 * bh), dim3(512), 0, s, a);
+    return;
+  }
   if (per4 >= 240) {
     hipLaunchKernelGGL((attn_kernel<4, SPLIT>), dim3((a.N + 63) / 64 * bh), dim3(256), 0, s, a);
   } else if (per4 * 2 >= 240) {

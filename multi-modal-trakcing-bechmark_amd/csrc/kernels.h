@@ -107,7 +107,8 @@ struct LnPromptArgs {
   const float* w; const float* b;
   bf16_t* out; bf16_t* out_lo;
 };
-// fovea (s8 for every slot), then the prompt residual (conv1x1 of s8, formed in registers) and LN1
+// fovea (s8 for every slot), then the prompt residual (conv1x1 of s8, formed per row from an LDS copy
+// of conv1x1) and LN1
 // for the compact rows
 void prompt_expand_ln(const PromptArgs& pa, const LnPromptArgs& a, hipStream_t s);
 

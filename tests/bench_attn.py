@@ -11,10 +11,10 @@ from mmtrack_amd import _lib  # noqa: E402
 lib = _lib.load()
 B = int(os.environ.get("B", "32"))
 s = torch.cuda.current_stream().cuda_stream
-for N in [int(n) for n in os.environ.get("NS", "320,244,190,153").split(",")]:
+for N in [int(n) for n in os.environ.get("NS", "320,244,190,153,720").split(",")]:
     qkv = (torch.randn(B, N, 3 * 768, device="cuda") * 2.0).bfloat16()
     out = torch.empty(B, N, 768, device="cuda", dtype=torch.bfloat16)
-    prob = torch.empty(B, 12, N - 64, device="cuda")
+    prob = torch.empty(B, 12, N - 64, device="cuda")  # (OSTrack-384: N = 720)
     run = lambda: lib.mmt_op_attention(qkv.data_ptr(), out.data_ptr(), B, N, 12, 27, 64, prob.data_ptr(), s)
     for _ in range(3):
         run()

@@ -143,10 +143,11 @@ def test_gemm_conv3x3(lib, B, hw, cin, cout, epi):
 
 
 @pytest.mark.parametrize("B,N", [(1, 320), (3, 244), (2, 153), (1, 720), (5, 190), (1, 17),
-                                 (12, 320), (16, 244), (11, 190), (12, 153), (16, 64), (11, 17)])
+                                 (12, 320), (16, 244), (11, 190), (12, 153), (16, 64), (11, 17), (11, 720),
+                                 (12, 548)])
 def test_attention(lib, B, N):
     """attn.py:33-59 with the CE probability row of template token 27 (attn_blocks.py:44-53).
-    B * heads >= 128 with N <= 320 takes the whole-K/V-in-LDS kernel, the others the streaming one."""
+    B * heads >= 128 with N > 320 takes the 8-wave workgroups, the others 1-4 waves."""
     heads, C = 12, 768
     g = torch.Generator(device="cuda").manual_seed(N + B)
     qkv = (torch.randn(B, N, 3 * C, device="cuda", generator=g) * 2.0).bfloat16()
