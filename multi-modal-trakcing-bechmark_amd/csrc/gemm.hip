@@ -815,8 +815,10 @@ static void launch_persist(const GemmArgs& a0, hipStream_t s) {
 template <int BM, int BN, int WMW, int WNW, bool SPLIT, int ST = 2, int BK = 64>
 static void launch_cfg(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.amode == A_CONV3) {
-    if (epi == EPI_RELU_BF16) return launch_one<BM, BN, WMW, WNW, EPI_RELU_BF16, A_CONV3, SPLIT, ST>(a, s);
-    if (epi == EPI_RELU_F32) return launch_one<BM, BN, WMW, WNW, EPI_RELU_F32, A_CONV3, SPLIT, ST>(a, s);
+    if constexpr (BK == 64) {   // the conv gather walks 64-channel K-tiles
+      if (epi == EPI_RELU_BF16) return launch_one<BM, BN, WMW, WNW, EPI_RELU_BF16, A_CONV3, SPLIT, ST>(a, s);
+      if (epi == EPI_RELU_F32) return launch_one<BM, BN, WMW, WNW, EPI_RELU_F32, A_CONV3, SPLIT, ST>(a, s);
+    }
     return;
   }
   switch (epi) {
@@ -883,6 +885,8 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         case 11: return launch_cfg<128, 128, 4, 2, false, 4, 32>(a, epi, s);
         case 12: return launch_cfg<128, 128, 4, 2, false, 3, 32>(a, epi, s);
         case 13: return launch_cfg<128, 64, 2, 2, false, 4, 32>(a, epi, s);
+        case 14: return launch_cfg<256, 128, 4, 2, false, 3, 32>(a, epi, s);
+        case 15: return launch_cfg<256, 128, 4, 2, false, 4, 32>(a, epi, s);
         case 10:
           if (a.N % 128 == 0 && a.groups == 1 && (epi == EPI_BF16 || epi == EPI_GELU_BF16))
             return epi == EPI_BF16 ? launch_persist<EPI_BF16>(a, s) : launch_persist<EPI_GELU_BF16>(a, s);
