@@ -568,6 +568,222 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_persist_kernel(const GemmA
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Persistent ring GEMM for the bf16-output GEMMs (qkv, fc1), no LDS in the epilogue.
+//
+// A grid of up to two workgroups per CU walks its XCD's tile range (as gemm_persist_kernel), and the
+// K-tiles of ALL of a workgroup's output tiles form one stream s = t * nk + kt through an NS-deep LDS
+// ring: step s + NS - 1 is issued while step s is multiplied, across tile boundaries, so the loads of
+// the next tile are in flight while the current tile's epilogue runs (a tile boundary costs no
+// prologue).  The epilogue never touches LDS (the ring keeps streaming): bias + activation per lane,
+// then a 4 x 4 transpose of 8-byte bf16 quads across the wave's four 16-lane groups
+// (v_permlane32_swap + v_permlane16_swap) so a lane holds 16 consecutive columns of one row, and
+// 16-B buffer stores (rows past M fall outside the C resource and are dropped, so every tile issues
+// the same number of stores).  vmcnt bookkeeping: a step's wait lets the younger ring loads stay in
+// flight and, within NS - 1 steps after an epilogue, that epilogue's stores and the next tile's bias
+// loads (issued after it) as well.
+template <int N>
+__device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <int MAXN>
+__device__ __forceinline__ void vm_wait_rt(int n) {   // n wave-uniform; scalar branch to an immediate
+  if constexpr (MAXN > 0) {
+    if (n >= MAXN) return vm_wait_n<MAXN>();
+    return vm_wait_rt<MAXN - 1>(n);
+  } else {
+    vm_wait_n<0>();
+  }
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int WMW, int WNW, int EPI, int NS, int BK>
+__global__ __launch_bounds__(WMW* WNW * 64) void gemm_ring_kernel(const GemmArgs args) {
+  using T = Tile<BM, BN, WMW, WNW, false, NS, BK>;
+  static_assert(epi_is_bf16(EPI) && T::FN % 4 == 0, "bf16 outputs, wave tiles of 64-column multiples");
+  constexpr int D = NS - 1;
+  constexpr int GPW = T::GROUPS / T::NW;
+  constexpr int RPI = T::NW * T::RPW;
+  static_assert(BM % RPI == 0 && BN % RPI == 0, "row blocks must not straddle operands");
+  constexpr int NSTORE = T::FM * (T::FN / 4) * 2;   // 16-B stores per lane per tile
+  constexpr int NBIAS = 1;                          // bias LDS-DMA pieces per wave per tile
+  static_assert(BN <= 256, "one 1-KB bias piece per tile");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * T::STAGE];
+  __shared__ __attribute__((aligned(16))) float sbias[2][256];   // bias of tile t in slot t & 1
+
+  const GemmGroup& g = args.g[0];
+  const int M = args.M, K = args.K;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = args.N / BN, ntiles = tiles_m * tiles_n;
+  const int b = blockIdx.x, x = b & 7, j = b >> 3, nb8 = gridDim.x >> 3;
+  const int per = (ntiles + 7) >> 3;
+  const int lo = x * per, hi = min(ntiles, lo + per);
+  const int first = lo + j;
+  if (first >= hi) return;
+  const int nt = (hi - first + nb8 - 1) / nb8;
+  const int nk = K / BK, G = nt * nk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+
+  const int chunk = (BK == 64 ? ((lane & 7) ^ (lane >> 3)) : ((lane & 3) ^ ((lane >> 4) & 2))) * 16;
+  uint32_t voff[GPW];
+#pragma unroll
+  for (int i = 0; i < GPW; ++i) {
+    const int r0 = i * RPI;
+    const int row = r0 + wave * T::RPW + lane / (BK / 8);
+    voff[i] = r0 < BM ? (uint32_t)(row * g.lda * 2 + chunk) : (uint32_t)((row - BM) * g.ldw * 2 + chunk);
+  }
+  auto geom = [&](int t, int& m0, int& n0) {
+    int tm, tn;
+    tile_of(first + t * nb8, tiles_m, tiles_n, args.gm, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  // issue cursor: the next K-step to load (tile is_t, K-tile is_kt, ring slot is_slot); the tile's
+  // geometry and buffer resources are recomputed once per tile, not per step
+  int is_t = 0, is_kt = 0, is_slot = 0;
+  int im0, in0;
+  geom(0, im0, in0);
+  rsrc_t rA = make_rsrc(g.A + (int64_t)im0 * g.lda, (int64_t)(M - im0) * g.lda * 2);
+  rsrc_t rW = make_rsrc(g.W + (int64_t)in0 * g.ldw, (int64_t)BN * g.ldw * 2);
+  auto issue_next = [&]() {
+    bf16_t* sbase = smem + is_slot * T::STAGE;
+    const int so = is_kt * BK * 2;
+#pragma unroll
+    for (int i = 0; i < GPW; ++i) {
+      const int r0 = i * RPI;
+      lptr_t dst = (lptr_t)(sbase + (r0 + wave * T::RPW) * BK);
+      const uint32_t vo = voff[i];
+      if (r0 < BM) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, vo, so, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, dst, 16, vo, so, 0, 0);
+    }
+    is_slot = is_slot + 1 == NS ? 0 : is_slot + 1;
+    if (++is_kt == nk) {
+      is_kt = 0;
+      if (++is_t < nt) {
+        geom(is_t, im0, in0);
+        rA = make_rsrc(g.A + (int64_t)im0 * g.lda, (int64_t)(M - im0) * g.lda * 2);
+        rW = make_rsrc(g.W + (int64_t)in0 * g.ldw, (int64_t)BN * g.ldw * 2);
+      }
+    }
+  };
+  // the tile's bias goes to LDS by DMA (every wave issues the same 1-KB piece, so each wave's own vmcnt
+  // covers the bytes it reads); no VGPR-destination load exists in the kernel, so the compiler inserts
+  // no vmcnt wait of its own
+  auto load_bias = [&](int n0, int slot) {
+    const rsrc_t rB = make_rsrc(g.bias ? g.bias + n0 : nullptr, g.bias ? BN * 4 : 0);
+    const uint32_t vo = (uint32_t)((lane % (BN / 4)) * 16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lptr_t)&sbias[slot][0], 16, vo, 0, 0, 0);
+  };
+  f32x4 acc[T::FM][T::FN];
+#pragma unroll
+  for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < T::FN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int slot) {
+    const bf16_t* S = smem + slot * T::STAGE;
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      const int c = 4 * s + (lane >> 4);
+      bf16x8 ah[T::FM], bh[T::FN];
+#pragma unroll
+      for (int i = 0; i < T::FM; ++i) ah[i] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(wm * T::WM + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj)
+        bh[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(BM + wn * T::WN + jj * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < T::FN; ++jj)
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[jj], ah[i], acc[i][jj], 0, 0, 0);
+    }
+  };
+  auto epilogue = [&](int m0, int n0, int slot) {
+    float4 bias[T::FN];
+#pragma unroll
+    for (int jj = 0; jj < T::FN; ++jj)
+      bias[jj] = *reinterpret_cast<const float4*>(&sbias[slot][wn * T::WN + jj * 16 + (lane >> 4) * 4]);
+    const rsrc_t rC = make_rsrc(static_cast<bf16_t*>(g.C) + (int64_t)m0 * g.ldc, (int64_t)(M - m0) * g.ldc * 2);
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i) {
+      const int row = wm * T::WM + i * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < T::FN / 4; ++q) {
+        uint32_t px[4], py[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          float v[4];
+          epi_values<EPI>(bias[4 * q + jj], acc[i][4 * q + jj], v);
+          px[jj] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          py[jj] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        }
+        // lane group G (= lane >> 4) holds columns 16 jj + 4 G .. + 3 in quad jj; afterwards quad jj
+        // of group G holds columns 16 G + 4 jj .. + 3 (a 4 x 4 transpose of quads)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          auto r = __builtin_amdgcn_permlane32_swap(px[jj], px[jj + 2], false, false);
+          px[jj] = r[0];
+          px[jj + 2] = r[1];
+          r = __builtin_amdgcn_permlane32_swap(py[jj], py[jj + 2], false, false);
+          py[jj] = r[0];
+          py[jj + 2] = r[1];
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; jj += 2) {
+          auto r = __builtin_amdgcn_permlane16_swap(px[jj], px[jj + 1], false, false);
+          px[jj] = r[0];
+          px[jj + 1] = r[1];
+          r = __builtin_amdgcn_permlane16_swap(py[jj], py[jj + 1], false, false);
+          py[jj] = r[0];
+          py[jj + 1] = r[1];
+        }
+        const int col = n0 + wn * T::WN + q * 64 + (lane >> 4) * 16;
+        const int off = (row * (int)g.ldc + col) * 2;
+        const u32x4 lo4 = {px[0], py[0], px[1], py[1]};
+        const u32x4 hi4 = {px[2], py[2], px[3], py[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(lo4, rC, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(hi4, rC, off + 16, 0, 0);
+      }
+    }
+  };
+
+  int m0, n0;
+  geom(0, m0, n0);
+  load_bias(n0, 0);
+  for (int p = 0; p < D; ++p)
+    if (p < G) issue_next();
+  vm_wait_rt<GPW * D>(GPW * (min(D, G) - 1));
+  __builtin_amdgcn_s_barrier();
+  int kt = 0, t = 0, e_last = -(1 << 20), slot = 0;
+  for (int s = 0; s < G; ++s) {
+    const bool steady = s + D < G;
+    if (steady) issue_next();
+    compute(slot);
+    slot = slot + 1 == NS ? 0 : slot + 1;
+    // step s + 1 must have landed; younger: the ring loads of steps s + 2 .. min(s + D, G - 1) and, within
+    // D steps after an epilogue, its stores and bias piece
+    const bool extra = s + 1 <= e_last + D;
+    if (steady) {
+      if (extra) vm_wait_n<GPW * (D - 1) + NSTORE + NBIAS>();
+      else vm_wait_n<GPW * (D - 1)>();
+    } else if (s + 1 < G) {
+      vm_wait_rt<GPW * (D - 1) + NSTORE + NBIAS>(GPW * (G - 2 - s) + (extra ? NSTORE + NBIAS : 0));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (++kt == nk) {
+      epilogue(m0, n0, t & 1);
+      kt = 0;
+      ++t;
+      if (t < nt) geom(t, m0, n0);
+      load_bias(n0, t & 1);   // next tile's bias (after the last tile a harmless reload: a constant count)
+      e_last = s;
+#pragma unroll
+      for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < T::FN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
 static int num_cus() {
   static int n = 0;
   if (!n) {
@@ -812,6 +1028,26 @@ static void launch_persist(const GemmArgs& a0, hipStream_t s) {
   hipLaunchKernelGGL((gemm_persist_kernel<128, 128, 4, 2, EPI>), dim3(grid), dim3(512), 0, s, a);
 }
 
+template <int BM, int BN, int WMW, int WNW, int EPI, int NS, int BK, int WG_PER_CU>
+static void launch_ring(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  const int tiles_m = (a.M + BM - 1) / BM, ntiles = tiles_m * (a.N / BN);
+  a.gm = tiles_m < 8 ? tiles_m : 8;
+  static const int slots = WG_PER_CU * num_cus();
+  int grid = (ntiles < slots ? ntiles : slots) & ~7;
+  if (grid < 8) grid = 8;
+  hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, WMW, WNW, EPI, NS, BK>), dim3(grid), dim3(WMW * WNW * 64), 0, s, a);
+}
+
+template <int BM, int BN, int WMW, int WNW, int NS, int BK, int WG_PER_CU>
+static bool launch_ring_epi(const GemmArgs& a, int epi, hipStream_t s) {
+  // K / BK >= NS: a tile's bias (issued after the previous epilogue) has landed before its own epilogue
+  if (a.N % BN != 0 || a.groups != 1 || a.amode != A_DENSE || a.K % BK != 0 || a.K / BK < NS) return false;
+  if (epi == EPI_BF16) return launch_ring<BM, BN, WMW, WNW, EPI_BF16, NS, BK, WG_PER_CU>(a, s), true;
+  if (epi == EPI_GELU_BF16) return launch_ring<BM, BN, WMW, WNW, EPI_GELU_BF16, NS, BK, WG_PER_CU>(a, s), true;
+  return false;
+}
+
 template <int BM, int BN, int WMW, int WNW, bool SPLIT, int ST = 2, int BK = 64>
 static void launch_cfg(const GemmArgs& a, int epi, hipStream_t s) {
   if (a.amode == A_CONV3) {
@@ -887,6 +1123,15 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         case 13: return launch_cfg<128, 64, 2, 2, false, 4, 32>(a, epi, s);
         case 14: return launch_cfg<256, 128, 4, 2, false, 3, 32>(a, epi, s);
         case 15: return launch_cfg<256, 128, 4, 2, false, 4, 32>(a, epi, s);
+        case 16: if (launch_ring_epi<256, 128, 4, 2, 3, 32, 2>(a, epi, s)) return; break;
+        case 17: if (launch_ring_epi<128, 128, 4, 2, 4, 32, 2>(a, epi, s)) return; break;
+        case 18: if (launch_ring_epi<128, 128, 4, 2, 2, 64, 2>(a, epi, s)) return; break;
+        case 19: if (launch_ring_epi<256, 256, 4, 2, 3, 32, 1>(a, epi, s)) return; break;
+        case 20: if (launch_ring_epi<256, 128, 4, 2, 2, 64, 1>(a, epi, s)) return; break;
+        case 21: return launch_cfg<128, 64, 4, 2, false, 2>(a, epi, s);
+        case 22: return launch_cfg<64, 128, 2, 4, false, 2>(a, epi, s);
+        case 23: return launch_cfg<128, 64, 4, 2, false, 3>(a, epi, s);
+        case 24: return launch_cfg<64, 128, 2, 4, false, 3>(a, epi, s);
         case 10:
           if (a.N % 128 == 0 && a.groups == 1 && (epi == EPI_BF16 || epi == EPI_GELU_BF16))
             return epi == EPI_BF16 ? launch_persist<EPI_BF16>(a, s) : launch_persist<EPI_GELU_BF16>(a, s);
@@ -908,7 +1153,11 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     if (epi == EPI_BF16) return launch_persist<EPI_BF16>(a, s);
     if (epi == EPI_GELU_BF16) return launch_persist<EPI_GELU_BF16>(a, s);
   }
-  if (a.N % 128 == 0 && t128 * (a.N / 128) * a.groups >= target) return launch_cfg<128, 128, 4, 2, SPLIT>(a, epi, s);
+  // a little under one 128 x 128 tile per CU (the N = 768 GEMMs of the CE-pruned layers): 128 x 64 tiles
+  // with 8 waves put two workgroups on most CUs (fc2 at M = 4896: 41.4 -> 34.8 us)
+  const int t128n = t128 * (a.N / 128) * a.groups;
+  if (a.N % 128 == 0 && t128n >= target && t128n < num_cus()) return launch_cfg<128, 64, 4, 2, SPLIT>(a, epi, s);
+  if (a.N % 128 == 0 && t128n >= target) return launch_cfg<128, 128, 4, 2, SPLIT>(a, epi, s);
   if (a.N % 64 == 0) {
     if (t128 * (a.N / 64) * a.groups >= target) return launch_cfg<128, 64, 2, 2, SPLIT>(a, epi, s);
     // few 64 x 64 tiles and a long K (small batches): split K over workgroups (fp32 partials in the

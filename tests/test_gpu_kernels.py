@@ -33,7 +33,7 @@ def _gemm(lib, A, W, bias, C, R=None, epi=0, conv_hw=0, conv_cin=0, pos_rows=0, 
 
 
 @pytest.mark.parametrize("M,N,K", [(320, 2304, 768), (306, 768, 3072), (64, 128, 768), (5120, 3072, 768),
-                                   (153, 768, 768), (1, 32, 64)])
+                                   (153, 768, 768), (1, 32, 64), (4896, 768, 3072), (4896, 768, 768)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 4])
 def test_gemm_dense(lib, M, N, K, epi):
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + epi)
@@ -107,6 +107,33 @@ def test_gemm_persistent_forced(lib, M, N, K, epi):
         lib.mmt_gemm_force_config(-1)
     torch.testing.assert_close(C.float(), F.gelu(ref) if epi == 1 else ref, rtol=1e-2, atol=1e-2)
     assert torch.equal(C, C0)   # same K order per output: bit-identical to the per-tile kernels
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(10240, 3072, 768, 1), (10240, 2304, 768, 0), (7808, 2304, 768, 0),
+                                       (4899, 3072, 768, 1), (60000, 256, 128, 0), (9000, 512, 128, 1),
+                                       (300, 256, 256, 1)])
+@pytest.mark.parametrize("cfg", [16, 17, 18, 19, 20])
+def test_gemm_ring_forced(lib, M, N, K, epi, cfg):
+    """The persistent ring kernel (forced): one K-tile stream across a workgroup's output tiles, the
+    permlane-transposed register epilogue, bias through LDS, M tails dropped by the C resource, small
+    grids; bit-identical to the per-tile kernels (same K order per output)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 11 * epi)
+    A = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    ref = A.float() @ W.float().t() + bias
+    C0 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    lib.mmt_gemm_force_config(3)   # a per-tile kernel (128 x 128, 4 waves) as the bitwise reference
+    try:
+        _gemm(lib, A, W, bias, C0, epi=epi)
+        lib.mmt_gemm_force_config(cfg)
+        C = torch.full((M + 1, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        _gemm(lib, A, W, bias, C[:M], epi=epi)
+    finally:
+        lib.mmt_gemm_force_config(-1)
+    torch.testing.assert_close(C[:M].float(), F.gelu(ref) if epi == 1 else ref, rtol=1e-2, atol=1e-2)
+    assert torch.equal(C[:M], C0)
+    assert torch.isnan(C[M].float()).all(), "a store past row M"
 
 
 def test_gemm_pos_epilogue(lib):
