@@ -1,6 +1,7 @@
 """Headline benchmark: tracked frames/sec/GPU, ViPT-deep ViT-B, 128^2 template / 256^2 search, bf16.
 
-One "step" = one tracking step of B independent sequences on each GPU (mmt_track_batch): crop +
+One "step" = one tracking step of B independent sequences on each GPU (mmt_track_batch_submit +
+_fetch, frames pipelined LAG deep; --sync: blocking mmt_track_batch): crop geometry from the last box +
 normalise from the HBM-resident frame, dual patch-embed, 12 ViT-B blocks with deep prompts and CE,
 CENTER head, windowed argmax decode, box back-mapping.  Frames are synthetic 640x480x6 uint8
 (RGB + thermal-like aux) already resident in HBM; weights are the seeded synthetic law of
@@ -11,6 +12,7 @@ Multi-GPU: one process per GPU (torchrun), sequences sharded per rank, no data-p
 max-over-ranks of the timed region only.
 """
 import argparse
+import collections
 import json
 import os
 import sys
@@ -26,6 +28,7 @@ import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0
+LAG = 2   # frames a sequence may have in flight ahead of its fetched boxes (pipelined mode)
 
 WORKLOADS = {
     # name: (engine kwargs, synth shape kwargs, frame H, W, C, published-config description)
@@ -107,6 +110,7 @@ def main():
     ap.add_argument("--workload", default="vipt_deep_rgbt", choices=list(WORKLOADS))
     ap.add_argument("--frames", type=int, default=8, help="distinct synthetic frames per sequence (cycled)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--sync", action="store_true", help="blocking per-frame calls (no frame pipelining)")
     ap.add_argument("--probe", default="fc1", help="kernel class timed with HIP events for the roofline ('none': off)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -141,15 +145,29 @@ def main():
     def step(k):
         eng.track_batch(0, frame_lists[k % args.frames])
 
-    for k in range(max(args.warmup, 2)):
-        step(k)
+    def run(k0, count):
+        """`count` frames of every sequence.  Pipelined (default): the tracker state lives on the device,
+        so frame k+1 is submitted before frame k's boxes are fetched (at most LAG frames in flight);
+        every frame's boxes reach the host before this returns.  --sync: one blocking call per frame."""
+        if args.sync:
+            for k in range(k0, k0 + count):
+                step(k)
+            return
+        pend = collections.deque()
+        for k in range(k0, k0 + count):
+            pend.append(eng.track_batch_submit(0, frame_lists[k % args.frames]))
+            if len(pend) > LAG:
+                eng.track_batch_fetch(pend.popleft())
+        while pend:
+            eng.track_batch_fetch(pend.popleft())
+
+    run(0, max(args.warmup, 2))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
+    run(args.warmup, args.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
@@ -189,7 +207,8 @@ def main():
             "config": {"workload": args.workload, "description": desc, "sequences_per_gpu": B,
                        "global_batch": B * world, "frame": f"{W}x{H}x{C} uint8 (HBM-resident)",
                        "template": cfg.template_size, "search": cfg.search_size, "parallelism": f"seq-shard x{world}",
-                       "graphs": cfg.use_graphs, "weights": "synthetic seeded (no checkpoint ships)"},
+                       "graphs": cfg.use_graphs, "pipelined_frames": 0 if args.sync else LAG,
+                       "weights": "synthetic seeded (no checkpoint ships)"},
             "per_gpu_fps": round(value / world, 2),
             "model_tflops": round(value * gf / 1e3, 1),
             "roofline": roof,

@@ -96,6 +96,20 @@ int mmt_track_batch(mmt_engine* e, int first_slot, int n, const uint8_t* const* 
 int mmt_get_state(const mmt_engine* e, int slot, double out_xywh[4]);
 int mmt_set_state(mmt_engine* e, int slot, const double xywh[4]);
 
+/* pipelined tracking.  The tracker state machine of ViPTTrack.track (crop geometry from the last box,
+ * processing_utils.py:32-41; box back-map + clip_box, vipt.py:84-88, box_ops.py:97-106) runs on the
+ * device, so a sequence's frame t+1 may be submitted before frame t's result is fetched: the host
+ * round trip leaves the per-frame critical path.  mmt_track_batch == submit + fetch.
+ *   submit: enqueue one frame for each of the n sequences (frames as in mmt_track_batch) -> ticket;
+ *   fetch:  wait for that frame's results ('target_bbox', 'best_score' per sequence) and report its
+ *           errors ("Too small bounding box." surfaces here when frames were in flight; the failing
+ *           sequence keeps its state, the others advance).
+ * At most MMT_PIPELINE_DEPTH submitted frames may be unfetched; initialize / set_state need none. */
+#define MMT_PIPELINE_DEPTH 8
+int mmt_track_batch_submit(mmt_engine* e, int first_slot, int n, const uint8_t* const* frames, const int* H,
+                           const int* W, int C, const int64_t* row_stride, int is_device, int64_t* ticket);
+int mmt_track_batch_fetch(mmt_engine* e, int64_t ticket, double* out_xywh, float* out_score);
+
 /* parity / debug read-back of the last track call (debug_outputs = 1):
  *   "crop"   uint8 [S][S][C]  search patch         "maps"  f32 [5][fs*fs] ctr,size_w,size_h,off_x,off_y
  *   "feat"   f32 [Lz+Lx][768] backbone output      "removed" i32 [Lx] removed slots, CE order

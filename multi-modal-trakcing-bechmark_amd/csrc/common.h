@@ -52,19 +52,21 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 // bf16-output GELU: the same erf GELU with erfc from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 on
-// erf, five coefficients; 1/2 and log2(e) folded as above): one v_rcp_f32, five FMAs, one v_exp_f32.
+// erf, five coefficients; 1/2 and log2(e) folded as above), written as
+//   GELU(x) = relu(x) - |x| * h(|x|),   h(a) = t p(t) 2^(-x^2 log2(e) / 2),  t = 1 / (1 + 0.3275911 a / sqrt2)
+// (x >= 0: x - x h; x < 0: x h), so the epilogue spends one v_rcp_f32, one v_exp_f32 and eleven
+// single-issue VALU ops per output (|x| and -|x| are source modifiers, no select).
 // Against exact erf GELU the result differs by < 5e-7 * max(1, |x|); after rounding to bf16, about
 // 0.1 % of outputs move by one bf16 ulp (tests/test_oracle_golden.py).  Used where the GEMM writes
 // plain bf16 (the fp32-faithful mode keeps gelu_erf).
 __device__ __forceinline__ float gelu_erf_bf16out(float x) {
-  const float u = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.0f));
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.2316418917f, a, 1.0f));   // 0.3275911 / sqrt2
   float p = 0.5307027145f;
   p = fmaf(p, t, -0.7265760135f);
   p = fmaf(p, t, 0.7107068705f);
   p = fmaf(p, t, -0.142248368f);
   p = fmaf(p, t, 0.127414796f);
-  const float h = t * p * __builtin_amdgcn_exp2f(-(u * 1.44269504f) * u);
-  const float xh = x * h;
-  return x >= 0.f ? x - xh : xh;
+  const float e = __builtin_amdgcn_exp2f((x * -0.7213475204f) * x);      // exp(-x^2 / 2)
+  return fmaf(-a, (p * t) * e, fmaxf(x, 0.f));
 }

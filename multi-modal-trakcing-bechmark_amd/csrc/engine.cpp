@@ -72,6 +72,8 @@ struct TimingProbe {
 
 }  // namespace
 
+constexpr int kRing = MMT_PIPELINE_DEPTH;   // submitted-but-unfetched frames an engine holds
+
 struct mmt_engine {
   mmt_config cfg{};
   int device = 0;
@@ -120,8 +122,22 @@ struct mmt_engine {
   int *gidx0 = nullptr, *gidx1 = nullptr, *slot2pos = nullptr, *gather = nullptr, *removed = nullptr;
   uint8_t* dbg_patch = nullptr;
   CropParam* params_dev = nullptr;
-  CropParam* params_host = nullptr;   // pinned
-  float* res_host = nullptr;          // pinned
+  SeqState* state_dev = nullptr;      // [max_batch] tracker state per slot (device-resident)
+  TrackOut* out_dev = nullptr;        // [max_batch] per-launch results
+  CropParam* params_host = nullptr;   // pinned [kRing][max_batch]
+  TrackOut* outs_host = nullptr;      // pinned [kRing][max_batch]
+
+  // pipelined frames (mmt_track_batch_submit / _fetch): ticket t uses ring entry t % kRing
+  struct Ticket {
+    int64_t id = -1;
+    int first = 0, n = 0;
+    bool open = false;
+    hipEvent_t done = nullptr;
+    const GraphEntry* replayed = nullptr;
+  };
+  Ticket ring[kRing];
+  int64_t next_ticket = 0;
+  int unfetched = 0;
 
   // host-frame staging (per slot)
   std::vector<uint8_t*> frame_dev;
@@ -130,7 +146,6 @@ struct mmt_engine {
   // tracker state (vipt.py:57, 88) in doubles
   std::vector<std::array<double, 4>> state;
   std::vector<char> active;
-  std::vector<double> last_rf;
   int last_batch = 0;
 
   std::map<std::tuple<int, int, std::string>, GraphEntry> graphs;
@@ -456,6 +471,7 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->gidx0, (size_t)B * Lx * 4},         {(void**)&e->gidx1, (size_t)B * Lx * 4},
       {(void**)&e->slot2pos, (size_t)B * Lx * 4},      {(void**)&e->gather, (size_t)B * L * 4},
       {(void**)&e->removed, (size_t)B * Lx * 4},       {(void**)&e->params_dev, (size_t)B * sizeof(CropParam)},
+      {(void**)&e->state_dev, (size_t)B * sizeof(SeqState)}, {(void**)&e->out_dev, (size_t)B * sizeof(TrackOut)},
   };
   reqs.push_back({(void**)&e->zero, 256});
   if (e->split) {
@@ -481,8 +497,9 @@ int alloc_acts(mmt_engine* e) {
     *r.p = static_cast<char*>(e->aarena) + off;
     off += (r.bytes + 255) & ~size_t(255);
   }
-  HIPCHECK(e, hipHostMalloc((void**)&e->params_host, (size_t)B * sizeof(CropParam), hipHostMallocDefault));
-  HIPCHECK(e, hipHostMalloc((void**)&e->res_host, (size_t)B * 8 * 4, hipHostMallocDefault));
+  HIPCHECK(e, hipHostMalloc((void**)&e->params_host, (size_t)kRing * B * sizeof(CropParam), hipHostMallocDefault));
+  HIPCHECK(e, hipHostMalloc((void**)&e->outs_host, (size_t)kRing * B * sizeof(TrackOut), hipHostMallocDefault));
+  for (auto& t : e->ring) HIPCHECK(e, hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
   return MMT_OK;
 }
 
@@ -631,7 +648,8 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
   bf16_t* A_rgb_l = off(e->A_rgb_l, (size_t)b0 * L * C);
   bf16_t* A_aux_l = off(e->A_aux_l, (size_t)b0 * L * C);
 
-  // 1. crop + normalise + patchify the search region of every sequence
+  // 1. crop geometry from each sequence's device-resident state, then crop + normalise + patchify
+  crop_geometry(e->params_dev + r0, e->state_dev + b0, n, c.search_factor, c.search_size, s);
   CropArgs ca{};
   ca.params = e->params_dev + r0;
   ca.B = n;
@@ -844,6 +862,10 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
   da.hann = e->hann;
   da.res = q_res;
   da.maps = q_dbg_maps;
+  da.state = e->state_dev + b0;
+  da.params = e->params_dev + r0;
+  da.out = e->out_dev + r0;
+  da.search_size = c.search_size;
   decode(da, s);
 }
 
@@ -879,28 +901,6 @@ int stage_frame(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww, i
   HIPCHECK(e, hipMemcpyAsync(e->frame_dev[slot], frame, bytes, hipMemcpyHostToDevice, e->stream));
   *dev = e->frame_dev[slot];
   return MMT_OK;
-}
-
-// vipt.py:84-88 + box_ops.py:97-106, float/double exactly as the reference's tensor/python mix
-void update_state(mmt_engine* e, int slot, const float* r, int Hh, int Ww, double rf) {
-  const float S = (float)e->cfg.search_size;
-  const float frf = (float)rf;
-  const double cx = (double)((r[0] * S) / frf), cy = (double)((r[1] * S) / frf);
-  const double w = (double)((r[2] * S) / frf), h = (double)((r[3] * S) / frf);
-  auto& st = e->state[slot];
-  const double cx_prev = st[0] + 0.5 * st[2], cy_prev = st[1] + 0.5 * st[3];
-  const double half = 0.5 * e->cfg.search_size / rf;
-  const double cxr = cx + (cx_prev - half), cyr = cy + (cy_prev - half);
-  double x1 = cxr - 0.5 * w, y1 = cyr - 0.5 * h, bw = w, bh = h;
-  const double margin = 10;
-  double x2 = x1 + bw, y2 = y1 + bh;
-  x1 = std::min(std::max(0.0, x1), Ww - margin);
-  x2 = std::min(std::max(margin, x2), (double)Ww);
-  y1 = std::min(std::max(0.0, y1), Hh - margin);
-  y2 = std::min(std::max(margin, y2), (double)Hh);
-  bw = std::max(margin, x2 - x1);
-  bh = std::max(margin, y2 - y1);
-  st = {x1, y1, bw, bh};
 }
 
 // One launch over n sequences.  Batches of >= overlap_min sequences run as two independent halves on
@@ -963,6 +963,16 @@ int launch(mmt_engine* e, int b0, int n, const GraphEntry** replayed) {
   return MMT_OK;
 }
 
+// the host copy of slot's state -> its device-resident copy (stream-ordered, synchronous)
+int write_state(mmt_engine* e, int slot) {
+  SeqState st{};
+  for (int k = 0; k < 4; ++k) st.box[k] = e->state[slot][k];
+  st.rf = 1.0;
+  HIPCHECK(e, hipMemcpyAsync(e->state_dev + slot, &st, sizeof(SeqState), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return MMT_OK;
+}
+
 int check_engine(mmt_engine* e) {
   if (!e) return MMT_E_ARG;
   if (!e->finalized) return e->fail(MMT_E_STATE, "engine not finalized (load every state_dict key first)");
@@ -1022,7 +1032,6 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   e->frame_cap.assign(c.max_batch, 0);
   e->state.assign(c.max_batch, {0, 0, 0, 0});
   e->active.assign(c.max_batch, 0);
-  e->last_rf.assign(c.max_batch, 1.0);
   if (alloc_acts(e.get()) != MMT_OK) return MMT_E_HIP;
   *out = e.release();
   return MMT_OK;
@@ -1049,7 +1058,9 @@ void mmt_destroy(mmt_engine* e) {
   if (e->warena) hipFree(e->warena);
   if (e->aarena) hipFree(e->aarena);
   if (e->params_host) hipHostFree(e->params_host);
-  if (e->res_host) hipHostFree(e->res_host);
+  if (e->outs_host) hipHostFree(e->outs_host);
+  for (auto& t : e->ring)
+    if (t.done) hipEventDestroy(t.done);
   if (e->stream) hipStreamDestroy(e->stream);
   if (e->stream2) hipStreamDestroy(e->stream2);
   if (e->fork_ev) hipEventDestroy(e->fork_ev);
@@ -1112,6 +1123,7 @@ int mmt_initialize(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww
   int r = check_engine(e);
   if (r) return r;
   if (slot < 0 || slot >= e->cfg.max_batch || !init_xywh) return e->fail(MMT_E_ARG, "bad slot / box");
+  if (e->unfetched) return e->fail(MMT_E_STATE, "initialize with unfetched frames in flight");
   int x1, y1, cs;
   double rf;
   TRY(geometry(e, init_xywh, e->cfg.template_factor, e->cfg.template_size, &x1, &y1, &cs, &rf));
@@ -1136,46 +1148,87 @@ int mmt_initialize(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww
   HIPCHECK(e, hipGetLastError());
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->state[slot] = {init_xywh[0], init_xywh[1], init_xywh[2], init_xywh[3]};
+  TRY(write_state(e, slot));
   e->active[slot] = 1;
   return MMT_OK;
+}
+
+int mmt_track_batch_submit(mmt_engine* e, int first_slot, int n, const uint8_t* const* frames, const int* Hs,
+                           const int* Ws, int Cc, const int64_t* row_stride, int is_device, int64_t* ticket) {
+  int r = check_engine(e);
+  if (r) return r;
+  if (n <= 0 || first_slot < 0 || first_slot + n > e->cfg.max_batch || !frames || !Hs || !Ws || !row_stride ||
+      !ticket)
+    return e->fail(MMT_E_ARG, "bad batch");
+  auto& t = e->ring[e->next_ticket % kRing];
+  if (t.open) return e->fail(MMT_E_STATE, "too many unfetched frames (fetch before submitting more)");
+  if (e->probe && e->unfetched > 0) return e->fail(MMT_E_STATE, "the timing probe needs fetch before the next submit");
+  CropParam* ph = e->params_host + (size_t)(e->next_ticket % kRing) * e->cfg.max_batch;
+  for (int i = 0; i < n; ++i) {
+    const int slot = first_slot + i;
+    if (!e->active[slot]) return e->fail(MMT_E_STATE, "track() before initialize() on slot " + std::to_string(slot));
+    // with nothing in flight the host copy of the state is current: reject a bad box before any work
+    // (the reference raises before touching its state); in flight, the device flags it per frame
+    if (e->unfetched == 0) {
+      int x1, y1, cs;
+      double rf;
+      TRY(geometry(e, e->state[slot].data(), e->cfg.search_factor, e->cfg.search_size, &x1, &y1, &cs, &rf));
+    }
+    const uint8_t* dev;
+    TRY(stage_frame(e, slot, frames[i], Hs[i], Ws[i], Cc, row_stride[i], is_device, &dev));
+    ph[i] = CropParam{dev, row_stride[i], Hs[i], Ws[i], Cc, 0, 0, 0, 0};   // geometry: crop_geometry()
+  }
+  HIPCHECK(e, hipMemcpyAsync(e->params_dev, ph, n * sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
+  const GraphEntry* replayed = nullptr;
+  TRY(launch(e, first_slot, n, &replayed));
+  TrackOut* oh = e->outs_host + (size_t)(e->next_ticket % kRing) * e->cfg.max_batch;
+  HIPCHECK(e, hipMemcpyAsync(oh, e->out_dev, (size_t)n * sizeof(TrackOut), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipEventRecord(t.done, e->stream));
+  t.id = e->next_ticket++;
+  t.first = first_slot;
+  t.n = n;
+  t.open = true;
+  t.replayed = replayed;
+  ++e->unfetched;
+  *ticket = t.id;
+  e->last_batch = n;
+  return MMT_OK;
+}
+
+int mmt_track_batch_fetch(mmt_engine* e, int64_t ticket, double* out_xywh, float* out_score) {
+  if (!e) return MMT_E_ARG;
+  if (ticket < 0) return e->fail(MMT_E_ARG, "bad ticket");
+  auto& t = e->ring[ticket % kRing];
+  if (!t.open || t.id != ticket) return e->fail(MMT_E_ARG, "unknown or already fetched ticket");
+  HIPCHECK(e, hipSetDevice(e->device));
+  HIPCHECK(e, hipEventSynchronize(t.done));
+  t.open = false;
+  --e->unfetched;
+  if (t.replayed)
+    probe_collect_graph(e, *t.replayed);
+  else
+    probe_collect(e);
+  const TrackOut* oh = e->outs_host + (size_t)(ticket % kRing) * e->cfg.max_batch;
+  int rc = MMT_OK;
+  for (int i = 0; i < t.n; ++i) {
+    const int slot = t.first + i;
+    e->state[slot] = {oh[i].box[0], oh[i].box[1], oh[i].box[2], oh[i].box[3]};
+    if (out_xywh)
+      for (int k = 0; k < 4; ++k) out_xywh[4 * i + k] = oh[i].box[k];
+    if (out_score) out_score[i] = oh[i].score;
+    if (oh[i].err && rc == MMT_OK)
+      rc = e->fail(oh[i].err, oh[i].err == MMT_E_BOX ? "Too small bounding box." : "crop size out of range");
+  }
+  return rc;
 }
 
 int mmt_track_batch(mmt_engine* e, int first_slot, int n, const uint8_t* const* frames, const int* Hs,
                     const int* Ws, int Cc, const int64_t* row_stride, int is_device, double* out_xywh,
                     float* out_score) {
-  int r = check_engine(e);
+  int64_t ticket;
+  int r = mmt_track_batch_submit(e, first_slot, n, frames, Hs, Ws, Cc, row_stride, is_device, &ticket);
   if (r) return r;
-  if (n <= 0 || first_slot < 0 || first_slot + n > e->cfg.max_batch || !frames || !Hs || !Ws || !row_stride)
-    return e->fail(MMT_E_ARG, "bad batch");
-  for (int i = 0; i < n; ++i) {
-    const int slot = first_slot + i;
-    if (!e->active[slot]) return e->fail(MMT_E_STATE, "track() before initialize() on slot " + std::to_string(slot));
-    int x1, y1, cs;
-    double rf;
-    TRY(geometry(e, e->state[slot].data(), e->cfg.search_factor, e->cfg.search_size, &x1, &y1, &cs, &rf));
-    const uint8_t* dev;
-    TRY(stage_frame(e, slot, frames[i], Hs[i], Ws[i], Cc, row_stride[i], is_device, &dev));
-    e->params_host[i] = CropParam{dev, row_stride[i], Hs[i], Ws[i], Cc, x1, y1, cs, 0};
-    e->last_rf[slot] = rf;
-  }
-  HIPCHECK(e, hipMemcpyAsync(e->params_dev, e->params_host, n * sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
-  const GraphEntry* replayed = nullptr;
-  TRY(launch(e, first_slot, n, &replayed));
-  HIPCHECK(e, hipMemcpyAsync(e->res_host, e->res, (size_t)n * 8 * 4, hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));
-  if (replayed)
-    probe_collect_graph(e, *replayed);
-  else
-    probe_collect(e);
-  for (int i = 0; i < n; ++i) {
-    const int slot = first_slot + i;
-    update_state(e, slot, e->res_host + 8 * i, Hs[i], Ws[i], e->last_rf[slot]);
-    if (out_xywh)
-      for (int k = 0; k < 4; ++k) out_xywh[4 * i + k] = e->state[slot][k];
-    if (out_score) out_score[i] = e->res_host[8 * i + 4];
-  }
-  e->last_batch = n;
-  return MMT_OK;
+  return mmt_track_batch_fetch(e, ticket, out_xywh, out_score);
 }
 
 int mmt_track(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride,
@@ -1191,8 +1244,9 @@ int mmt_get_state(const mmt_engine* e, int slot, double out_xywh[4]) {
 
 int mmt_set_state(mmt_engine* e, int slot, const double xywh[4]) {
   if (!e || slot < 0 || slot >= e->cfg.max_batch || !xywh) return MMT_E_ARG;
+  if (e->unfetched) return e->fail(MMT_E_STATE, "set_state with unfetched frames in flight");
   e->state[slot] = {xywh[0], xywh[1], xywh[2], xywh[3]};
-  return MMT_OK;
+  return write_state(e, slot);
 }
 
 int mmt_debug_fetch(mmt_engine* e, const char* what, int bi, void* dst, size_t nbytes) {

@@ -56,6 +56,77 @@ __device__ __forceinline__ float sigmoid_clamp(float x) {
   return fminf(fmaxf(y, 1e-4f), 1.0f - 1e-4f);
 }
 
+// ------------------------------------------------------------------ tracker state on the device
+// No FMA contraction in these two functions (pragma at the top of each body): every product and sum
+// rounds as in the reference's python doubles (and float32 tensor ops where it computes on tensors).
+__device__ __forceinline__ double dmax(double a, double b) { return a < b ? b : a; }   // std::max / python max
+__device__ __forceinline__ double dmin(double a, double b) { return b < a ? b : a; }   // std::min / python min
+
+// processing_utils.py:32-41: crop_sz = ceil(sqrt(w h) factor) ('Too small bounding box.' if < 1),
+// x1 = round(x + w/2 - crop_sz/2) with python's round (half to even)
+__global__ void geometry_kernel(CropParam* params, SeqState* state, int n, double factor, int out_sz) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  SeqState& st = state[i];
+  const double x = st.box[0], y = st.box[1], w = st.box[2], h = st.box[3];
+  const double cs = ceil(sqrt(w * h) * factor);
+  int err = 0;
+  if (!(cs >= 1.0)) err = -5;           // MMT_E_BOX
+  else if (cs > 1e6) err = -1;          // MMT_E_ARG
+  CropParam& p = params[i];
+  if (err) {                            // a harmless crop; the frame's result is discarded
+    p.x1 = p.y1 = 0;
+    p.crop_sz = 1;
+    st.rf = 1.0;
+  } else {
+    p.crop_sz = (int)cs;
+    p.x1 = (int)rint(x + 0.5 * w - cs * 0.5);
+    p.y1 = (int)rint(y + 0.5 * h - cs * 0.5);
+    st.rf = (double)out_sz / cs;
+  }
+  st.err = err;
+}
+
+void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, hipStream_t s) {
+  hipLaunchKernelGGL(geometry_kernel, dim3((n + 63) / 64), dim3(64), 0, s, params, state, n, factor, out_sz);
+}
+
+// vipt.py:84-88 (pred_box * S / resize_factor in float32 tensors, then python floats) + map_box_back
+// + clip_box (box_ops.py:97-106, margin 10)
+__device__ void update_state(const DecodeArgs& a, int b, const float* r) {
+#pragma clang fp contract(off)
+  SeqState& st = a.state[b];
+  TrackOut& o = a.out[b];
+  o.score = r[4];
+  o.err = st.err;
+  if (st.err) {
+    for (int k = 0; k < 4; ++k) o.box[k] = st.box[k];
+    return;
+  }
+  const float S = (float)a.search_size;
+  const float frf = (float)st.rf;
+  const double cx = (double)((r[0] * S) / frf), cy = (double)((r[1] * S) / frf);
+  const double w = (double)((r[2] * S) / frf), h = (double)((r[3] * S) / frf);
+  const double cx_prev = st.box[0] + 0.5 * st.box[2], cy_prev = st.box[1] + 0.5 * st.box[3];
+  const double half = 0.5 * a.search_size / st.rf;
+  const double cxr = cx + (cx_prev - half), cyr = cy + (cy_prev - half);
+  double x1 = cxr - 0.5 * w, y1 = cyr - 0.5 * h;
+  const double margin = 10;
+  double x2 = x1 + w, y2 = y1 + h;
+  const double Ww = a.params[b].W, Hh = a.params[b].H;
+  x1 = dmin(dmax(0.0, x1), Ww - margin);
+  x2 = dmin(dmax(margin, x2), Ww);
+  y1 = dmin(dmax(0.0, y1), Hh - margin);
+  y2 = dmin(dmax(margin, y2), Hh);
+  const double bw = dmax(margin, x2 - x1), bh = dmax(margin, y2 - y1);
+  st.box[0] = x1;
+  st.box[1] = y1;
+  st.box[2] = bw;
+  st.box[3] = bh;
+  for (int k = 0; k < 4; ++k) o.box[k] = st.box[k];
+}
+
 __global__ __launch_bounds__(256) void decode_kernel(const DecodeArgs a) {
   __shared__ float sv[256];
   __shared__ int si[256];
@@ -120,6 +191,7 @@ __global__ __launch_bounds__(256) void decode_kernel(const DecodeArgs a) {
     r[5] = (float)p;
     r[6] = 0.f;
     r[7] = 0.f;
+    if (a.state) update_state(a, b, r);
   }
 }
 

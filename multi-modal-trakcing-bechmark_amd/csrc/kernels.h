@@ -149,6 +149,27 @@ struct CropArgs {
 void crop_patchify(const CropArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- head tail + decode
+// ---------------------------------------------------------------- device-resident tracker state
+// The per-sequence state machine of ViPTTrack.track (vipt.py:64-88) lives on the device, so a
+// sequence's next frame can be enqueued before this frame's box is read back: the crop geometry is
+// derived from the last box on the device (geometry_kernel) and the box back-map + clip_box run in
+// the decode kernel.  Doubles and rounding exactly as the reference's python / tensor mix.
+struct SeqState {                  // one per slot
+  double box[4];                   // self.state [x, y, w, h]
+  double rf;                       // resize_factor of the frame being tracked
+  int err;                         // MMT_E_BOX / MMT_E_ARG of this frame's geometry, else 0
+  int pad_;
+};
+struct TrackOut {                  // one per sequence of a launch (read back by the host)
+  double box[4];                   // 'target_bbox' after this frame (unchanged state on error)
+  float score;                     // 'best_score'
+  int err;                         // 0, or the geometry error of this frame
+  int pad_[2];
+};
+// processing_utils.py:32-41 for the search crop of sequences [0, n): params[i] <- x1, y1, crop_sz of
+// state[i].box (factor, out_sz), state[i].rf <- out_sz / crop_sz, state[i].err <- geometry error
+void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, hipStream_t s);
+
 struct DecodeArgs {
   int B, fs;                       // feature map fs x fs
   const float* h4;                 // [3][B][fs*fs][32]  (ctr, offset, size) conv4 outputs (ReLU'd)
@@ -157,6 +178,11 @@ struct DecodeArgs {
   const float* hann;               // [fs*fs]
   float* res;                      // [B][8]: cx, cy, w, h, score, idx
   float* maps;                     // optional [B][5][fs*fs] (ctr, size w/h, offset x/y)
+  // tracker-state update (vipt.py:84-88, box_ops.py:97-106); null state: result rows only
+  SeqState* state;                 // [B]
+  const CropParam* params;         // [B] frame H / W of this frame
+  TrackOut* out;                   // [B]
+  int search_size;
 };
 void decode(const DecodeArgs& a, hipStream_t s);
 

@@ -71,6 +71,9 @@ SIGNATURES = {
     "mmt_track": (_I, [_P, _I, _P, _I, _I, _I, _I64, _I, ctypes.POINTER(_D), ctypes.POINTER(_F)]),
     "mmt_track_batch": (_I, [_P, _I, _I, ctypes.POINTER(_P), ctypes.POINTER(_I), ctypes.POINTER(_I), _I,
                              ctypes.POINTER(_I64), _I, ctypes.POINTER(_D), ctypes.POINTER(_F)]),
+    "mmt_track_batch_submit": (_I, [_P, _I, _I, ctypes.POINTER(_P), ctypes.POINTER(_I), ctypes.POINTER(_I), _I,
+                                    ctypes.POINTER(_I64), _I, ctypes.POINTER(_I64)]),
+    "mmt_track_batch_fetch": (_I, [_P, _I64, ctypes.POINTER(_D), ctypes.POINTER(_F)]),
     "mmt_get_state": (_I, [_P, _I, ctypes.POINTER(_D)]),
     "mmt_set_state": (_I, [_P, _I, ctypes.POINTER(_D)]),
     "mmt_debug_fetch": (_I, [_P, ctypes.c_char_p, _I, _P, ctypes.c_size_t]),

@@ -119,6 +119,7 @@ class Engine:
         if rc != L.MMT_OK:
             raise TrackerError(f"mmt_create failed ({rc}) for {cfg}")
         self.h = h
+        self._pending = {}
         self.feat_sz = cfg.search_size // 16
         if state_dict is not None:
             self.load_state_dict(state_dict)
@@ -176,6 +177,30 @@ class Engine:
         out = (ctypes.c_double * (4 * n))()
         sc = (ctypes.c_float * n)()
         self._check(self.lib.mmt_track_batch(self.h, first_slot, n, ptrs, Hs, Ws, C, strides, dev, out, sc))
+        return np.array(out[:], dtype=np.float64).reshape(n, 4), np.array(sc[:], dtype=np.float32)
+
+    # -- pipelined frames: the tracker state lives on the device, so frame t+1 of every sequence can be
+    # submitted before frame t's boxes are fetched (include/mmtrack.h, mmt_track_batch_submit)
+    def track_batch_submit(self, first_slot: int, frames) -> int:
+        n = len(frames)
+        args = [_frame_arg(f) for f in frames]
+        ptrs = (ctypes.c_void_p * n)(*[a[1] for a in args])
+        Hs = (ctypes.c_int * n)(*[a[2] for a in args])
+        Ws = (ctypes.c_int * n)(*[a[3] for a in args])
+        strides = (ctypes.c_int64 * n)(*[a[5] for a in args])
+        ticket = ctypes.c_int64()
+        self._check(self.lib.mmt_track_batch_submit(self.h, first_slot, n, ptrs, Hs, Ws, args[0][4], strides,
+                                                    args[0][6], ctypes.byref(ticket)))
+        self._pending[ticket.value] = (n, args)   # keep host frames alive until their copy has run
+        return ticket.value
+
+    def track_batch_fetch(self, ticket: int) -> tuple:
+        if ticket not in self._pending:
+            raise ValueError("unknown or already fetched ticket")
+        n, _ = self._pending.pop(ticket)
+        out = (ctypes.c_double * (4 * n))()
+        sc = (ctypes.c_float * n)()
+        self._check(self.lib.mmt_track_batch_fetch(self.h, ticket, out, sc))
         return np.array(out[:], dtype=np.float64).reshape(n, 4), np.array(sc[:], dtype=np.float32)
 
     def state(self, slot: int):

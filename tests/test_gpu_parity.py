@@ -20,6 +20,7 @@ import pytest
 import torch
 
 from mmtrack_amd import Engine, EngineConfig, synth
+from mmtrack_amd.engine import TrackerError
 from oracle import crop as ocrop
 from oracle import tracker as otracker
 from oracle import vipt as ov
@@ -228,3 +229,39 @@ def test_device_resident_frames(engines):
     eng.initialize(0, dev[0], list(gts[0]))
     devb = [eng.track(0, dev[t])[0] for t in (1, 2)]
     np.testing.assert_allclose(host, devb, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("use_graphs", [False, True])
+def test_pipelined_frames_equal_blocking(use_graphs):
+    """Frames submitted ahead of their fetch (device-resident tracker state: crop geometry and the box
+    back-map run on the GPU) give bit-identical boxes and scores to blocking per-frame calls; the host
+    copy of the state follows the fetches; tickets are checked."""
+    sd = synth.make_state_dict(0, **SHAPES["deep_rgbt"])
+    seqs = [synth.make_frames(90 + i, 6, 360, 480, 6, box=(120.0 + 30 * i, 100.0, 36.0 + 4 * i, 28.0)) for i in
+            range(3)]
+    res = {}
+    for mode in ("sync", "pipe"):
+        eng = Engine(EngineConfig(max_batch=3, use_graphs=use_graphs), sd)
+        for i, (fr, gt) in enumerate(seqs):
+            eng.initialize(i, fr[0], list(gt[0]))
+        out = []
+        if mode == "sync":
+            for t in range(1, 6):
+                out.append(eng.track_batch(0, [seqs[i][0][t] for i in range(3)]))
+        else:
+            tickets = [eng.track_batch_submit(0, [seqs[i][0][t] for i in range(3)]) for t in range(1, 4)]
+            with pytest.raises(TrackerError):                    # initialize needs nothing in flight
+                eng.initialize(0, seqs[0][0][0], list(seqs[0][1][0]))
+            out.append(eng.track_batch_fetch(tickets[0]))
+            tickets.append(eng.track_batch_submit(0, [seqs[i][0][4] for i in range(3)]))
+            for tk in tickets[1:]:
+                out.append(eng.track_batch_fetch(tk))
+            with pytest.raises(ValueError):                      # already fetched
+                eng.track_batch_fetch(tickets[0])
+            out.append(eng.track_batch(0, [seqs[i][0][5] for i in range(3)]))
+        res[mode] = (np.stack([o[0] for o in out]), np.stack([o[1] for o in out]),
+                     np.array([eng.state(i) for i in range(3)]))
+        eng.close()
+    for a, b in zip(res["sync"], res["pipe"]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(res["pipe"][2], res["pipe"][0][-1])

@@ -110,14 +110,13 @@ def test_gelu_bf16out_accuracy():
     import math
     f = np.float32
     x = np.concatenate([np.linspace(-12, 12, 20001), np.random.default_rng(1).normal(0, 1.5, 50000)]).astype(np.float32)
-    u = np.abs(x) * f(0.70710678118654752440)
-    t = f(1) / (f(0.3275911) * u + f(1))
+    a = np.abs(x)
+    t = f(1) / (f(0.2316418917) * a + f(1))
     p = f(0.5307027145)
     for c in (-0.7265760135, 0.7107068705, -0.142248368, 0.127414796):
         p = p * t + f(c)
-    h = t * p * np.exp2(-(u * f(1.44269504)) * u).astype(np.float32)
-    xh = x * h
-    y = np.where(x >= 0, x - xh, xh)
+    e = np.exp2((x * f(-0.7213475204)) * x).astype(np.float32)
+    y = (np.maximum(x, f(0)).astype(np.float64) - a.astype(np.float64) * ((p * t) * e)).astype(np.float32)  # fma
     ref = np.array([0.5 * v * (1 + math.erf(v / math.sqrt(2))) for v in x.astype(np.float64)])
     assert (np.abs(y - ref) <= 5e-7 * np.maximum(1.0, np.abs(x))).all()
 
