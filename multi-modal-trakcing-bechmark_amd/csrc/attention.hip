@@ -24,12 +24,16 @@ typedef __attribute__((address_space(3))) bf16x4* lds_bf16x4_t;
 
 constexpr int KB = 64;         // keys per LDS tile
 constexpr int CE_MAX = 1024;   // max tokens for the exported CE row
+// bf16 kernels of 4+ waves: ask for 4 waves per SIMD (114 VGPRs instead of 128 + 16 AGPRs -> 3 waves)
+#ifndef ATTN_WPE
+#define ATTN_WPE 4
+#endif
 
 // byte offset of 16-B chunk c of row r in a [64][64] bf16 tile (128-B rows, chunk XOR row)
 __device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 
 template <int WAVES, bool SPLIT, int RB = 1>
-__global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((SPLIT || WAVES < 4) ? 1 : ATTN_WPE))) void attn_kernel(const AttnArgs a) {
   // SPLIT (fp32-faithful): every operand is an (hi, lo) bf16 pair and each product is
   // hi*hi + lo*hi + hi*lo; the LDS images of K and V^T are held for both halves.
   // RB: 16-query row blocks per wave, multiplied together against each K / V fragment (fragment
@@ -66,10 +70,15 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bf16_t* bb = hl ? base_lo : base;
-        if (qi < N)
-          qf[rb][hl][s] = *reinterpret_cast<const bf16x8*>(bb + (int64_t)qi * C3 + h * 64 + 32 * s + 8 * g);
-        else
+        if (qi < N) {
+          // the softmax scale 64^-0.5 = 2^-3 folded into Q: exact in bf16, and MFMA products and sums
+          // commute with a power-of-two scale, so S = K (Q / 8)^T is the scaled score bit for bit
+          const bf16x8 qv = *reinterpret_cast<const bf16x8*>(bb + (int64_t)qi * C3 + h * 64 + 32 * s + 8 * g);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) qf[rb][hl][s][e] = (__bf16)((float)qv[e] * 0.125f);
+        } else {
           qf[rb][hl][s] = bf16x8{};
+        }
       }
   }
 
@@ -143,20 +152,23 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
       }
     }
     bf16x8 pf[RB][2], pl[RB][2];
+    const bool tail = kb + KB > N;   // only the last key tile has keys past N (wave-uniform)
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       float bmax = -INFINITY;
+      if (tail) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (kb + 16 * t + 4 * g + r >= N) sc[rb][t][r] = -INFINITY;
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kb + 16 * t + 4 * g + r;
-          const float v = key < N ? sc[rb][t][r] * 0.125f : -INFINITY;
-          sc[rb][t][r] = v;
-          bmax = fmaxf(bmax, v);
-        }
-      bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
-      bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+        for (int r = 0; r < 4; ++r) bmax = fmaxf(bmax, sc[rb][t][r]);
+      bmax = xmax16(bmax);   // xor 16, xor 32 by permlane half-exchanges (no LDS round trip)
+      bmax = xmax32(bmax);
       if (ce_lane && rb == ce_rb) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -168,17 +180,19 @@ __global__ __launch_bounds__(WAVES * 64) void attn_kernel(const AttnArgs a) {
       }
       const float mnew = fmaxf(m[rb], bmax);
       const float alpha = __expf(m[rb] - mnew);
+      // p = e^(s - m) = 2^(s log2e - m log2e): one FMA + v_exp_f32 per score
+      const float ml2 = mnew * 1.44269504f;
       float psum = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = __expf(sc[rb][t][r] - mnew);
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[rb][t][r], 1.44269504f, -ml2));
           sc[rb][t][r] = p;
           psum += p;
         }
-      psum += __shfl_xor(psum, 16, 64);
-      psum += __shfl_xor(psum, 32, 64);
+      psum = xsum16(psum, psum);
+      psum = xsum32(psum, psum);
       l[rb] = l[rb] * alpha + psum;
       m[rb] = mnew;
 #pragma unroll

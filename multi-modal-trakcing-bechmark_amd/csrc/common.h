@@ -16,15 +16,57 @@ __device__ __forceinline__ float bf2f(bf16_t x) {
   return __uint_as_float(((uint32_t)x) << 16);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+// ---- cross-lane butterflies without the LDS.  __shfl_xor lowers to ds_bpermute_b32 (an LDS round trip
+// per step, serialised along a reduction); these use v_permlane32_swap / v_permlane16_swap across the
+// 32- and 16-lane halves and DPP inside a 16-lane row (row_ror:8 is xor 8; once bit 3 is uniform,
+// row_ror:4 reads the xor-4 partner's value; quad_perm gives xor 2 / xor 1).  Every step adds or maxes
+// a lane's own value with its xor partner's, in the order 32, 16, 8, 4, 2, 1, so the results are bit for
+// bit those of the __shfl_xor butterfly.
+__device__ __forceinline__ uint32_t f2u(float v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ float u2f(uint32_t v) { return __builtin_bit_cast(float, v); }
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128 };
+// (x, y) -> lanes < 32 get x[l] + x[l+32] (or x's partner), lanes >= 32 the same for y: the half-exchange
+// of v_permlane32_swap (vdst x: its upper half swaps with the lower half of y)
+__device__ __forceinline__ float xsum32(float x, float y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(f2u(x), f2u(y), false, false);
+  return u2f(r[0]) + u2f(r[1]);
+}
+// rows of 16 lanes: rows 0 / 2 get x[l] + x[l^16], rows 1 / 3 get y[l] + y[l^16]
+__device__ __forceinline__ float xsum16(float x, float y) {
+  const auto r = __builtin_amdgcn_permlane16_swap(f2u(x), f2u(y), false, false);
+  return u2f(r[0]) + u2f(r[1]);
+}
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(f2u(v), f2u(v), false, false);
+  return fmaxf(u2f(r[0]), u2f(r[1]));
+}
+__device__ __forceinline__ float xmax16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(f2u(v), f2u(v), false, false);
+  return fmaxf(u2f(r[0]), u2f(r[1]));
+}
+__device__ __forceinline__ float row16_sum(float v) {   // xor 8, 4, 2, 1 inside each 16-lane row
+  v += dpp<DPP_ROR8>(v);
+  v += dpp<DPP_ROR4>(v);
+  v += dpp<DPP_XOR2>(v);
+  v += dpp<DPP_XOR1>(v);
   return v;
 }
+__device__ __forceinline__ float wave_sum(float v) {
+  v = xsum32(v, v);
+  v = xsum16(v, v);
+  return row16_sum(v);
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = xmax32(v);
+  v = xmax16(v);
+  v = fmaxf(v, dpp<DPP_ROR8>(v));
+  v = fmaxf(v, dpp<DPP_ROR4>(v));
+  v = fmaxf(v, dpp<DPP_XOR2>(v));
+  return fmaxf(v, dpp<DPP_XOR1>(v));
 }
 
 // Exact-erf GELU (nn.GELU default; vit_ce_prompt.py:122), GELU(x) = x * (1 - h) for x >= 0 and x * h for

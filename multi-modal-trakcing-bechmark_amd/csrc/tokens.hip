@@ -128,30 +128,23 @@ void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16,
 // dot products are reduced with a transposing butterfly (10 shuffles instead of 8 x 6).
 constexpr int PR_ROWS = 4;
 
-// out[c] (valid in lane c for c < 8) = sum over the wave of part[c]
+// out[c] (valid in lane c for c < 8) = sum over the wave of part[c]: a transposing butterfly, the
+// 32 / 16-lane stages as permlane half-exchanges, the rest DPP (one ds_bpermute for the final gather)
 __device__ __forceinline__ float reduce8(float (&part)[8], int lane) {
-  // stage xor 32: lanes < 32 keep channels 0-3, others 4-7
+  // stage 32: lanes < 32 keep channels 0-3, others 4-7
   float v4[4];
-  const bool hi32 = lane & 32;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float send = hi32 ? part[i] : part[i + 4];
-    const float keep = hi32 ? part[i + 4] : part[i];
-    v4[i] = keep + __shfl_xor(send, 32, 64);
-  }
+  for (int i = 0; i < 4; ++i) v4[i] = xsum32(part[i], part[i + 4]);
+  // stage 16: rows 0 / 2 keep the lower pair, rows 1 / 3 the upper
   float v2[2];
-  const bool hi16 = lane & 16;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const float send = hi16 ? v4[i] : v4[i + 2];
-    const float keep = hi16 ? v4[i + 2] : v4[i];
-    v2[i] = keep + __shfl_xor(send, 16, 64);
-  }
+  for (int i = 0; i < 2; ++i) v2[i] = xsum16(v4[i], v4[i + 2]);
   const bool hi8 = lane & 8;
-  float v1 = (hi8 ? v2[1] : v2[0]) + __shfl_xor(hi8 ? v2[0] : v2[1], 8, 64);
-  v1 += __shfl_xor(v1, 4, 64);
-  v1 += __shfl_xor(v1, 2, 64);
-  v1 += __shfl_xor(v1, 1, 64);
+  float v1 = (hi8 ? v2[1] : v2[0]) + dpp<DPP_ROR8>(hi8 ? v2[0] : v2[1]);
+  // the 8 lanes of a channel: xor 1, xor 2 (quad_perm), then the quads' sums meet by row_half_mirror
+  v1 += dpp<DPP_XOR1>(v1);
+  v1 += dpp<DPP_XOR2>(v1);
+  v1 += dpp<0x141>(v1);
   // lane holds channel ((lane>>5)&1)*4 + ((lane>>4)&1)*2 + ((lane>>3)&1); gather to lane c
   const int c = lane & 7;
   const int src = ((c >> 2) & 1) * 32 + ((c >> 1) & 1) * 16 + (c & 1) * 8;
@@ -223,7 +216,7 @@ constexpr int TOK_THREADS = 512;   // 8 waves per block share one LDS copy of th
 
 struct DeepIn {
   Row12 x;
-  float4 s0, s1;
+  float sp, sq;   // s8[lane & 7], s8[lane >> 3] of the row: the lane's term of the LN_B variance form
 };
 
 // compact position of slot row `row` (-1: pruned search slot)
@@ -239,9 +232,9 @@ __device__ __forceinline__ DeepIn deep_fetch(const PromptArgs& a, int row, int p
   // in-order vmcnt waits count exactly the loads issued
   d.x = load_row(a.srcA + ((int64_t)b * a.srcA_rows + max(pos, 0)) * C768, lane);
   if (pos < 0) d.x = zero_row();
-  const float4* sp = reinterpret_cast<const float4*>(a.s8 + (int64_t)row * 8);
-  d.s0 = sp[0];
-  d.s1 = sp[1];
+  const float* sp = a.s8 + (int64_t)row * 8;
+  d.sp = sp[lane & 7];
+  d.sq = sp[lane >> 3];
   return d;
 }
 
@@ -265,45 +258,43 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const int rj = min(r0 + j * nw, rows - 1);
-    in[j] = deep_fetch(a, rj, __shfl(posv, j, 64), L, lane);
+    in[j] = deep_fetch(a, rj, __builtin_amdgcn_readlane(posv, j), L, lane);
   }
 #pragma unroll
   for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[threadIdx.x + TOK_THREADS * k] = wst[k];
   if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
   __syncthreads();
   const int kk = lane & 7;
+  // the lane's coefficients of the LN_B variance form: G[q][p] s_p s_q (+ 2 g_q s_q for p = 0, + gb in lane 0)
+  const float vG = fold[FOLD_G + lane], vg = kk == 0 ? 2.f * fold[FOLD_g + (lane >> 3)] : 0.f;
+  const float vb = lane == 0 ? fold[FOLD_gb] : 0.f;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const int row = r0 + j * nw;
     if (row >= rows) break;
-    const Row12 y = ln_hat(in[j].x);   // LN_A's affine is folded into w00 / b00 (engine pack_weights)
-    float part[8];
+    float ra = 0.f;   // a pruned slot is a zero row: its LN is 0 and a8 = b00 exactly
+    if (__builtin_amdgcn_readlane(posv, j) >= 0) {   // wave-uniform
+      const Row12 y = ln_hat(in[j].x);   // LN_A's affine is folded into w00 / b00 (engine pack_weights)
+      float part[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float t = 0.f;
+      for (int k = 0; k < 8; ++k) {
+        float t = 0.f;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const float4 w = reinterpret_cast<const float4*>(W0 + k * C768)[lane + 64 * i];
-        t += y.v[i].x * w.x + y.v[i].y * w.y + y.v[i].z * w.z + y.v[i].w * w.w;
+        for (int i = 0; i < 3; ++i) {
+          const float4 w = reinterpret_cast<const float4*>(W0 + k * C768)[lane + 64 * i];
+          t += y.v[i].x * w.x + y.v[i].y * w.y + y.v[i].z * w.z + y.v[i].w * w.w;
+        }
+        part[k] = t;
       }
-      part[k] = t;
+      ra = reduce8(part, lane);
     }
-    const float ra = reduce8(part, lane);
-    // c8 from the previous prompt's s8
-    const float sv[8] = {in[j].s0.x, in[j].s0.y, in[j].s0.z, in[j].s0.w,
-                         in[j].s1.x, in[j].s1.y, in[j].s1.z, in[j].s1.w};
-    float var = fold[FOLD_gb];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float gj = 2.f * fold[FOLD_g + q];
-#pragma unroll
-      for (int l = 0; l < 8; ++l) gj += fold[FOLD_G + q * 8 + l] * sv[l];
-      var += gj * sv[q];
-    }
+    // c8 from the previous prompt's s8: var = s^T G s + 2 g.s + gb, one (q, p) term per lane
+    const float var = wave_sum(fmaf(fmaf(vG, in[j].sp, vg), in[j].sq, vb));
     const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + LN_EPS);
+    // lane kk < 8: mk = mc[kk] + MC[kk][:] . s   (s[q] is lane 8q's sq)
     float mk = fold[FOLD_mc + kk];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) mk += fold[FOLD_MC + kk * 8 + q] * sv[q];
+    for (int q = 0; q < 8; ++q) mk += fold[FOLD_MC + kk * 8 + q] * u2f(__builtin_amdgcn_readlane(f2u(in[j].sq), 8 * q));
     const float rb = rstd * mk + fold[FOLD_cb + kk];
     if (lane < 8) {
       a.a8[(int64_t)row * 8 + lane] = ra + ba;
@@ -367,9 +358,9 @@ __global__ __launch_bounds__(256) void fovea_kernel(const PromptArgs a) {
   const int c = tid & 7, stripe = tid >> 3;
   float mx = -INFINITY;
   for (int t = stripe; t < n; t += 32) mx = fmaxf(mx, va[t * 8 + c] * sm);
-  mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = fmaxf(mx, dpp<DPP_ROR8>(mx));
+  mx = xmax16(mx);
+  mx = xmax32(mx);
   if ((tid & 63) < 8) red[(tid >> 6) * 8 + c] = mx;
   __syncthreads();
   if (tid < 8) smax[tid] = fmaxf(fmaxf(red[tid], red[8 + tid]), fmaxf(red[16 + tid], red[24 + tid]));
@@ -377,9 +368,9 @@ __global__ __launch_bounds__(256) void fovea_kernel(const PromptArgs a) {
   const float cm = smax[c];
   float sum = 0.f;
   for (int t = stripe; t < n; t += 32) sum += __expf(va[t * 8 + c] * sm - cm);
-  sum += __shfl_xor(sum, 8, 64);
-  sum += __shfl_xor(sum, 16, 64);
-  sum += __shfl_xor(sum, 32, 64);
+  sum += dpp<DPP_ROR8>(sum);
+  sum = xsum16(sum, sum);
+  sum = xsum32(sum, sum);
   __syncthreads();
   if ((tid & 63) < 8) red[(tid >> 6) * 8 + c] = sum;
   __syncthreads();
@@ -461,7 +452,7 @@ __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptAr
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const int rj = min(r0 + j * nw, a.rows - 1);
-    in[j] = lnp_fetch<MODE>(a, rj, __shfl(slotv, j, 64), lane);
+    in[j] = lnp_fetch<MODE>(a, rj, __builtin_amdgcn_readlane(slotv, j), lane);
   }
 #pragma unroll
   for (int k = 0; k < WE; ++k) {

@@ -192,6 +192,16 @@ def test_attention(lib, B, N):
     torch.testing.assert_close(prob, attn[:, :, ceq, lens_t:], rtol=1e-4, atol=1e-6)
 
 
+def test_xlane_reductions_bitwise():
+    """common.h's permlane / DPP wave reductions equal the __shfl_xor butterfly bit for bit (built by build())."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "bin", "xlane_check")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_layernorm(lib):
     g = torch.Generator(device="cuda").manual_seed(9)
     x = torch.randn(333, 768, device="cuda", generator=g) * 3 + 1

@@ -124,7 +124,7 @@ def test_network_bf16_statistics(engines, name):
     ocfg = ov.NetCfg(kind=SHAPES[name]["kind"], prompt_type=SHAPES[name].get("prompt_type", "vipt_deep"),
                      search_size=cfg.search_size, template_size=cfg.template_size)
     agree, ious = 0, []
-    n = 12
+    n = int(os.environ.get("MMT_STAT_N", "32"))   # 12 samples measured too noisy for the thresholds
     for j in range(n):
         zp = synth.make_patch(500 + j, cfg.template_size, cfg.in_chans)
         xp = synth.make_patch(600 + j, cfg.search_size, cfg.in_chans)
