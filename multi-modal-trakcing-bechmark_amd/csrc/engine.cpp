@@ -325,7 +325,13 @@ int pack_weights(mmt_engine* e) {
     TRY(upload_f32(e, &w.b00, H(e, p + "conv0_0.bias")));
     TRY(upload_f32(e, &w.w01, H(e, p + "conv0_1.weight")));
     TRY(upload_f32(e, &w.b01, H(e, p + "conv0_1.bias")));
-    TRY(upload_f32(e, &w.w1, H(e, p + "conv1x1.weight")));
+    {   // conv1x1 [768][8] stored channel-major [8][768]: the LN1 kernel's LDS image is a straight copy
+      const auto& v = H(e, p + "conv1x1.weight");
+      std::vector<float> t(v.size());
+      for (size_t c = 0; c < (size_t)C; ++c)
+        for (size_t k = 0; k < 8; ++k) t[k * C + c] = v[c * 8 + k];
+      TRY(upload_f32(e, &w.w1, t));
+    }
     TRY(upload_f32(e, &w.b1, H(e, p + "conv1x1.bias")));
     w.smooth = H(e, p + "fovea.smooth")[0];
     TRY(upload_f32(e, &w.nw, H(e, "backbone.prompt_norms." + std::to_string(i) + ".weight")));

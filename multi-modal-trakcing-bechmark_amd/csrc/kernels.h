@@ -100,7 +100,7 @@ struct LnPromptArgs {
   int rows, rows_per_seq, Lz, Lx;
   float* X;
   const float* s8;           // [B][Lz+Lx][8] fovea output of every slot (PromptArgs::s8)
-  const float* w1; const float* b1;         // conv1x1 [768][8] -> the prompt P = w1 s8 + b1
+  const float* w1; const float* b1;         // conv1x1 channel-major [8][768] -> the prompt P = w1^T s8 + b1
   const float* tok_rgb;      // mode 1
   const float* pos;          // mode 1: [Lz+Lx][768]
   const int* gidx;           // mode 2: [B][rows_per_seq - Lz] slot of each compact search token

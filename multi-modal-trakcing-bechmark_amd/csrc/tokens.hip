@@ -438,10 +438,10 @@ __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptAr
   const int r0 = blockIdx.x * (TOK_THREADS / 64) + (threadIdx.x >> 6);
   const int pr = r0 + lane * nw;
   const int slotv = (lane < R && pr < a.rows) ? lnp_slot<MODE>(a, pr) : 0;
-  constexpr int WE = 8 * C768 / TOK_THREADS;   // 12 conv1x1 elements per thread
-  float wst[WE];
+  constexpr int WE = 8 * C768 / 4 / TOK_THREADS;   // 3 float4 of conv1x1 (channel-major, a.w1 = W1t) per thread
+  float4 wst[WE];
 #pragma unroll
-  for (int k = 0; k < WE; ++k) wst[k] = a.w1[threadIdx.x + TOK_THREADS * k];
+  for (int k = 0; k < WE; ++k) wst[k] = reinterpret_cast<const float4*>(a.w1)[threadIdx.x + TOK_THREADS * k];
   float cs[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -455,10 +455,7 @@ __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptAr
     in[j] = lnp_fetch<MODE>(a, rj, __builtin_amdgcn_readlane(slotv, j), lane);
   }
 #pragma unroll
-  for (int k = 0; k < WE; ++k) {
-    const int e = threadIdx.x + TOK_THREADS * k;
-    W1t[(e & 7) * C768 + (e >> 3)] = wst[k];
-  }
+  for (int k = 0; k < WE; ++k) reinterpret_cast<float4*>(W1t)[threadIdx.x + TOK_THREADS * k] = wst[k];
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     const int e = threadIdx.x + TOK_THREADS * k;
@@ -526,36 +523,53 @@ __device__ __forceinline__ bool before(float ka, int va, float kb, int vb) {
 // Rank selection instead of a sort network: every search token's position in the descending order
 // (ties -> lower index, the order "before" defines) is the number of tokens before it, counted in
 // one parallel pass over LDS (Ls <= 1024), so there is a single barrier instead of log^2 stages.
-__global__ __launch_bounds__(512) void ce_select_kernel(const CEArgs a) {
+// Four threads per search token (a quad) each count a quarter of the keys and the quad's counts meet
+// by DPP, so the serial LDS scan is Ls / 4 long; the 12 head rows of a token are requested together.
+constexpr int CE_THREADS = 1024, CE_MAX_HEADS = 16;
+__global__ __launch_bounds__(CE_THREADS) void ce_select_kernel(const CEArgs a) {
   __shared__ float key[1024];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float* prob = a.prob + (int64_t)b * a.heads * a.Ls;
-  for (int i = tid; i < a.Ls; i += 512) {
+  for (int i = tid; i < a.Ls; i += CE_THREADS) {
+    float v[CE_MAX_HEADS];
+#pragma unroll
+    for (int h = 0; h < CE_MAX_HEADS; ++h) v[h] = h < a.heads ? prob[h * a.Ls + i] : 0.f;
     float s = 0.f;
-    for (int h = 0; h < a.heads; ++h) s += prob[h * a.Ls + i];
+#pragma unroll
+    for (int h = 0; h < CE_MAX_HEADS; ++h)
+      if (h < a.heads) s += v[h];   // head order 0, 1, ... as before
+    for (int h = CE_MAX_HEADS; h < a.heads; ++h) s += prob[h * a.Ls + i];
     key[i] = s / (float)a.heads;
   }
   __syncthreads();
   const int Ln = a.Lz + a.keep;
-  for (int i = tid; i < a.Ls; i += 512) {
-    const float ki = key[i];
+  const int q = tid & 3, nq = (a.Ls + 3) / 4;   // the quad member's key range [q nq, (q + 1) nq)
+  for (int i0 = 0; i0 < a.Ls; i0 += CE_THREADS / 4) {
+    const int i = i0 + (tid >> 2);   // quad-uniform
+    const int ic = min(i, a.Ls - 1);
+    const float ki = key[ic];
     int rank = 0;
-    for (int j = 0; j < a.Ls; ++j) rank += before(key[j], j, ki, i) ? 1 : 0;
-    const int slot = a.gidx_in[b * a.Ls + i];
-    if (rank < a.keep) {
-      a.gidx_out[b * a.keep + rank] = slot;
-      a.gather[b * Ln + a.Lz + rank] = a.Lz + i;
-      a.slot2pos[b * a.Lx + slot] = a.Lz + rank;
-    } else {
-      a.removed[b * a.Lx + a.removed_off + (rank - a.keep)] = slot;
-      a.slot2pos[b * a.Lx + slot] = -1;
+    const int j1 = min((q + 1) * nq, a.Ls);
+    for (int j = q * nq; j < j1; ++j) rank += before(key[j], j, ki, ic) ? 1 : 0;
+    rank += __builtin_bit_cast(int, dpp<DPP_XOR1>(__builtin_bit_cast(float, rank))) ;
+    rank += __builtin_bit_cast(int, dpp<DPP_XOR2>(__builtin_bit_cast(float, rank)));
+    if (q == 0 && i < a.Ls) {
+      const int slot = a.gidx_in[b * a.Ls + i];
+      if (rank < a.keep) {
+        a.gidx_out[b * a.keep + rank] = slot;
+        a.gather[b * Ln + a.Lz + rank] = a.Lz + i;
+        a.slot2pos[b * a.Lx + slot] = a.Lz + rank;
+      } else {
+        a.removed[b * a.Lx + a.removed_off + (rank - a.keep)] = slot;
+        a.slot2pos[b * a.Lx + slot] = -1;
+      }
     }
   }
-  for (int t = tid; t < a.Lz; t += 512) a.gather[b * Ln + t] = t;
+  for (int t = tid; t < a.Lz; t += CE_THREADS) a.gather[b * Ln + t] = t;
 }
 
 void ce_select(const CEArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(ce_select_kernel, dim3(a.B), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(ce_select_kernel, dim3(a.B), dim3(CE_THREADS), 0, s, a);
 }
 
 __global__ void init_indices_kernel(int* gidx, int* slot2pos, int B, int Lz, int Lx) {
