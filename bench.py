@@ -1,4 +1,4 @@
-"""Headline benchmark: tracked frames/sec/GPU, ViPT-deep ViT-B, 128^2 template / 256^2 search, bf16.
+"""Headline benchmark: tracked frames/sec/GPU, ViPT-deep ViT-B, 128^2 template / 256^2 search.
 
 One "step" = one tracking step of B independent sequences on each GPU (mmt_track_batch_submit +
 _fetch, frames pipelined LAG deep; --sync: blocking mmt_track_batch): crop geometry from the last box +
@@ -7,14 +7,22 @@ CENTER head, windowed argmax decode, box back-mapping.  Frames are synthetic 640
 (RGB + thermal-like aux) already resident in HBM; weights are the seeded synthetic law of
 mmtrack_amd.synth (no checkpoint ships with the reference).
 
-Multi-GPU: one process per GPU (torchrun), sequences sharded per rank, no data-path collective
-(the reference shards sequences over a Pool, test_rgbt_mgpus.py:180-184); a gloo barrier and a
-max-over-ranks of the timed region only.
+Precision (--precision): "fp32" (default) is the parity mode -- every MFMA product split into bf16
+hi/lo halves (hi*hi + lo*hi + hi*lo, "bf16x3"), which reproduces the fp32 reference's candidate-
+elimination decisions and windowed argmax (tests/test_gpu_parity.py); "bf16" is plain bf16 operands,
+faster, but its CE decisions flip against the reference.
+
+Multi-GPU: one process per GPU, sequences sharded per rank, no data-path collective (the reference
+shards sequences over a Pool, test_rgbt_mgpus.py:180-184); a gloo barrier and a max-over-ranks of the
+timed region only.  `--gpus N` without a torchrun environment spawns the N rank processes itself
+(before anything touches a GPU); under torchrun WORLD_SIZE must equal --gpus.
 """
 import argparse
 import collections
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,6 +37,7 @@ import torch  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0
 LAG = 2   # frames a sequence may have in flight ahead of its fetched boxes (pipelined mode)
+METRIC = "tracked frames/sec/GPU, ViPT ViT-B 256² search bf16, at 1/2/4/8 MI355X"
 
 WORKLOADS = {
     # name: (engine kwargs, synth shape kwargs, frame H, W, C, published-config description)
@@ -41,64 +50,161 @@ WORKLOADS = {
                    "OSTrack RGB ViT-B, template 192 / search 384 (BASELINE configs[3])"),
 }
 GFLOP_PER_FRAME = {"vipt_deep_rgbt": 45.80, "vipt_deep_rgbd": 45.80, "ostrack384": 109.34}
+PROBE_CLASSES = ("qkv", "proj", "fc1", "fc2", "attn", "conv1", "patch")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(workload, frames_np, gts, seconds=12.0):
-    """The fp32 CPU oracle tracker (oracle/tracker.py) on the same synthetic frames, bounded sample."""
+def cpu_quota():
+    """CPUs this process may use: the cgroup quota (the GPU box's share) capped by the affinity mask."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(workload, frames_np, gts, seconds=4.0):
+    """The fp32 CPU oracle tracker (oracle/tracker.py) on the same synthetic frames, bounded samples:
+    full track (crop + network + decode) and network only, at the box's CPU share and at 1 thread."""
     from mmtrack_amd import synth
+    from oracle import crop as ocrop
     from oracle import tracker as otracker
     from oracle import vipt as ov
     ekw, skw, H, W, C, _ = WORKLOADS[workload]
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
     sd = synth.make_state_dict(0, **skw)
     cfg = ov.NetCfg(kind=skw["kind"], prompt_type=skw.get("prompt_type", "vipt_deep"),
                     search_size=skw.get("search_size", 256), template_size=skw.get("template_size", 128))
-    tr = otracker.OracleTracker(sd, cfg, search_factor=ekw.get("search_factor", 4.0))
-    tr.initialize(frames_np[0], {"init_bbox": list(gts[0])})
-    tr.track(frames_np[1])  # warm
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        tr.track(frames_np[2 + n % (len(frames_np) - 2)])
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frames of one sequence through the fp32 CPU oracle tracker "
-                      f"(crop+net+decode, torch {threads} threads, {dt:.1f}s)"}
+    quota = cpu_quota()
+    variants = []
+    for threads in (quota, 1):
+        torch.set_num_threads(threads)
+        tr = otracker.OracleTracker(sd, cfg, search_factor=ekw.get("search_factor", 4.0))
+        tr.initialize(frames_np[0], {"init_bbox": list(gts[0])})
+        tr.track(frames_np[1])  # warm
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            tr.track(frames_np[2 + n % (len(frames_np) - 2)])
+            n += 1
+        dt = time.perf_counter() - t0
+        variants.append({"part": "track", "threads": threads, "value": round(n / dt, 3), "frames": n,
+                         "seconds": round(dt, 2)})
+        # network only: the oracle forward on a fixed pre-cropped pair
+        z = ocrop.preprocess(synth.make_patch(1, cfg.template_size, C))
+        x = ocrop.preprocess(synth.make_patch(2, cfg.search_size, C))
+        mask = ov.ce_template_mask(cfg)
+        ov.forward(sd, z, x, cfg, mask)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            ov.forward(sd, z, x, cfg, mask)
+            n += 1
+        dt = time.perf_counter() - t0
+        variants.append({"part": "network", "threads": threads, "value": round(n / dt, 3), "frames": n,
+                         "seconds": round(dt, 2)})
+    head = variants[0]
+    return {"value": head["value"], "unit": "frames/s", "cores": quota, "kind": "port",
+            "machine_cpus": os.cpu_count(), "variants": variants,
+            "sample": f"{head['frames']} frames of one sequence through the fp32 CPU oracle tracker (crop + "
+                      f"network + decode, {quota} torch threads = the box's CPU share, {head['seconds']} s); "
+                      f"'variants' adds network-only and 1-thread samples of ~{seconds:.0f} s each"}
 
 
-def pmc_traffic(probe, path=None):
+def pmc_traffic(cls, precision, path=None):
     """HBM bytes per launch of the probed kernel class from the committed PMC summary
     (tests/pmc_bench.sh + tests/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes)."""
     import glob
-    import re
-    epi = {"fc1": 1, "qkv": 0, "fc2": 2, "proj": 2}.get(probe)
-    files = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")))
-    if epi is None or not files or not os.path.exists(files[-1]):
+    pat = f"*pmc_traffic_{precision}*.json"
+    files = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", pat)))
+    if not files or not os.path.exists(files[-1]):
         return None, None
-    ks = json.load(open(files[-1]))["kernels"]
-    best = None
-    for name, d in ks.items():
-        m = (re.match(r"gemm_kernel<\d+, \d+, \d+, \d+, (\d+), 0, false", name) or re.match(r"gemm256_kernel<(\d+)>", name)
-             or re.match(r"gemm_persist_kernel<\d+, \d+, \d+, \d+, (\d+)>", name))
-        if m and int(m.group(1)) == epi and "traffic_bytes_per_dispatch" in d:
-            if best is None or d["dispatches"] > best[1]["dispatches"]:
-                best = (name, d)
-    if best is None:
+    d = json.load(open(files[-1]))
+    c = d.get("classes", {}).get(cls)
+    if not c or "traffic_bytes_per_dispatch" not in c:
         return None, None
-    return best[1]["traffic_bytes_per_dispatch"], os.path.relpath(files[-1], REPO) + ":" + best[0]
+    return c["traffic_bytes_per_dispatch"], os.path.relpath(files[-1], REPO) + ":" + cls
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """One child process per GPU with the torchrun environment; rank 0 prints the JSON line.  Called
+    before this process touches any GPU (no HIP context to inherit)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
 
 
 def aggregate_throughput(batch, steps, elapsed):
-    """(whole-job frames/s, max-over-ranks elapsed): every rank tracked batch x steps frames."""
+    """(whole-job frames/s, max-over-ranks elapsed, world): every rank tracked batch x steps frames."""
     from mmtrack_amd.sharding import max_over_ranks, rank_world
     _, world = rank_world()
     elapsed = max_over_ranks(elapsed)
-    return world * batch * steps / elapsed, elapsed
+    return world * batch * steps / elapsed, elapsed, world
+
+
+def probe_classes(eng, step, k0, nsteps, precision):
+    """HIP-event timing of every launch of each kernel class on the engine stream (eager replays of the
+    same steps: HIP cannot time event nodes captured in a graph)."""
+    out = {}
+    for cls in PROBE_CLASSES:
+        eng.timing_enable(cls)
+        for k in range(nsteps):
+            step(k0 + k)
+        tr = eng.timing_read()
+        eng.timing_enable(None)
+        if not tr["launches"]:
+            continue
+        avg_ms = tr["total_ms"] / tr["launches"]
+        fl = tr["flops"] / tr["launches"]
+        by = tr["bytes"] / tr["launches"]
+        out[cls] = {"launches": tr["launches"], "avg_launch_us": round(avg_ms * 1e3, 2),
+                    "ms_per_step": round(tr["total_ms"] / nsteps, 4), "flop_per_launch": fl,
+                    "algorithmic_bytes_per_launch": by,
+                    "achieved_tflops": round(fl / (avg_ms * 1e-3) / 1e12, 1),
+                    "achieved_gbs": round(by / (avg_ms * 1e-3) / 1e9, 1)}
+    return out
+
+
+def roofline_from(classes, precision, workload, batch):
+    """The dominant class (most time per step) as the roofline line; every class kept beside it."""
+    if not classes:
+        return None
+    dom = max(classes, key=lambda c: classes[c]["ms_per_step"])
+    c = classes[dom]
+    split = precision == "fp32"
+    # bf16x3: three bf16 MFMAs per product, so the arithmetic's dense peak is the bf16 peak / 3
+    peak = PEAK_BF16_TFLOPS / 3 if split else PEAK_BF16_TFLOPS
+    traffic, src = pmc_traffic(dom, precision) if (batch == 32 and workload == "vipt_deep_rgbt") else (None, None)
+    for k, v in classes.items():
+        v["frac_of_peak"] = round(v["achieved_tflops"] / peak, 4)
+    return {"bound": "mfma", "kernel": dom, "achieved": c["achieved_tflops"], "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(c["achieved_tflops"] / peak, 4),
+            "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (HBM, PMC)",
+            "traffic_source": src, "algorithmic_bytes_per_launch": c["algorithmic_bytes_per_launch"],
+            "avg_launch_us": c["avg_launch_us"], "flop_per_launch": c["flop_per_launch"],
+            "launches": c["launches"],
+            "peak_note": ("bf16x3 split products (hi*hi + lo*hi + hi*lo): dense bf16 2500 TF/s / 3; achieved counts "
+                          "algorithmic 2MNK flops, the MFMA pipe issues 3x that") if split else "dense bf16",
+            "mfma_pipe_frac": round(c["achieved_tflops"] * (3 if split else 1) / PEAK_BF16_TFLOPS, 4),
+            "classes": classes}
 
 
 def main():
@@ -108,27 +214,38 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=32, help="sequences tracked per GPU per step")
     ap.add_argument("--workload", default="vipt_deep_rgbt", choices=list(WORKLOADS))
+    ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16"),
+                    help="fp32: parity mode (bf16x3 split products); bf16: plain bf16 operands")
     ap.add_argument("--frames", type=int, default=8, help="distinct synthetic frames per sequence (cycled)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--sync", action="store_true", help="blocking per-frame calls (no frame pipelining)")
-    ap.add_argument("--probe", default="fc1", help="kernel class timed with HIP events for the roofline ('none': off)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--probe", default="all", help="'all': time every kernel class for the roofline; 'none': off")
+    ap.add_argument("--host-frames", type=int, default=10,
+                    help="steps of an extra PCIe-inclusive pass with frames in pinned host memory (0: off)")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="per CPU-baseline sample (4 samples)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry", action="store_true", help="no GPU: sleep for the step (tests the multi-rank plumbing)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")
+    if args.dry:
+        return dry_main(args, rank, world, dist)
     torch.cuda.set_device(local)
 
     from mmtrack_amd import Engine, EngineConfig, synth
     ekw, skw, H, W, C, desc = WORKLOADS[args.workload]
     B = args.batch
-    cfg = EngineConfig(max_batch=B, use_graphs=not args.no_graphs, **ekw)
+    cfg = EngineConfig(max_batch=B, use_graphs=not args.no_graphs, precision=args.precision, **ekw)
     sd = synth.make_state_dict(0, **skw)
     eng = Engine(cfg, sd, device=local)
 
@@ -142,20 +259,20 @@ def main():
     torch.cuda.synchronize()
     frame_lists = [[video[1 + t]] * B for t in range(args.frames)]
 
-    def step(k):
-        eng.track_batch(0, frame_lists[k % args.frames])
+    def step(k, lists=frame_lists):
+        eng.track_batch(0, lists[k % args.frames])
 
-    def run(k0, count):
+    def run(k0, count, lists=frame_lists):
         """`count` frames of every sequence.  Pipelined (default): the tracker state lives on the device,
         so frame k+1 is submitted before frame k's boxes are fetched (at most LAG frames in flight);
         every frame's boxes reach the host before this returns.  --sync: one blocking call per frame."""
         if args.sync:
             for k in range(k0, k0 + count):
-                step(k)
+                step(k, lists)
             return
         pend = collections.deque()
         for k in range(k0, k0 + count):
-            pend.append(eng.track_batch_submit(0, frame_lists[k % args.frames]))
+            pend.append(eng.track_batch_submit(0, lists[k % args.frames]))
             if len(pend) > LAG:
                 eng.track_batch_fetch(pend.popleft())
         while pend:
@@ -172,27 +289,25 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    value, elapsed = aggregate_throughput(B, args.steps, t1 - t0)
+    value, elapsed, world = aggregate_throughput(B, args.steps, t1 - t0)
 
-    # roofline probe: the same steps again, launched eagerly (HIP cannot time event nodes captured in a
-    # graph), with HIP events on the engine stream around every launch of the dominant kernel class
+    # PCIe-inclusive rate: the same steps with every frame handed over as a host array in pinned memory
+    # (the reference's per-frame call receives a host np.ndarray); copies run on the engine's copy stream
+    host_fps = None
+    if args.host_frames > 0:
+        pinned = [torch.from_numpy(video_np[1 + t]).pin_memory().numpy() for t in range(args.frames)]
+        host_lists = [[pinned[t]] * B for t in range(args.frames)]
+        run(0, 2, host_lists)
+        torch.cuda.synchronize()
+        th = time.perf_counter()
+        run(0, args.host_frames, host_lists)
+        torch.cuda.synchronize()
+        host_fps = B * args.host_frames / (time.perf_counter() - th)
+
     roof = None
     if args.probe and args.probe != "none":
-        eng.timing_enable(args.probe)
-        for k in range(min(args.steps, 20)):
-            step(args.warmup + k)
-        tr = eng.timing_read()
-        eng.timing_enable(None)
-        if tr["launches"]:
-            avg_ms = tr["total_ms"] / tr["launches"]
-            fl = tr["flops"] / tr["launches"]
-            achieved = fl / (avg_ms * 1e-3) / 1e12
-            traffic, src = pmc_traffic(args.probe) if B == 32 and args.workload == "vipt_deep_rgbt" else (None, None)
-            roof = {"bound": "mfma", "kernel": f"gemm[{args.probe}]", "achieved": round(achieved, 1),
-                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                    "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (HBM, PMC)",
-                    "traffic_source": src, "algorithmic_bytes_per_launch": tr["bytes"] / tr["launches"],
-                    "avg_launch_us": round(avg_ms * 1e3, 2), "flop_per_launch": fl, "launches": tr["launches"]}
+        classes = probe_classes(eng, step, args.warmup, min(args.steps, 10), args.precision)
+        roof = roofline_from(classes, args.precision, args.workload, B)
 
     if rank == 0:
         cpu = None
@@ -200,22 +315,48 @@ def main():
             cpu = cpu_baseline(args.workload, video_np, gts, args.cpu_seconds)
         gf = GFLOP_PER_FRAME[args.workload]
         line = {
-            "metric": "tracked frames/sec/GPU, ViPT ViT-B 256² search bf16, at 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16x3" if args.precision == "fp32" else "bf16", "data": "synthetic",
             "config": {"workload": args.workload, "description": desc, "sequences_per_gpu": B,
                        "global_batch": B * world, "frame": f"{W}x{H}x{C} uint8 (HBM-resident)",
                        "template": cfg.template_size, "search": cfg.search_size, "parallelism": f"seq-shard x{world}",
+                       "precision": args.precision, "parity_mode": args.precision == "fp32",
                        "graphs": cfg.use_graphs, "pipelined_frames": 0 if args.sync else LAG,
                        "weights": "synthetic seeded (no checkpoint ships)"},
             "per_gpu_fps": round(value / world, 2),
+            "host_frames_fps_rank0": round(host_fps, 2) if host_fps else None,
             "model_tflops": round(value * gf / 1e3, 1),
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def dry_main(args, rank, world, dist):
+    """The multi-rank plumbing without a GPU: each 'step' sleeps 1 ms per sequence."""
+    def run(n):
+        for _ in range(n):
+            time.sleep(1e-3 * args.batch / 32)
+    run(args.warmup)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run(args.steps)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    value, elapsed, w = aggregate_throughput(args.batch, args.steps, t1 - t0)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": w,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "dry": True,
+                          "config": {"sequences_per_gpu": args.batch, "global_batch": args.batch * w}}), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -113,8 +113,15 @@ int mmt_track_batch_fetch(mmt_engine* e, int64_t ticket, double* out_xywh, float
 /* parity / debug read-back of the last track call (debug_outputs = 1):
  *   "crop"   uint8 [S][S][C]  search patch         "maps"  f32 [5][fs*fs] ctr,size_w,size_h,off_x,off_y
  *   "feat"   f32 [Lz+Lx][768] backbone output      "removed" i32 [Lx] removed slots, CE order
- *   "result" f32 [8] cx,cy,w,h (normalised), best_score, argmax index                        */
+ *   "result" f32 [8] cx,cy,w,h (normalised), best_score, argmax index
+ *   "ce_keys" f32 [n_ce][Lx] CE score (head mean of the CTR_POINT row, attn_blocks.py:44-53) of every
+ *            slot that entered each CE stage, by slot id                                        */
 int mmt_debug_fetch(mmt_engine* e, const char* what, int batch_index, void* dst, size_t nbytes);
+/* teacher-forced candidate elimination (parity diagnosis, debug_outputs = 1): keys [n_ce][Lx] by slot id
+ * replace the engine's CE scores of `slot` in every later track call, so the reference's own scores give
+ * the reference's kept sets and the remaining difference is kernel arithmetic alone.  keys = NULL turns
+ * forcing off (for every slot).  Drops captured graphs.                                            */
+int mmt_debug_force_ce(mmt_engine* e, int slot, const float* keys, size_t n_floats);
 
 /* kernel timing probe: bracket every launch of one kernel class with HIP events on the engine
  * stream ("fc1", "fc2", "qkv", "proj", "attn", "conv1"); returns launches and summed ms */

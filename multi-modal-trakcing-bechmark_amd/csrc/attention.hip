@@ -34,8 +34,8 @@ __device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (
 
 template <int WAVES, bool SPLIT, int RB = 1>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((SPLIT || WAVES < 4) ? 1 : ATTN_WPE))) void attn_kernel(const AttnArgs a) {
-  // SPLIT (fp32-faithful): every operand is an (hi, lo) bf16 pair and each product is
-  // hi*hi + lo*hi + hi*lo; the LDS images of K and V^T are held for both halves.
+  // SPLIT (fp32-faithful f16x3, common.h): every operand is an (hi, lo) fp16 pair of a range-scaled
+  // value and each product is hi*hi + lo*hi + hi*lo; the LDS images of K and V^T hold both halves.
   // RB: 16-query row blocks per wave, multiplied together against each K / V fragment (fragment
   // reads shared, RB independent softmax chains interleaved).
   static_assert(RB == 1 || !SPLIT, "split mode uses one row block per wave");
@@ -74,8 +74,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((SPL
           // the softmax scale 64^-0.5 = 2^-3 folded into Q: exact in bf16, and MFMA products and sums
           // commute with a power-of-two scale, so S = K (Q / 8)^T is the scaled score bit for bit
           const bf16x8 qv = *reinterpret_cast<const bf16x8*>(bb + (int64_t)qi * C3 + h * 64 + 32 * s + 8 * g);
+          if (SPLIT) {   // f16x3: the 1/8 is folded into qk_inv
+            qf[rb][hl][s] = qv;
+          } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) qf[rb][hl][s][e] = (__bf16)((float)qv[e] * 0.125f);
+            for (int e = 0; e < 8; ++e) qf[rb][hl][s][e] = (__bf16)((float)qv[e] * 0.125f);
+          }
         } else {
           qf[rb][hl][s] = bf16x8{};
         }
@@ -142,14 +146,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((SPL
         const int r = 16 * t + (lane & 15), c = 4 * s + g;
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(Ks[0]) + tile_off(r, c));
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) sc[rb][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[rb][0][s], sc[rb][t], 0, 0, 0);
+        for (int rb = 0; rb < RB; ++rb) sc[rb][t] = mfma16<SPLIT>(kf, qf[rb][0][s], sc[rb][t]);
         if (SPLIT) {
           const bf16x8 kl =
               *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(Ks[NH - 1]) + tile_off(r, c));
-          sc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qf[0][0][s], sc[0][t], 0, 0, 0);
-          sc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][NH - 1][s], sc[0][t], 0, 0, 0);
+          sc[0][t] = mfma16<SPLIT>(kl, qf[0][0][s], sc[0][t]);
+          sc[0][t] = mfma16<SPLIT>(kf, qf[0][NH - 1][s], sc[0][t]);
         }
       }
+      if (SPLIT) sc[0][t] *= a.qk_inv;   // S = (K s)(Q s)^T / s^2 / 8
     }
     bf16x8 pf[RB][2], pl[RB][2];
     const bool tail = kb + KB > N;   // only the last key tile has keys past N (wave-uniform)
@@ -201,11 +206,17 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((SPL
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          pf[rb][u][r] = (__bf16)sc[rb][2 * u][r];
-          pf[rb][u][4 + r] = (__bf16)sc[rb][2 * u + 1][r];
-          if (SPLIT) {
-            pl[rb][u][r] = (__bf16)(sc[rb][2 * u][r] - (float)pf[rb][u][r]);
-            pl[rb][u][4 + r] = (__bf16)(sc[rb][2 * u + 1][r] - (float)pf[rb][u][4 + r]);
+          if (SPLIT) {   // f16x3 halves of p * 2^14
+            uint16_t h0, l0, h1, l1;
+            split_h(sc[rb][2 * u][r] * 16384.0f, h0, l0);
+            split_h(sc[rb][2 * u + 1][r] * 16384.0f, h1, l1);
+            pf[rb][u][r] = __builtin_bit_cast(__bf16, h0);
+            pf[rb][u][4 + r] = __builtin_bit_cast(__bf16, h1);
+            pl[rb][u][r] = __builtin_bit_cast(__bf16, l0);
+            pl[rb][u][4 + r] = __builtin_bit_cast(__bf16, l1);
+          } else {
+            pf[rb][u][r] = (__bf16)sc[rb][2 * u][r];
+            pf[rb][u][4 + r] = (__bf16)sc[rb][2 * u + 1][r];
           }
         }
     }
@@ -225,15 +236,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((SPL
         const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[0]) + oB));
         const bf16x8 vf = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) o[rb][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[rb][u], o[rb][dt], 0, 0, 0);
+        for (int rb = 0; rb < RB; ++rb) o[rb][dt] = mfma16<SPLIT>(vf, pf[rb][u], o[rb][dt]);
         if (SPLIT) {
           const bf16x4 w0 =
               __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[NH - 1]) + oA));
           const bf16x4 w1 =
               __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(reinterpret_cast<char*>(Vs[NH - 1]) + oB));
           const bf16x8 vl = __builtin_shufflevector(w0, w1, 0, 1, 2, 3, 4, 5, 6, 7);
-          o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, pf[0][u], o[0][dt], 0, 0, 0);
-          o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pl[0][u], o[0][dt], 0, 0, 0);
+          o[0][dt] = mfma16<SPLIT>(vl, pf[0][u], o[0][dt]);
+          o[0][dt] = mfma16<SPLIT>(vf, pl[0][u], o[0][dt]);
         }
       }
     }
@@ -242,28 +253,24 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((SPL
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int qi = q0 + 16 * rb + (lane & 15);
-    const float inv = 1.0f / l[rb];
+    const float inv = SPLIT ? a.pv_inv / l[rb] : 1.0f / l[rb];
     if (qi < N) {
       const int64_t orow = ((int64_t)b * N + qi) * Cd + h * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         float v[4];
-        bf16_t hv[4];
+        uint16_t hv[4], lv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           v[r] = o[rb][dt][r] * inv;
-          hv[r] = f2bf(v[r]);
+          if (SPLIT) split_h(v[r] * a.out_scale, hv[r], lv[r]);
+          else hv[r] = f2bf(v[r]);
         }
-        uint2 w;
-        w.x = (uint32_t)hv[0] | ((uint32_t)hv[1] << 16);
-        w.y = (uint32_t)hv[2] | ((uint32_t)hv[3] << 16);
-        *reinterpret_cast<uint2*>(a.out + orow + 16 * dt + 4 * g) = w;
-        if (SPLIT) {
-          uint2 lo;
-          lo.x = (uint32_t)f2bf(v[0] - bf2f(hv[0])) | ((uint32_t)f2bf(v[1] - bf2f(hv[1])) << 16);
-          lo.y = (uint32_t)f2bf(v[2] - bf2f(hv[2])) | ((uint32_t)f2bf(v[3] - bf2f(hv[3])) << 16);
-          *reinterpret_cast<uint2*>(a.out_lo + orow + 16 * dt + 4 * g) = lo;
-        }
+        *reinterpret_cast<uint2*>(a.out + orow + 16 * dt + 4 * g) =
+            make_uint2((uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16));
+        if (SPLIT)
+          *reinterpret_cast<uint2*>(a.out_lo + orow + 16 * dt + 4 * g) =
+              make_uint2((uint32_t)lv[0] | ((uint32_t)lv[1] << 16), (uint32_t)lv[2] | ((uint32_t)lv[3] << 16));
       }
     }
   }

@@ -16,6 +16,28 @@ __device__ __forceinline__ float bf2f(bf16_t x) {
   return __uint_as_float(((uint32_t)x) << 16);
 }
 
+// ---- fp32-faithful operands ("f16x3"): a value v, pre-multiplied by its tensor's power-of-two range
+// scale s (|v s| <= 2^14 by a host-computed bound, engine.cpp range_scale), travels as two fp16 halves
+// hi = f16(v s), lo = f16(v s - hi) -- 22 significant bits -- and a product is hi*hi + lo*hi + hi*lo
+// (three fp16 MFMAs at the bf16 rate; the dropped lo*lo is 2^-22 relative).  The GEMM / attention
+// epilogues multiply the fp32 accumulator by 1 / (s_a s_w), exact for powers of two.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint16_t f2h(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }  // RNE
+__device__ __forceinline__ float h2f(uint16_t x) { return (float)__builtin_bit_cast(_Float16, x); }
+__device__ __forceinline__ void split_h(float v, uint16_t& hi, uint16_t& lo) {
+  hi = f2h(v);
+  lo = f2h(v - h2f(hi));   // v - hi is exact in fp32
+}
+// 16x16x32 MFMA on 8-element fragments held as bf16x8 registers: bf16 operands, or fp16 (F16 = true)
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 // ---- cross-lane butterflies without the LDS.  __shfl_xor lowers to ds_bpermute_b32 (an LDS round trip
 // per step, serialised along a reduction); these use v_permlane32_swap / v_permlane16_swap across the
 // 32- and 16-lane halves and DPP inside a 16-lane row (row_ror:8 is xor 8; once bit 3 is uniform,

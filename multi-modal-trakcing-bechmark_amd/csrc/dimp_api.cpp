@@ -50,6 +50,31 @@ bool bad_dims(int I, int S, int C, int H, int W, int fh, int fw) {
 
 }  // namespace
 
+namespace {
+// pinned host staging of mmt_dimp_optimize's per-call constants (one per process; calls are serial per
+// the ABI's threading rule)
+struct ConstStage {
+  float* host = nullptr;
+  size_t cap = 0;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+} g_stage;
+
+int stage_constants(size_t n) {
+  if (g_stage.pending && hipEventSynchronize(g_stage.done) != hipSuccess) return MMT_E_HIP;
+  g_stage.pending = false;
+  if (!g_stage.done && hipEventCreateWithFlags(&g_stage.done, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
+  if (g_stage.cap < n) {
+    if (g_stage.host) hipHostFree(g_stage.host);
+    g_stage.host = nullptr;
+    g_stage.cap = 0;
+    if (hipHostMalloc((void**)&g_stage.host, n * 4, hipHostMallocDefault) != hipSuccess) return MMT_E_HIP;
+    g_stage.cap = n;
+  }
+  return MMT_OK;
+}
+}  // namespace
+
 extern "C" {
 
 size_t mmt_dimp_workspace_bytes(int I, int S, int C, int H, int W, int fh, int fw, int num_iter) {
@@ -111,10 +136,21 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
   std::memcpy(params.data(), p->label_w, 32 * 4);
   std::memcpy(params.data() + 32, p->mask_w, 32 * 4);
   std::memcpy(params.data() + 64, p->spatial_w, 32 * 4);
-  if (hipMemcpyAsync(F(L.centers), centers.data(), centers.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(F(L.sqrtsw), sqrtsw.data(), sqrtsw.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(F(L.params), params.data(), params.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess)
+  // the constants travel from a pinned staging buffer (never from these stack vectors: the copies are
+  // asynchronous); the buffer is reused only after the previous call's copies have completed
+  const size_t nconst = centers.size() + sqrtsw.size() + params.size();
+  if (stage_constants(nconst) != MMT_OK) return MMT_E_HIP;
+  float* h = g_stage.host;
+  std::memcpy(h, centers.data(), centers.size() * 4);
+  std::memcpy(h + centers.size(), sqrtsw.data(), sqrtsw.size() * 4);
+  std::memcpy(h + centers.size() + sqrtsw.size(), params.data(), params.size() * 4);
+  if (hipMemcpyAsync(F(L.centers), h, centers.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(F(L.sqrtsw), h + centers.size(), sqrtsw.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(F(L.params), h + centers.size() + sqrtsw.size(), params.size() * 4, hipMemcpyHostToDevice,
+                     st) != hipSuccess ||
+      hipEventRecord(g_stage.done, st) != hipSuccess)
     return MMT_E_HIP;
+  g_stage.pending = true;
   const float step = std::exp(p->log_step_length);
   const float reg = std::fmax(p->filter_reg * p->filter_reg, p->min_filter_reg * p->min_filter_reg);
 

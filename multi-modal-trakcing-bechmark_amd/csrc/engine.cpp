@@ -44,6 +44,9 @@ struct LayerW {
   bf16_t *qkv_w, *proj_w, *fc1_w, *fc2_w;
   bf16_t *qkv_wl, *proj_wl, *fc1_wl, *fc2_wl;   // low halves (fp32-faithful mode)
   float *qkv_b, *proj_b, *fc1_b, *fc2_b, *n1w, *n1b, *n2w, *n2b;
+  // f16x3 range scales (powers of two, 1 in bf16 mode): weights, and the split activations this block
+  // produces -- LN1 / LN2 outputs, qkv output (Q, K, V and the attention output O), fc1 (GELU) output
+  float qkv_s = 1, proj_s = 1, fc1_s = 1, fc2_s = 1, ln1_s = 1, ln2_s = 1, qkv_os = 1, fc1_os = 1;
 };
 constexpr int64_t kSplitKWsElems = 4 << 20;   // 16 MB of fp32 split-K partials (mmt_op_gemm)
 
@@ -105,6 +108,9 @@ struct mmt_engine {
   bf16_t* hw[3] = {};   // conv2..4, [3 branches] contiguous
   bf16_t* hwl[3] = {};
   float* hb[3] = {};
+  // f16x3 range scales: patch-embed weights, head conv weights, final-norm output (head input) and the
+  // head's split intermediates h1..h3
+  float pe_s = 1, pep_s = 1, hw1_s = 1, hw_s[3] = {1, 1, 1}, feat_s = 1, h_s[3] = {1, 1, 1};
   float *w5 = nullptr, *b5 = nullptr, *hann = nullptr;
 
   // activations (max_batch)
@@ -115,6 +121,9 @@ struct mmt_engine {
   bf16_t *A_rgb_l = nullptr, *A_aux_l = nullptr, *Hn_l = nullptr, *QKV_l = nullptr, *O_l = nullptr, *Hm_l = nullptr,
          *feat_l = nullptr, *h1_l = nullptr, *h2_l = nullptr, *h3_l = nullptr, *zero = nullptr;
   bool split = false;
+  // parity diagnostics (debug_outputs): CE keys by slot [B][n_ce][Lx] as computed, and teacher-forced keys
+  float *ce_keys = nullptr, *ce_forced = nullptr;
+  bool force_ce = false;
   float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *s8 = nullptr,
         *a8 = nullptr,
         *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
@@ -139,9 +148,12 @@ struct mmt_engine {
   int64_t next_ticket = 0;
   int unfetched = 0;
 
-  // host-frame staging (per slot)
-  std::vector<uint8_t*> frame_dev;
+  // host-frame staging: per (slot, ring entry) device copies, made on a copy stream so a pipelined
+  // frame's PCIe transfer overlaps the compute of the frames before it
+  std::vector<uint8_t*> frame_dev;     // [max_batch * kRing]
   std::vector<size_t> frame_cap;
+  hipStream_t cstream = nullptr;
+  hipEvent_t copy_ev[kRing] = {};
 
   // tracker state (vipt.py:57, 88) in doubles
   std::vector<std::array<double, 4>> state;
@@ -252,18 +264,61 @@ int upload_f32(mmt_engine* e, float** dst, const std::vector<float>& v) {
   HIPCHECK(e, hipMemcpy(*dst, v.data(), v.size() * 4, hipMemcpyHostToDevice));
   return MMT_OK;
 }
-inline float host_bf2f(uint16_t h) {
-  uint32_t u = (uint32_t)h << 16;
-  float f;
-  std::memcpy(&f, &u, 4);
-  return f;
+// ---- f16x3 range scales (common.h): the power of two s with bound * s <= 2^14, so the fp16 halves of
+// every value * s stay finite and normal down to bound * 2^-28
+float range_scale(double bound) {
+  if (!(bound > 0) || !std::isfinite(bound)) return 1.0f;
+  const int ex = std::min(std::max((int)std::ceil(std::log2(bound)), -60), 60);
+  return std::ldexp(1.0f, 14 - ex);
 }
-// GEMM weight: bf16 hi part, and in fp32-faithful mode the bf16 residual lo = bf16(w - hi)
-int upload_w(mmt_engine* e, bf16_t** dst, bf16_t** dst_lo, const std::vector<float>& v) {
+inline uint16_t host_f16(float f) {   // RNE, finite inputs within the fp16 range
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+inline float host_f16f(uint16_t u) {
+  _Float16 h;
+  std::memcpy(&h, &u, 2);
+  return (float)h;
+}
+double max_abs(const std::vector<float>& v) {
+  double m = 0;
+  for (float x : v) m = std::max(m, (double)std::fabs(x));
+  return m;
+}
+// bounds of a LayerNorm output y = xhat * g + b (sum xhat^2 <= C): per element, and of the row's 2-norm
+double ln_elem_bound(const std::vector<float>& g, const std::vector<float>& b) {
+  return std::sqrt((double)g.size()) * max_abs(g) + max_abs(b);
+}
+double ln_norm_bound(const std::vector<float>& g, const std::vector<float>& b) {
+  double bb = 0;
+  for (float x : b) bb += (double)x * x;
+  return std::sqrt((double)g.size()) * max_abs(g) + std::sqrt(bb);
+}
+// max_j |w_j . a + b_j| over inputs with |a|_2 <= anorm (rows of w, K each)
+double linear_bound(const std::vector<float>& w, const std::vector<float>& b, size_t K, double anorm) {
+  double m = 0;
+  for (size_t j = 0; j * K < w.size(); ++j) {
+    double n2 = 0;
+    for (size_t k = 0; k < K; ++k) n2 += (double)w[j * K + k] * w[j * K + k];
+    m = std::max(m, std::sqrt(n2) * anorm + (j < b.size() ? std::fabs((double)b[j]) : 0.0));
+  }
+  return m;
+}
+
+// GEMM weight: bf16 in bf16 mode; in fp32-faithful mode the f16x3 halves of w * s (s = range_scale(max|w|))
+int upload_w(mmt_engine* e, bf16_t** dst, bf16_t** dst_lo, const std::vector<float>& v, float* scale = nullptr) {
   std::vector<uint16_t> t(v.size()), tl(v.size());
+  const float sc = e->split ? range_scale(max_abs(v)) : 1.0f;
+  if (scale) *scale = sc;
   for (size_t i = 0; i < v.size(); ++i) {
-    t[i] = host_bf16(v[i]);
-    tl[i] = host_bf16(v[i] - host_bf2f(t[i]));
+    if (e->split) {
+      t[i] = host_f16(v[i] * sc);
+      tl[i] = host_f16(v[i] * sc - host_f16f(t[i]));
+    } else {
+      t[i] = host_bf16(v[i]);
+    }
   }
   *dst = walloc<bf16_t>(e, v.size());
   if (!*dst) return e->fail(MMT_E_HIP, "weight arena overflow");
@@ -308,10 +363,10 @@ int pack_weights(mmt_engine* e) {
   const bool vipt = c.model == MMT_MODEL_VIPT;
   e->wcap = (e->split ? 400ull : 200ull) << 20;
   HIPCHECK(e, hipMalloc(&e->warena, e->wcap));
-  TRY(upload_w(e, &e->pe_w, &e->pe_wl, H(e, "backbone.patch_embed.proj.weight")));
+  TRY(upload_w(e, &e->pe_w, &e->pe_wl, H(e, "backbone.patch_embed.proj.weight"), &e->pe_s));
   TRY(upload_f32(e, &e->pe_b, H(e, "backbone.patch_embed.proj.bias")));
   if (vipt) {
-    TRY(upload_w(e, &e->pep_w, &e->pep_wl, H(e, "backbone.patch_embed_prompt.proj.weight")));
+    TRY(upload_w(e, &e->pep_w, &e->pep_wl, H(e, "backbone.patch_embed_prompt.proj.weight"), &e->pep_s));
     TRY(upload_f32(e, &e->pep_b, H(e, "backbone.patch_embed_prompt.proj.bias")));
   }
   std::vector<float> pos(H(e, "backbone.pos_embed_z"));
@@ -408,14 +463,24 @@ int pack_weights(mmt_engine* e) {
   for (int i = 0; i < DEPTH; ++i) {
     const std::string p = "backbone.blocks." + std::to_string(i) + ".";
     LayerW& w = e->lw[i];
-    TRY(upload_w(e, &w.qkv_w, &w.qkv_wl, H(e, p + "attn.qkv.weight")));
+    TRY(upload_w(e, &w.qkv_w, &w.qkv_wl, H(e, p + "attn.qkv.weight"), &w.qkv_s));
     TRY(upload_f32(e, &w.qkv_b, H(e, p + "attn.qkv.bias")));
-    TRY(upload_w(e, &w.proj_w, &w.proj_wl, H(e, p + "attn.proj.weight")));
+    TRY(upload_w(e, &w.proj_w, &w.proj_wl, H(e, p + "attn.proj.weight"), &w.proj_s));
     TRY(upload_f32(e, &w.proj_b, H(e, p + "attn.proj.bias")));
-    TRY(upload_w(e, &w.fc1_w, &w.fc1_wl, H(e, p + "mlp.fc1.weight")));
+    TRY(upload_w(e, &w.fc1_w, &w.fc1_wl, H(e, p + "mlp.fc1.weight"), &w.fc1_s));
     TRY(upload_f32(e, &w.fc1_b, H(e, p + "mlp.fc1.bias")));
-    TRY(upload_w(e, &w.fc2_w, &w.fc2_wl, H(e, p + "mlp.fc2.weight")));
+    TRY(upload_w(e, &w.fc2_w, &w.fc2_wl, H(e, p + "mlp.fc2.weight"), &w.fc2_s));
     TRY(upload_f32(e, &w.fc2_b, H(e, p + "mlp.fc2.bias")));
+    if (e->split) {   // activation range scales from the weights (bounds: LN outputs, linear layers)
+      const auto &g1 = H(e, p + "norm1.weight"), &b1 = H(e, p + "norm1.bias");
+      const auto &g2 = H(e, p + "norm2.weight"), &b2 = H(e, p + "norm2.bias");
+      w.ln1_s = range_scale(ln_elem_bound(g1, b1));
+      w.ln2_s = range_scale(ln_elem_bound(g2, b2));
+      w.qkv_os = range_scale(linear_bound(H(e, p + "attn.qkv.weight"), H(e, p + "attn.qkv.bias"), C,
+                                          ln_norm_bound(g1, b1)));
+      w.fc1_os = range_scale(linear_bound(H(e, p + "mlp.fc1.weight"), H(e, p + "mlp.fc1.bias"), C,
+                                          ln_norm_bound(g2, b2)));   // |GELU(h)| <= |h|
+    }
     TRY(upload_f32(e, &w.n1w, H(e, p + "norm1.weight")));
     TRY(upload_f32(e, &w.n1b, H(e, p + "norm1.bias")));
     TRY(upload_f32(e, &w.n2w, H(e, p + "norm2.weight")));
@@ -431,8 +496,13 @@ int pack_weights(mmt_engine* e) {
     std::vector<float> w((size_t)3 * hc * 9 * C), b((size_t)3 * hc);
     for (int k = 0; k < 3; ++k)
       fold_conv(e, std::string("box_head.conv1_") + br[k], hc, C, w, b, (size_t)k * hc * 9 * C, (size_t)k * hc);
-    TRY(upload_w(e, &e->hw1, &e->hw1l, w));
+    TRY(upload_w(e, &e->hw1, &e->hw1l, w, &e->hw1_s));
     TRY(upload_f32(e, &e->hb1, b));
+    if (e->split) {   // head input: final-norm rows; a 3x3 window of them has 2-norm <= 3 * the row bound
+      const auto &gn = H(e, "backbone.norm.weight"), &bn = H(e, "backbone.norm.bias");
+      e->feat_s = range_scale(ln_elem_bound(gn, bn));
+      e->h_s[0] = range_scale(linear_bound(w, b, (size_t)9 * C, 3.0 * ln_norm_bound(gn, bn)));
+    }
   }
   for (int j = 2; j <= 4; ++j) {
     const int co = ch[j], ci = ch[j - 1];
@@ -440,8 +510,12 @@ int pack_weights(mmt_engine* e) {
     for (int k = 0; k < 3; ++k)
       fold_conv(e, std::string("box_head.conv") + std::to_string(j) + "_" + br[k], co, ci, w, b,
                 (size_t)k * co * 9 * ci, (size_t)k * co);
-    TRY(upload_w(e, &e->hw[j - 2], &e->hwl[j - 2], w));
+    TRY(upload_w(e, &e->hw[j - 2], &e->hwl[j - 2], w, &e->hw_s[j - 2]));
     TRY(upload_f32(e, &e->hb[j - 2], b));
+    if (e->split && j < 4) {   // h_{j}: input elements <= 2^14 / h_s[j-2], window 2-norm <= 3 sqrt(ci) of that
+      const double in_b = std::ldexp(1.0, 14) / e->h_s[j - 2];
+      e->h_s[j - 1] = range_scale(linear_bound(w, b, (size_t)9 * ci, 3.0 * std::sqrt((double)ci) * in_b));
+    }
   }
   {
     std::vector<float> w5, b5;
@@ -490,6 +564,9 @@ int alloc_acts(mmt_engine* e) {
     reqs.insert(reqs.end(), lo.begin(), lo.end());
   }
   if (e->cfg.debug_outputs) {
+    const size_t nce = std::max(e->cfg.n_ce, 1);
+    reqs.push_back({(void**)&e->ce_keys, (size_t)B * nce * Lx * 4});
+    reqs.push_back({(void**)&e->ce_forced, (size_t)B * nce * Lx * 4});
     reqs.push_back({(void**)&e->dbg_patch, (size_t)B * S * S * Cin});
     reqs.push_back({(void**)&e->dbg_maps, (size_t)B * 5 * Lx * 4});
     reqs.push_back({(void**)&e->dbg_feat, (size_t)B * L * C * 4});
@@ -590,6 +667,15 @@ GemmArgs dense(mmt_engine* e, const bf16_t* A, const bf16_t* Al, int64_t lda, co
   return a;
 }
 
+// f16x3 scaling of a GEMM's groups: acc * 1 / (s_A s_W), 16-bit outputs split at out_scale
+GemmArgs scaled(GemmArgs a, float sa_sw, float out_scale) {
+  for (int k = 0; k < 3; ++k) {
+    a.g[k].inv = 1.0f / sa_sw;
+    a.g[k].out_scale = out_scale;
+  }
+  return a;
+}
+
 void run_gemm(mmt_engine* e, hipStream_t st, const char* cls, const GemmArgs& a, int epi) {
   const double flops = 2.0 * a.M * a.N * (double)a.K * a.groups;
   // algorithmic HBM bytes: A and W once, C once (bf16 or fp32), R once for the residual epilogues
@@ -678,11 +764,13 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
                        n * L, C, C);
     g.g[1] = GemmGroup{A_aux, A_aux_l, C, e->pep_w, e->pep_wl, C, e->pep_b, q_tok_aux, nullptr, C, nullptr, 0};
     g.groups = 2;
+    g = scaled(g, kPixScale * e->pe_s, 1.0f);
+    g.g[1].inv = 1.0f / (kPixScale * e->pep_s);
     run_gemm(e, s, "patch", g, EPI_F32);
   } else {
     GemmArgs g = dense(e, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, X, nullptr, C, e->pos, C, n * L, C, C);
     g.pos_rows = L;
-    run_gemm(e, s, "patch", g, EPI_POS_F32);
+    run_gemm(e, s, "patch", scaled(g, kPixScale * e->pe_s, 1.0f), EPI_POS_F32);
   }
   init_indices(q_gidx0, q_slot2pos, n, Lz, Lx, s);
 
@@ -719,6 +807,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
   int* gout = q_gidx1;
   int removed_off = 0;
   int Ls = Lx;
+  int ce_stage = 0;
   for (int i = 0; i < DEPTH; ++i) {
     const LayerW& w = e->lw[i];
     const int Na = Lz + Ls;
@@ -750,13 +839,15 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
       la.b = w.n1b;
       la.out = q_Hn;
       la.out_lo = q_Hn_l;
+      la.out_scale = w.ln1_s;
       prompt_expand_ln(pa, la, s);
     } else {
-      layernorm(X, w.n1w, w.n1b, q_Hn, q_Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+      layernorm(X, w.n1w, w.n1b, q_Hn, q_Hn_l, w.ln1_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
     }
     run_gemm(e, s, "qkv",
-             dense(e, q_Hn, q_Hn_l, C, w.qkv_w, w.qkv_wl, C, w.qkv_b, q_QKV, q_QKV_l, 3 * C, nullptr, 0, n * Na,
-                   3 * C, C),
+             scaled(dense(e, q_Hn, q_Hn_l, C, w.qkv_w, w.qkv_wl, C, w.qkv_b, q_QKV, q_QKV_l, 3 * C, nullptr, 0,
+                          n * Na, 3 * C, C),
+                    w.ln1_s * w.qkv_s, w.qkv_os),
              EPI_BF16);
     const bool ce = e->keep_at[i] != e->ls_before[i];
     AttnArgs aa{};
@@ -764,6 +855,9 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
     aa.qkv_lo = q_QKV_l;
     aa.out = q_O;
     aa.out_lo = q_O_l;
+    aa.qk_inv = 0.125f / (w.qkv_os * w.qkv_os);   // attn.py:15 scale 64^-0.5
+    aa.pv_inv = 1.0f / (16384.0f * w.qkv_os);
+    aa.out_scale = w.qkv_os;                      // |O| <= max |V|
     aa.B = n;
     aa.N = Na;
     aa.heads = HEADS;
@@ -774,7 +868,8 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
     attention(aa, s);
     probe_end(e, s, "attn");
     run_gemm(e, s, "proj",
-             dense(e, q_O, q_O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
+             scaled(dense(e, q_O, q_O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
+                    w.qkv_os * w.proj_s, 1.0f),
              EPI_RESID_F32);
     if (ce) {  // attn_blocks.py:99-101
       const int keep = e->keep_at[i];
@@ -792,25 +887,35 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
       ce_a.slot2pos = q_slot2pos;
       ce_a.removed = q_removed;
       ce_a.removed_off = removed_off;
+      const size_t nce = std::max(c.n_ce, 1);
+      ce_a.keys_pitch = (int)(nce * Lx);
+      ce_a.keys_out = e->ce_keys ? e->ce_keys + (size_t)r0 * nce * Lx + (size_t)ce_stage * Lx : nullptr;
+      ce_a.forced = (e->force_ce && e->ce_forced) ? e->ce_forced + (size_t)b0 * nce * Lx + (size_t)ce_stage * Lx
+                                                  : nullptr;
+      ++ce_stage;
       ce_select(ce_a, s);
       removed_off += Ls - keep;
       std::swap(gin, gout);
       Ls = keep;
-      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, nullptr, n * (Lz + Ls), Lz + Ls, q_gather, Na, X2, s);
+      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * (Lz + Ls), Lz + Ls, q_gather, Na, X2, s);
       std::swap(X, X2);
     } else {
-      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
     }
     const int Nm = Lz + Ls;
     run_gemm(e, s, "fc1",
-             dense(e, q_Hn, q_Hn_l, C, w.fc1_w, w.fc1_wl, C, w.fc1_b, q_Hm, q_Hm_l, MLPD, nullptr, 0, n * Nm, MLPD,
-                   C),
+             scaled(dense(e, q_Hn, q_Hn_l, C, w.fc1_w, w.fc1_wl, C, w.fc1_b, q_Hm, q_Hm_l, MLPD, nullptr, 0,
+                          n * Nm, MLPD, C),
+                    w.ln2_s * w.fc1_s, w.fc1_os),
              EPI_GELU_BF16);
     run_gemm(e, s, "fc2",
-             dense(e, q_Hm, q_Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C, n * Nm, C, MLPD),
+             scaled(dense(e, q_Hm, q_Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C, n * Nm, C,
+                          MLPD),
+                    w.fc1_os * w.fc2_s, 1.0f),
              EPI_RESID_F32);
   }
-  final_norm_recover(X, Lz + Ls, q_slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, q_feat, q_feat_l, q_dbg_feat, s);
+  final_norm_recover(X, Lz + Ls, q_slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, q_feat, q_feat_l, e->feat_s,
+                     q_dbg_feat, s);
 
   // CENTER head: conv1 of the three branches fused (N = 3*hc), then per-branch grouped convs
   const int hc = c.head_channels, fs = e->fs, M = n * Lx;
@@ -820,7 +925,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
     g.amode = A_CONV3;
     g.conv_hw = fs;
     g.conv_cin = C;
-    run_gemm(e, s, "conv1", g, EPI_RELU_BF16);
+    run_gemm(e, s, "conv1", scaled(g, e->feat_s * e->hw1_s, e->h_s[0]), EPI_RELU_BF16);
   }
   const int ch[4] = {hc, hc / 2, hc / 4, hc / 8};
   for (int j = 0; j < 3; ++j) {   // conv2, conv3, conv4
@@ -857,7 +962,8 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
     g.amode = A_CONV3;
     g.conv_hw = fs;
     g.conv_cin = ci;
-    run_gemm(e, s, j == 0 ? "conv2" : (j == 1 ? "conv3" : "conv4"), g, j == 2 ? EPI_RELU_F32 : EPI_RELU_BF16);
+    run_gemm(e, s, j == 0 ? "conv2" : (j == 1 ? "conv3" : "conv4"),
+             scaled(g, e->h_s[j] * e->hw_s[j], j < 2 ? e->h_s[j + 1] : 1.0f), j == 2 ? EPI_RELU_F32 : EPI_RELU_BF16);
   }
   DecodeArgs da{};
   da.B = n;
@@ -889,8 +995,8 @@ int geometry(mmt_engine* e, const double box[4], double factor, int out_sz, int*
   return MMT_OK;
 }
 
-int stage_frame(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww, int Cc, int64_t stride,
-                int is_device, const uint8_t** dev) {
+int stage_frame(mmt_engine* e, int slot, int ring, const uint8_t* frame, int Hh, int Ww, int Cc, int64_t stride,
+                int is_device, const uint8_t** dev, hipStream_t cs) {
   if (!frame || Hh < 2 || Ww < 2 || Cc != e->cfg.in_chans || stride < (int64_t)Ww * Cc)
     return e->fail(MMT_E_ARG, "bad frame (expect H x W x in_chans uint8, H,W >= 2)");
   if (is_device) {
@@ -898,14 +1004,19 @@ int stage_frame(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww, i
     return MMT_OK;
   }
   const size_t bytes = (size_t)stride * Hh;
-  if (e->frame_cap[slot] < bytes) {
-    if (e->frame_dev[slot]) hipFree(e->frame_dev[slot]);
-    e->frame_dev[slot] = nullptr;
-    HIPCHECK(e, hipMalloc(&e->frame_dev[slot], bytes));
-    e->frame_cap[slot] = bytes;
+  const size_t k = (size_t)slot * kRing + ring;
+  if (e->frame_cap[k] < bytes) {
+    if (e->frame_dev[k]) {
+      HIPCHECK(e, hipStreamSynchronize(e->stream));
+      HIPCHECK(e, hipStreamSynchronize(cs));
+      hipFree(e->frame_dev[k]);
+    }
+    e->frame_dev[k] = nullptr;
+    HIPCHECK(e, hipMalloc(&e->frame_dev[k], bytes));
+    e->frame_cap[k] = bytes;
   }
-  HIPCHECK(e, hipMemcpyAsync(e->frame_dev[slot], frame, bytes, hipMemcpyHostToDevice, e->stream));
-  *dev = e->frame_dev[slot];
+  HIPCHECK(e, hipMemcpyAsync(e->frame_dev[k], frame, bytes, hipMemcpyHostToDevice, cs));
+  *dev = e->frame_dev[k];
   return MMT_OK;
 }
 
@@ -1029,13 +1140,16 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   if (hipSetDevice(device) != hipSuccess) return MMT_E_HIP;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
   if (hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
+  if (hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
+  for (auto& ev : e->copy_ev)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
   if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess)
     return MMT_E_HIP;
   if (const char* ov = std::getenv("MMT_OVERLAP_MIN")) e->overlap_min = std::atoi(ov);
   build_expected(e.get());
-  e->frame_dev.assign(c.max_batch, nullptr);
-  e->frame_cap.assign(c.max_batch, 0);
+  e->frame_dev.assign((size_t)c.max_batch * kRing, nullptr);
+  e->frame_cap.assign((size_t)c.max_batch * kRing, 0);
   e->state.assign(c.max_batch, {0, 0, 0, 0});
   e->active.assign(c.max_batch, 0);
   if (alloc_acts(e.get()) != MMT_OK) return MMT_E_HIP;
@@ -1069,6 +1183,12 @@ void mmt_destroy(mmt_engine* e) {
     if (t.done) hipEventDestroy(t.done);
   if (e->stream) hipStreamDestroy(e->stream);
   if (e->stream2) hipStreamDestroy(e->stream2);
+  if (e->cstream) {
+    hipStreamSynchronize(e->cstream);
+    hipStreamDestroy(e->cstream);
+  }
+  for (auto& ev : e->copy_ev)
+    if (ev) hipEventDestroy(ev);
   if (e->fork_ev) hipEventDestroy(e->fork_ev);
   if (e->join_ev) hipEventDestroy(e->join_ev);
   delete e;
@@ -1134,7 +1254,7 @@ int mmt_initialize(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww
   double rf;
   TRY(geometry(e, init_xywh, e->cfg.template_factor, e->cfg.template_size, &x1, &y1, &cs, &rf));
   const uint8_t* dev;
-  TRY(stage_frame(e, slot, frame, Hh, Ww, Cc, row_stride, is_device, &dev));
+  TRY(stage_frame(e, slot, 0, frame, Hh, Ww, Cc, row_stride, is_device, &dev, e->stream));
   CropParam p{dev, row_stride, Hh, Ww, Cc, x1, y1, cs, 0};
   e->params_host[0] = p;
   HIPCHECK(e, hipMemcpyAsync(e->params_dev, e->params_host, sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
@@ -1181,8 +1301,14 @@ int mmt_track_batch_submit(mmt_engine* e, int first_slot, int n, const uint8_t* 
       TRY(geometry(e, e->state[slot].data(), e->cfg.search_factor, e->cfg.search_size, &x1, &y1, &cs, &rf));
     }
     const uint8_t* dev;
-    TRY(stage_frame(e, slot, frames[i], Hs[i], Ws[i], Cc, row_stride[i], is_device, &dev));
+    TRY(stage_frame(e, slot, (int)(e->next_ticket % kRing), frames[i], Hs[i], Ws[i], Cc, row_stride[i], is_device,
+                    &dev, e->cstream));
     ph[i] = CropParam{dev, row_stride[i], Hs[i], Ws[i], Cc, 0, 0, 0, 0};   // geometry: crop_geometry()
+  }
+  if (!is_device) {   // the launch waits for this frame's copies only (copy stream, overlapping compute)
+    hipEvent_t ce = e->copy_ev[e->next_ticket % kRing];
+    HIPCHECK(e, hipEventRecord(ce, e->cstream));
+    HIPCHECK(e, hipStreamWaitEvent(e->stream, ce, 0));
   }
   HIPCHECK(e, hipMemcpyAsync(e->params_dev, ph, n * sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
   const GraphEntry* replayed = nullptr;
@@ -1279,11 +1405,39 @@ int mmt_debug_fetch(mmt_engine* e, const char* what, int bi, void* dst, size_t n
   } else if (w == "result") {
     sz = 8 * 4;
     src = reinterpret_cast<const char*>(e->res) + bi * sz;
+  } else if (w == "ce_keys") {
+    sz = (size_t)std::max(e->cfg.n_ce, 1) * e->Lx * 4;
+    src = reinterpret_cast<const char*>(e->ce_keys) + bi * sz;
   } else {
     return e->fail(MMT_E_ARG, "unknown debug buffer " + w);
   }
   if (nbytes < sz) return e->fail(MMT_E_ARG, "debug buffer too small");
   HIPCHECK(e, hipMemcpy(dst, src, sz, hipMemcpyDeviceToHost));
+  return MMT_OK;
+}
+
+int mmt_debug_force_ce(mmt_engine* e, int slot, const float* keys, size_t n_floats) {
+  int r = check_engine(e);
+  if (r) return r;
+  if (!e->cfg.debug_outputs) return e->fail(MMT_E_STATE, "engine built without debug_outputs");
+  const size_t per = (size_t)std::max(e->cfg.n_ce, 1) * e->Lx;
+  if (e->unfetched) return e->fail(MMT_E_STATE, "force_ce with unfetched frames in flight");
+  if (!keys) {
+    e->force_ce = false;
+  } else {
+    if (slot < 0 || slot >= e->cfg.max_batch || n_floats != per) return e->fail(MMT_E_ARG, "bad forced CE keys");
+    HIPCHECK(e, hipMemcpy(e->ce_forced + (size_t)slot * per, keys, per * 4, hipMemcpyHostToDevice));
+    e->force_ce = true;
+  }
+  // captured graphs carry the old kernel arguments
+  for (auto& kv : e->graphs) {
+    hipGraphExecDestroy(kv.second.exec);
+    for (auto& pr : kv.second.ev) {
+      hipEventDestroy(pr.first);
+      hipEventDestroy(pr.second);
+    }
+  }
+  e->graphs.clear();
   return MMT_OK;
 }
 
@@ -1424,7 +1578,8 @@ int mmt_op_attention(const void* qkv, void* out, int B, int N, int heads, int ce
 int mmt_op_layernorm(const float* x, const float* w, const float* b, void* out_bf16, float* out_f32, int rows,
                      void* stream) {
   if (!x || !w || !b || rows <= 0 || (!out_bf16 && !out_f32)) return MMT_E_ARG;
-  layernorm(x, w, b, (bf16_t*)out_bf16, nullptr, out_f32, rows, rows, nullptr, rows, nullptr, (hipStream_t)stream);
+  layernorm(x, w, b, (bf16_t*)out_bf16, nullptr, 1.0f, out_f32, rows, rows, nullptr, rows, nullptr,
+            (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 

@@ -14,8 +14,9 @@
 // * XCD-aware tile order: blocks that share an XCD (b % 8) get a compact rectangle of output tiles
 //   (a few W column tiles x all A rows, or an A row slice x all W tiles), so the L2 of each XCD
 //   serves the re-reads;
-// * SPLIT (fp32-faithful "bf16x3" mode): A = Ah + Al, W = Wh + Wl as bf16 pairs,
-//   acc += Wh*Ah + Wl*Ah + Wh*Al  (relative error ~1e-5, vs ~2e-3 for plain bf16);
+// * SPLIT (fp32-faithful "f16x3" mode, common.h): A = Ah + Al, W = Wh + Wl as fp16 pairs of range-scaled
+//   values, acc += Wh*Ah + Wl*Ah + Wh*Al with v_mfma_f32_16x16x32_f16 (22-bit operands: the fp32
+//   reference's accuracy, vs ~2e-3 relative for plain bf16), acc * inv in the epilogue;
 // * the MFMA is issued W-fragment x A-fragment, so a lane ends with 4 consecutive output columns
 //   of one row: 8-B (bf16) / 16-B (fp32) epilogue stores.
 #include <type_traits>
@@ -81,7 +82,8 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
 template <int EPI, bool SPLIT>
 __device__ __forceinline__ void store4(const GemmGroup& g, const GemmArgs& args, int m, int n, const f32x4& a) {
   const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-  float v[4] = {a[0] + bv.x, a[1] + bv.y, a[2] + bv.z, a[3] + bv.w};
+  const float sc = SPLIT ? g.inv : 1.0f;
+  float v[4] = {a[0] * sc + bv.x, a[1] * sc + bv.y, a[2] * sc + bv.z, a[3] * sc + bv.w};
   if (EPI == EPI_GELU_BF16)
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
@@ -90,18 +92,22 @@ __device__ __forceinline__ void store4(const GemmGroup& g, const GemmArgs& args,
     for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
   const int64_t off = (int64_t)m * g.ldc + n;
   if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
-    bf16_t h[4];
+    if (SPLIT && g.C_lo) {   // the f16x3 pair of v * out_scale
+      uint16_t h[4], l[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) h[e] = f2bf(v[e]);
-    uint2 o;
-    o.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-    o.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
-    *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C) + off) = o;
-    if (SPLIT && g.C_lo) {
-      uint2 lo;
-      lo.x = (uint32_t)f2bf(v[0] - bf2f(h[0])) | ((uint32_t)f2bf(v[1] - bf2f(h[1])) << 16);
-      lo.y = (uint32_t)f2bf(v[2] - bf2f(h[2])) | ((uint32_t)f2bf(v[3] - bf2f(h[3])) << 16);
-      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C_lo) + off) = lo;
+      for (int e = 0; e < 4; ++e) split_h(v[e] * g.out_scale, h[e], l[e]);
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C) + off) =
+          make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C_lo) + off) =
+          make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+    } else {
+      bf16_t h[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) h[e] = f2bf(v[e]);
+      uint2 o;
+      o.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      o.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.C) + off) = o;
     }
   } else {
     float4 o = make_float4(v[0], v[1], v[2], v[3]);
@@ -335,10 +341,10 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
       for (int i = 0; i < T::FM; ++i)
 #pragma unroll
         for (int jj = 0; jj < T::FN; ++jj) {
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[jj], ah[i], acc[i][jj], 0, 0, 0);
+          acc[i][jj] = mfma16<SPLIT>(bh[jj], ah[i], acc[i][jj]);
           if (SPLIT) {
-            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[jj], ah[i], acc[i][jj], 0, 0, 0);
-            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[jj], al[i], acc[i][jj], 0, 0, 0);
+            acc[i][jj] = mfma16<SPLIT>(bl[jj], ah[i], acc[i][jj]);
+            acc[i][jj] = mfma16<SPLIT>(bh[jj], al[i], acc[i][jj]);
           }
         }
     }

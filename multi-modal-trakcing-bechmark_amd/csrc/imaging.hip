@@ -38,10 +38,15 @@ __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
   for (int c = 0; c < a.C; ++c) {
     const float t = ((float)u8[c] / 255.0f - kMean[c]) / kStd[c];
     const int64_t o = rowoff + (c % 3) * 256 + within;
-    const bf16_t h = f2bf(t);
-    (c < 3 ? a.A_rgb : a.A_aux)[o] = h;
     bf16_t* lo = c < 3 ? a.A_rgb_lo : a.A_aux_lo;
-    if (lo) lo[o] = f2bf(t - bf2f(h));
+    if (lo) {   // f16x3 halves of t * 2^12
+      uint16_t h, l;
+      split_h(t * kPixScale, h, l);
+      (c < 3 ? a.A_rgb : a.A_aux)[o] = h;
+      lo[o] = l;
+    } else {
+      (c < 3 ? a.A_rgb : a.A_aux)[o] = f2bf(t);
+    }
     if (a.dbg_patch) a.dbg_patch[((int64_t)b * O * O + idx) * a.C + c] = (uint8_t)u8[c];
   }
 }

@@ -25,8 +25,11 @@ struct GemmGroup {
   const bf16_t* A; const bf16_t* A_lo; int64_t lda;     // A_lo: low half of the split operand (SPLIT)
   const bf16_t* W; const bf16_t* W_lo; int64_t ldw;
   const float* bias;
-  void* C; void* C_lo; int64_t ldc;                     // C_lo: bf16 outputs also emit their low half
+  void* C; void* C_lo; int64_t ldc;                     // C_lo: 16-bit outputs also emit their low half
   const float* R; int64_t ldr;
+  // SPLIT ("f16x3", common.h): A / W / C halves are fp16 of range-scaled values; acc * inv = A W^T
+  // (inv = 1 / (s_A s_W)) and 16-bit outputs are written as the split of value * out_scale
+  float inv = 1.0f, out_scale = 1.0f;
 };
 
 struct GemmArgs {
@@ -37,7 +40,7 @@ struct GemmArgs {
   int conv_hw;      // A_CONV3: feature map is conv_hw x conv_hw (NHWC rows), zero padding 1
   int conv_cin;     // A_CONV3: input channels (multiple of 64)
   int pos_rows;     // EPI_POS_F32
-  int split;        // 1: fp32-faithful bf16x3 products
+  int split;        // 1: fp32-faithful f16x3 products (common.h)
   int gm;           // (set by the launcher) tile rows per super-tile group of the tile order
   int ksplit;       // (set by the launcher) K splits (1: none)
   float* ws;        // split-K workspace ([groups][ksplit][M][N] fp32) or null: never split
@@ -59,13 +62,18 @@ struct AttnArgs {
   int ce_query;        // template token whose probability row is exported (-1: none)
   int ce_lens_t;       // template length; exported keys are [ce_lens_t, N)
   float* ce_prob;      // [B][heads][N - ce_lens_t]
+  // split mode (f16x3): qkv halves are fp16 of qkv * s_qkv; qk_inv = 1 / s_qkv^2, pv_inv = 1 / (2^14 s_qkv)
+  // (P travels as the split of p * 2^14), out halves = split of O * out_scale
+  float qk_inv = 1.0f, pv_inv = 1.0f, out_scale = 1.0f;
 };
 void attention(const AttnArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- layer norm (row of 768)
 // out_bf16[r] = LN(x[src(r)]), src(r) = gather ? b*in_pitch + gather[b][t] : r ; optional copy of x[src] to xcopy[r]
-void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float* out_f32,
-               int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy, hipStream_t s);
+// out_lo non-null: out_bf16 / out_lo are the f16x3 halves of LN * out_scale instead (common.h)
+void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float out_scale,
+               float* out_f32, int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy,
+               hipStream_t s);
 
 // ---------------------------------------------------------------- ViPT prompt blocks
 struct PromptArgs {
@@ -105,7 +113,8 @@ struct LnPromptArgs {
   const float* pos;          // mode 1: [Lz+Lx][768]
   const int* gidx;           // mode 2: [B][rows_per_seq - Lz] slot of each compact search token
   const float* w; const float* b;
-  bf16_t* out; bf16_t* out_lo;
+  bf16_t* out; bf16_t* out_lo;   // out_lo non-null: f16x3 halves of LN * out_scale
+  float out_scale;
 };
 // fovea (s8 for every slot), then the prompt residual (conv1x1 of s8, formed per row from an LDS copy
 // of conv1x1) and LN1
@@ -122,13 +131,20 @@ struct CEArgs {
   int* slot2pos;          // [B][Lx] updated
   int* removed;           // [B][Lx] removed slot ids, appended at removed_off
   int removed_off;
+  // parity diagnostics (null in production):
+  const float* forced;    // [B][Lx] keys by slot id replacing the head-mean scores (teacher-forced CE:
+                          // the reference's own scores give the reference's kept set)
+  float* keys_out;        // [B][Lx] the head-mean score of every surviving slot, by slot id
+  int keys_pitch;         // floats between sequences of forced / keys_out
 };
 void ce_select(const CEArgs& a, hipStream_t s);
 void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s);
 
 // final norm + token recovery (zeros at pruned slots) -> head input NHWC bf16 [B][Lx][768]
+// feat_lo non-null: feat / feat_lo are the f16x3 halves of the normed rows * feat_scale
 void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
-                        int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float* feat_f32_dbg, hipStream_t s);
+                        int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float feat_scale, float* feat_f32_dbg,
+                        hipStream_t s);
 
 // ---------------------------------------------------------------- crop + normalise + patchify
 struct CropParam {                 // one per sequence (device memory, rewritten every frame)
@@ -142,11 +158,13 @@ struct CropArgs {
   const CropParam* params;         // [B]
   int B, out_sz, C;                // C = 6 (RGB+aux) or 3
   bf16_t* A_rgb; bf16_t* A_aux;    // [B][rows_per_seq][768]
-  bf16_t* A_rgb_lo; bf16_t* A_aux_lo;  // split mode low halves (else null)
+  bf16_t* A_rgb_lo; bf16_t* A_aux_lo;  // split mode (else null): A / A_lo are the f16x3 halves of the
+                                       // normalised pixel * kPixScale
   int rows_per_seq, row0;          // patch rows land at row0 + patch index
   uint8_t* dbg_patch;              // optional [B][out][out][C]
 };
 void crop_patchify(const CropArgs& a, hipStream_t s);
+constexpr float kPixScale = 4096.0f;   // |(p/255 - mean) / std| <= 2.64: 2^12 keeps the f16x3 halves below 2^14
 
 // ---------------------------------------------------------------- head tail + decode
 // ---------------------------------------------------------------- device-resident tracker state

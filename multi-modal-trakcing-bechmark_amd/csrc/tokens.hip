@@ -78,15 +78,18 @@ __device__ __forceinline__ void store_bf16(bf16_t* p, const Row12& y, int lane) 
     q[lane + 64 * i] = o;
   }
 }
-__device__ __forceinline__ void store_bf16_lo(bf16_t* p, const Row12& y, int lane) {   // y - bf16(y)
-  uint2* q = reinterpret_cast<uint2*>(p);
+// the f16x3 halves of y * scale (common.h)
+__device__ __forceinline__ void store_split(bf16_t* hi, bf16_t* lo, const Row12& y, float scale, int lane) {
+  uint2* qh = reinterpret_cast<uint2*>(hi);
+  uint2* ql = reinterpret_cast<uint2*>(lo);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const float4 v = y.v[i];
-    uint2 o;
-    o.x = (uint32_t)f2bf(v.x - bf2f(f2bf(v.x))) | ((uint32_t)f2bf(v.y - bf2f(f2bf(v.y))) << 16);
-    o.y = (uint32_t)f2bf(v.z - bf2f(f2bf(v.z))) | ((uint32_t)f2bf(v.w - bf2f(f2bf(v.w))) << 16);
-    q[lane + 64 * i] = o;
+    const float v[4] = {y.v[i].x * scale, y.v[i].y * scale, y.v[i].z * scale, y.v[i].w * scale};
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split_h(v[e], h[e], l[e]);
+    qh[lane + 64 * i] = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+    ql[lane + 64 * i] = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
   }
 }
 __device__ __forceinline__ void store_f32(float* p, const Row12& y, int lane) {
@@ -97,7 +100,7 @@ __device__ __forceinline__ void store_f32(float* p, const Row12& y, int lane) {
 
 // ------------------------------------------------------------------ LayerNorm (optionally fused CE gather)
 __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w, const float* b, bf16_t* ob,
-                                                 bf16_t* olo, float* of, int rows, int rows_per_seq,
+                                                 bf16_t* olo, float oscale, float* of, int rows, int rows_per_seq,
                                                  const int* gather, int in_rows_per_seq, float* xcopy) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
@@ -109,15 +112,16 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
   const Row12 xv = load_row(x + src * C768, lane);
   if (xcopy) store_f32(xcopy + (int64_t)r * C768, xv, lane);
   const Row12 y = ln_row(xv, w, b, lane);
-  if (ob) store_bf16(ob + (int64_t)r * C768, y, lane);
-  if (olo) store_bf16_lo(olo + (int64_t)r * C768, y, lane);
+  if (olo) store_split(ob + (int64_t)r * C768, olo + (int64_t)r * C768, y, oscale, lane);
+  else if (ob) store_bf16(ob + (int64_t)r * C768, y, lane);
   if (of) store_f32(of + (int64_t)r * C768, y, lane);
 }
 
-void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float* out_f32,
-               int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy, hipStream_t s) {
-  hipLaunchKernelGGL(ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_f32, rows,
-                     rows_per_seq, gather, in_rows_per_seq, xcopy);
+void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float out_scale,
+               float* out_f32, int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy,
+               hipStream_t s) {
+  hipLaunchKernelGGL(ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_scale, out_f32,
+                     rows, rows_per_seq, gather, in_rows_per_seq, xcopy);
 }
 
 // ------------------------------------------------------------------ prompt block, part 1
@@ -498,8 +502,8 @@ __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptAr
       y.v[i] = make_float4(y.v[i].x * gw.x + gb.x, y.v[i].y * gw.y + gb.y, y.v[i].z * gw.z + gb.z,
                            y.v[i].w * gw.w + gb.w);
     }
-    store_bf16(a.out + (int64_t)r * C768, y, lane);
-    if (a.out_lo) store_bf16_lo(a.out_lo + (int64_t)r * C768, y, lane);
+    if (a.out_lo) store_split(a.out + (int64_t)r * C768, a.out_lo + (int64_t)r * C768, y, a.out_scale, lane);
+    else store_bf16(a.out + (int64_t)r * C768, y, lane);
   }
 }
 
@@ -539,7 +543,13 @@ __global__ __launch_bounds__(CE_THREADS) void ce_select_kernel(const CEArgs a) {
     for (int h = 0; h < CE_MAX_HEADS; ++h)
       if (h < a.heads) s += v[h];   // head order 0, 1, ... as before
     for (int h = CE_MAX_HEADS; h < a.heads; ++h) s += prob[h * a.Ls + i];
-    key[i] = s / (float)a.heads;
+    s = s / (float)a.heads;
+    if (a.keys_out || a.forced) {   // parity diagnostics only
+      const int slot = a.gidx_in[b * a.Ls + i];
+      if (a.keys_out) a.keys_out[(int64_t)b * a.keys_pitch + slot] = s;
+      if (a.forced) s = a.forced[(int64_t)b * a.keys_pitch + slot];
+    }
+    key[i] = s;
   }
   __syncthreads();
   const int Ln = a.Lz + a.keep;
@@ -589,7 +599,7 @@ void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s
 // to their 16x16 slots; pruned slots are exact zeros.
 __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int rows_per_seq, const int* slot2pos,
                                                          const float* w, const float* b, int B, int Lz, int Lx,
-                                                         bf16_t* feat, bf16_t* feat_lo, float* dbg) {
+                                                         bf16_t* feat, bf16_t* feat_lo, float fscale, float* dbg) {
   const int L = Lz + Lx;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= B * L) return;
@@ -597,16 +607,20 @@ __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int row
   int pos = s < Lz ? s : slot2pos[bs * Lx + (s - Lz)];
   Row12 y = zero_row();
   if (pos >= 0) y = ln_row(load_row(X + ((int64_t)bs * rows_per_seq + pos) * C768, lane), w, b, lane);
-  if (s >= Lz) store_bf16(feat + ((int64_t)bs * Lx + (s - Lz)) * C768, y, lane);
-  if (s >= Lz && feat_lo) store_bf16_lo(feat_lo + ((int64_t)bs * Lx + (s - Lz)) * C768, y, lane);
+  if (s >= Lz && feat_lo)
+    store_split(feat + ((int64_t)bs * Lx + (s - Lz)) * C768, feat_lo + ((int64_t)bs * Lx + (s - Lz)) * C768, y, fscale,
+                lane);
+  else if (s >= Lz)
+    store_bf16(feat + ((int64_t)bs * Lx + (s - Lz)) * C768, y, lane);
   if (dbg) store_f32(dbg + (int64_t)r * C768, y, lane);
 }
 
 void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
-                        int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float* feat_f32_dbg, hipStream_t s) {
+                        int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float feat_scale, float* feat_f32_dbg,
+                        hipStream_t s) {
   const int rows = B * (Lz + Lx);
   hipLaunchKernelGGL(final_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, X, rows_per_seq, slot2pos, w, b, B,
-                     Lz, Lx, feat, feat_lo, feat_f32_dbg);
+                     Lz, Lx, feat, feat_lo, feat_scale, feat_f32_dbg);
 }
 
 }  // namespace mmt

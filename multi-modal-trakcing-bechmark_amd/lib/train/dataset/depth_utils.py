@@ -9,8 +9,15 @@ import numpy as np
 
 
 def _imread(path, unchanged=False):
+    """cv2.imread(path) (IMREAD_COLOR: always 3 channels) + BGR2RGB for colour reads; cv2.imread(path, -1)
+    (IMREAD_UNCHANGED: 16-bit depth and grayscale stay single-channel, palette images expand to colour)
+    for the aux modality (depth_utils.py:79-85)."""
     from PIL import Image
     im = Image.open(path)
+    if not unchanged:
+        return np.asarray(im.convert('RGB'))
+    if im.mode == 'P':
+        im = im.convert('RGB')
     a = np.asarray(im)
     if a.ndim == 3 and a.shape[2] == 4:
         a = a[..., :3]

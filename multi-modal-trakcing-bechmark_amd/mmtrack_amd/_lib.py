@@ -77,6 +77,7 @@ SIGNATURES = {
     "mmt_get_state": (_I, [_P, _I, ctypes.POINTER(_D)]),
     "mmt_set_state": (_I, [_P, _I, ctypes.POINTER(_D)]),
     "mmt_debug_fetch": (_I, [_P, ctypes.c_char_p, _I, _P, ctypes.c_size_t]),
+    "mmt_debug_force_ce": (_I, [_P, _I, _P, ctypes.c_size_t]),
     "mmt_timing_enable": (_I, [_P, ctypes.c_char_p]),
     "mmt_timing_read": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_D), ctypes.POINTER(_D), ctypes.POINTER(_D)]),
     "mmt_xcorr": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P]),

@@ -216,11 +216,22 @@ class Engine:
     def debug(self, what: str, bi: int = 0) -> np.ndarray:
         S, C, fs = self.cfg.search_size, self.cfg.in_chans, self.feat_sz
         L_ = (self.cfg.template_size // 16) ** 2 + fs * fs
+        nce = max(len(self.cfg.ce_loc), 1)
         spec = {"crop": (np.uint8, (S, S, C)), "maps": (np.float32, (5, fs, fs)), "feat": (np.float32, (L_, 768)),
-                "removed": (np.int32, (fs * fs,)), "result": (np.float32, (8,))}[what]
+                "removed": (np.int32, (fs * fs,)), "result": (np.float32, (8,)),
+                "ce_keys": (np.float32, (nce, fs * fs))}[what]
         out = np.empty(spec[1], dtype=spec[0])
         self._check(self.lib.mmt_debug_fetch(self.h, what.encode(), bi, out.ctypes.data, out.nbytes))
         return out
+
+    def force_ce(self, slot: int, keys=None):
+        """Teacher-forced CE (parity diagnosis): keys [n_ce][Lx] by slot id, e.g. the reference's own CE
+        scores; None turns forcing off."""
+        if keys is None:
+            self._check(self.lib.mmt_debug_force_ce(self.h, slot, None, 0))
+            return
+        k = np.ascontiguousarray(keys, dtype=np.float32)
+        self._check(self.lib.mmt_debug_force_ce(self.h, slot, k.ctypes.data, k.size))
 
     # -- kernel timing probe (bench roofline)
     def timing_enable(self, cls: str | None):

@@ -62,6 +62,20 @@ def gen_config(seq_path, set_type):
     return rgb, aux, gt
 
 
+def sequence_list(seq_home, dataset_name):
+    """Sequence names as the reference lists them (test_rgbt_mgpus.py:155-177): VTUAV reads its split file
+    ('group/sequence' entries), the other datasets list the directories under seq_home."""
+    if dataset_name in ('VTUAVST', 'VTUAVLT'):
+        with open(join(seq_home, 'VTUAV-ST.txt' if dataset_name == 'VTUAVST' else 'VTUAV-LT.txt')) as f:
+            return [l for l in f.read().splitlines() if l.strip()]
+    return sorted(f for f in os.listdir(seq_home) if isdir(join(seq_home, f)))
+
+
+def result_name(seq_name, dataset_name):
+    """Result-file stem: VTUAV's 'group/sequence' entries save under the sequence part (test_rgbt_mgpus.py:70)."""
+    return seq_name.split('/')[-1] if 'VTUAV' in dataset_name else seq_name
+
+
 def synthetic_sequences(n, frames, H=480, W=640, C=6, seed=0):
     from mmtrack_amd import synth
     out = []
@@ -98,8 +112,7 @@ def save_result(path, result, modality):
 def run_sequence(seq_name, seq_home, dataset_name, yaml_name, num_gpu=1, epoch=60, debug=0, script_name='vipt',
                  modality='rgbt', out_root='.', synthetic=None, params_overrides=None):
     save_folder = join(out_root, f'{modality.upper()}_workspace', 'results', dataset_name, yaml_name)
-    seq_txt = seq_name.split('/')[1] if 'VTUAV' in dataset_name else seq_name
-    save_path = join(save_folder, seq_txt + '.txt')
+    save_path = join(save_folder, result_name(seq_name, dataset_name) + '.txt')
     os.makedirs(save_folder, exist_ok=True)
     if os.path.exists(save_path):
         print(f'-1 {seq_name}')
@@ -164,7 +177,7 @@ def run_batched_dataset(seqs, yaml_name, batch, modality, out_root, dataset_name
     jobs = [SeqJob(name, n, get, list(np.array(gt[0], dtype=np.float64))) for name, n, get, gt in seqs]
 
     def done(job):
-        save_result(join(save_folder, job.name + '.txt'), job.boxes, modality)
+        save_result(join(save_folder, result_name(job.name, dataset_name) + '.txt'), job.boxes, modality)
         print('{} , fps:{}'.format(job.name, (job.n_frames - 1) / max(job.seconds, 1e-9)))
 
     t0 = time.perf_counter()
@@ -205,7 +218,7 @@ def main(modality='rgbt', argv=None):
         syn = synthetic_sequences(args.synthetic, args.frames, C=3 if args.script_name == 'ostrack' else 6)
         names = [s[0] for s in syn]
     else:
-        names = sorted(f for f in os.listdir(args.seq_home) if isdir(join(args.seq_home, f)))
+        names = sequence_list(args.seq_home, args.dataset_name)
         if args.video:
             names = [args.video]
     from mmtrack_amd.sharding import rank_world, shard_indices

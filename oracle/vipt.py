@@ -146,12 +146,23 @@ def ce_block(x, sd, i, gi_t, gi_s, keep_ratio, box_mask_z, heads, trace=None):
     lens_t = gi_t.shape[1]
     removed = None
     if keep_ratio < 1:
+        gi_prev = gi_s
         x, gi_s, removed, sorted_attn = candidate_elimination(attn, x, lens_t, keep_ratio, gi_s, box_mask_z)
         if trace is not None and sorted_attn is not None:
             k = gi_s.shape[1]
             trace.setdefault("ce_margin", []).append(
                 float(((sorted_attn[:, k - 1] - sorted_attn[:, k]) / sorted_attn[:, k - 1]).min()))
             trace.setdefault("ce_keep", []).append(gi_s.clone())
+            # every surviving slot's score, by slot id (sequence 0): the teacher-forcing keys
+            lx = trace.get("lens_x")
+            if lx:
+                keys = torch.zeros(lx)
+                attn_t = attn[:1, :, :lens_t, lens_t:]
+                if box_mask_z is not None:
+                    m = box_mask_z[:1].unsqueeze(1).unsqueeze(-1).expand(-1, attn_t.shape[1], -1, attn_t.shape[-1])
+                    attn_t = attn_t[m].view(1, attn_t.shape[1], -1, attn_t.shape[-1])
+                keys[gi_prev[0].long()] = attn_t.mean(dim=2).mean(dim=1)[0]
+                trace.setdefault("ce_keys", []).append(keys)
     h = _lin(_ln(x, sd, p + ".norm2"), sd, p + ".mlp.fc1")
     h = F.gelu(h)
     x = x + _lin(h, sd, p + ".mlp.fc2")
@@ -175,6 +186,8 @@ def _recover(x, gi_s, removed, lens_x):
 def backbone(sd, z, x, cfg: NetCfg, box_mask_z=None, trace=None):
     B = x.shape[0]
     lens_z, lens_x = cfg.lens_z, cfg.lens_x
+    if trace is not None:
+        trace["lens_x"] = lens_x
     prompted = cfg.kind == "vipt" and cfg.prompt_type in ("vipt_shaw", "vipt_deep")
     if cfg.kind == "vipt":
         x_rgb, z_rgb = x[:, :3], z[:, :3]

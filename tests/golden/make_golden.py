@@ -197,12 +197,47 @@ def run_net(model, cfg, z, x, C):
     return out
 
 
-def net_fixture(name, model, cfg, sd, C, tsz, ssz, seeds):
+CE_LOG = []
+
+
+def install_ce_recorder():
+    """Record every candidate-elimination decision the reference makes: the score of each surviving slot
+    (by global slot id) and the relative gap between the last kept and the first removed score (the CE
+    boundary margin).  The reference function itself still makes the decision."""
+    import lib.models.layers.attn_blocks as ab
+    orig = ab.candidate_elimination
+
+    def recorder(attn, tokens, lens_t, keep_ratio, global_index, box_mask_z):
+        out = orig(attn, tokens, lens_t, keep_ratio, global_index, box_mask_z)
+        lens_s = attn.shape[-1] - lens_t
+        lens_keep = math.ceil(keep_ratio * lens_s)
+        if lens_keep < lens_s:
+            bs, hn = attn.shape[:2]
+            attn_t = attn[:, :, :lens_t, lens_t:]
+            if box_mask_z is not None:
+                m = box_mask_z.unsqueeze(1).unsqueeze(-1).expand(-1, hn, -1, lens_s)
+                attn_t = attn_t[m].view(bs, hn, -1, lens_s)
+            keys = attn_t.mean(dim=2).mean(dim=1)[0]
+            srt = torch.sort(keys, descending=True).values
+            CE_LOG.append((global_index[0].numpy().copy(), keys.numpy().copy(),
+                           float((srt[lens_keep - 1] - srt[lens_keep]) / srt[lens_keep - 1])))
+        return out
+    ab.candidate_elimination = recorder
+
+
+def net_fixture(name, model, cfg, sd, C, tsz, ssz, seeds, feat_seeds=2):
     res = {"seeds": np.array(seeds)}
+    lx = (ssz // 16) ** 2
     for j, (sz, ss) in enumerate(seeds):
         z = preprocess(synth.make_patch(sz, tsz, C))
         x = preprocess(synth.make_patch(ss, ssz, C))
+        CE_LOG.clear()
         out = run_net(model, cfg, z, x, C)
+        keys = np.zeros((max(len(CE_LOG), 1), lx), np.float32)
+        for st, (gi, kv, _) in enumerate(CE_LOG):
+            keys[st, gi.astype(np.int64)] = kv
+        res[f"ce_keys_{j}"] = keys
+        res[f"ce_margin_{j}"] = np.array([m for _, _, m in CE_LOG], dtype=np.float64)
         feat_sz = ssz // 16
         resp = (synth_hann(feat_sz) * out["score_map"]).flatten()
         top = torch.sort(resp, descending=True).values
@@ -211,12 +246,13 @@ def net_fixture(name, model, cfg, sd, C, tsz, ssz, seeds):
         res[f"offset_map_{j}"] = out["offset_map"].numpy()
         res[f"pred_boxes_{j}"] = out["pred_boxes"].numpy()
         res[f"removed_{j}"] = np.concatenate([r.numpy() for r in out["removed_indexes_s"]], axis=1).astype(np.int64)
-        res[f"feat_rows_{j}"] = out["backbone_feat"][0, ::8].numpy()
+        if j < feat_seeds:
+            res[f"feat_rows_{j}"] = out["backbone_feat"][0, ::8].numpy()
         res[f"feat_sum_{j}"] = np.array([float(out["backbone_feat"].double().sum())])
         res[f"resp_argmax_{j}"] = np.array([int(torch.argmax(resp))])
         res[f"resp_top2gap_{j}"] = np.array([float((top[0] - top[1]) / top[0])])
     np.savez_compressed(os.path.join(HERE, f"net_{name}.npz"), **res)
-    print("wrote net", name)
+    print("wrote net", name, "CE margins", [np.round(res[f"ce_margin_{j}"], 6).tolist() for j in range(len(seeds))])
 
 
 def synth_hann(sz):
@@ -307,11 +343,15 @@ def main():
     sys.path.insert(0, os.path.join(REF, "ViPT"))
     torch.set_num_threads(8)
     from lib.models.vipt import build_viptrack, build_ostrack
+    install_ce_recorder()
 
     mani = {}
-    # --- ViPT deep / shaw, RGB-T and RGB-D yamls (C2, C3)
-    for yaml_name, seeds in (("deep_rgbt", [(101, 201), (102, 202)]), ("deep_rgbd", [(103, 203)]),
-                             ("shaw_rgbt", [(104, 204)])):
+    # --- ViPT deep / shaw, RGB-T and RGB-D yamls (C2, C3): 8 crop pairs each (the first ones are the
+    # round-1 fixtures, unchanged)
+    more = lambda base: [(base + k, base + 100 + k) for k in range(1, 8)]
+    for yaml_name, seeds in (("deep_rgbt", [(101, 201), (102, 202)] + more(110)[:6]),
+                             ("deep_rgbd", [(103, 203)] + more(120)),
+                             ("shaw_rgbt", [(104, 204)] + more(130))):
         cfg = load_cfg(yaml_name)
         model = build_viptrack(cfg, training=False).eval()
         pt = cfg.TRAIN.PROMPT.TYPE
@@ -325,12 +365,14 @@ def main():
     sd = synth.make_state_dict(0, kind="ostrack", search_size=384, template_size=192)
     model.load_state_dict(sd, strict=True)
     mani["ostrack384"] = manifest(model)
-    net_fixture("ostrack384", model, cfg, sd, 3, 192, 384, [(105, 205)])
+    net_fixture("ostrack384", model, cfg, sd, 3, 192, 384, [(105, 205)] + more(140))
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(mani, f)
     # --- tracker-level sequences
     sd = synth.make_state_dict(0, kind="vipt", prompt_type="vipt_deep")
     tracker_fixture("deep_rgbt", "deep_rgbt", sd, 10, 31, 480, 640, 6, (300.0, 200.0, 40.0, 30.0))
+    # a second, longer sequence at DepthTrack's frame shape (C3) with a different target
+    tracker_fixture("deep_rgbd", "deep_rgbd", sd, 20, 47, 360, 640, 6, (220.0, 140.0, 52.0, 44.0))
     crop_fixture()
     dimp_fixture()
 

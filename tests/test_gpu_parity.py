@@ -103,15 +103,24 @@ def test_network_matches_reference_golden(engines, name):
         res = eng.debug("result")
         removed = eng.debug("removed")
         ref_removed = g[f"removed_{j}"][0]
+        # every recorded reference CE margin is >= 2.5e-4 relative, far above the split products' error
+        assert min(g[f"ce_margin_{j}"]) > 1e-5
         np.testing.assert_array_equal(np.sort(removed[:len(ref_removed)]), np.sort(ref_removed))
+        keys = eng.debug("ce_keys")
+        ref_keys = g[f"ce_keys_{j}"]
+        m = ref_keys > 0
+        rel = np.abs(keys[m] - ref_keys[m]) / ref_keys[m]
+        print(f"{name}[{j}] CE score max rel err {rel.max():.2e} (reference min margin {min(g[f'ce_margin_{j}']):.2e})")
+        assert rel.max() < 1e-4
         gs = g[f"score_map_{j}"][0, 0]
         print(f"{name}[{j}] fp32-faithful max|dscore| {np.abs(maps[0] - gs).max():.2e}")
         np.testing.assert_allclose(maps[0], gs, atol=1e-3)
         np.testing.assert_allclose(maps[1:3], g[f"size_map_{j}"][0], atol=1e-3)
         np.testing.assert_allclose(maps[3:5], g[f"offset_map_{j}"][0], atol=3e-3)
         assert int(res[5]) == int(g[f"resp_argmax_{j}"][0]), "windowed argmax differs from the reference"
-        feat = eng.debug("feat")
-        np.testing.assert_allclose(feat[::8], g[f"feat_rows_{j}"], atol=5e-3)
+        if f"feat_rows_{j}" in g.files:
+            feat = eng.debug("feat")
+            np.testing.assert_allclose(feat[::8], g[f"feat_rows_{j}"], atol=5e-3)
 
 
 @pytest.mark.parametrize("name", ["deep_rgbt", "ostrack384"])
@@ -145,9 +154,10 @@ def test_network_bf16_statistics(engines, name):
     assert np.median(ious) >= 0.9
 
 
-def test_tracker_sequence_matches_reference(engines):
-    """10-frame sequence of the reference ViPTTrack (golden) vs the engine, same frames."""
-    g = np.load(os.path.join(GOLDEN, "tracker_deep_rgbt.npz"))
+@pytest.mark.parametrize("seq", ["deep_rgbt", "deep_rgbd"])
+def test_tracker_sequence_matches_reference(engines, seq):
+    """Sequences of the reference ViPTTrack (golden: 10 frames 640x480, 20 frames 640x360) vs the engine."""
+    g = np.load(os.path.join(GOLDEN, f"tracker_{seq}.npz"))
     seed, n, H, W, C = [int(v) for v in g["meta"]]
     frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
     eng = engines("deep_rgbt", "fp32")

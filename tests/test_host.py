@@ -180,3 +180,48 @@ def test_benchmark_scripts_dry_run(mod):
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "[benchmark]" in r.stdout
+
+
+def test_vtuav_sequence_list_and_result_names(tmp_path):
+    """VTUAV lists 'group/sequence' entries in VTUAV-ST.txt / VTUAV-LT.txt (test_rgbt_mgpus.py:163-170)
+    and saves results under the sequence part; other datasets list directories."""
+    from mmtrack_amd import workspace as ws
+    st = tmp_path / "short-term"
+    (st / "animal_001" / "rgb").mkdir(parents=True)
+    (st / "VTUAV-ST.txt").write_text("animal/animal_001\nbike/bike_003\n")
+    assert ws.sequence_list(str(st), "VTUAVST") == ["animal/animal_001", "bike/bike_003"]
+    lt = tmp_path / "long-term"
+    lt.mkdir()
+    (lt / "VTUAV-LT.txt").write_text("car/car_010\n")
+    assert ws.sequence_list(str(lt), "VTUAVLT") == ["car/car_010"]
+    assert ws.result_name("animal/animal_001", "VTUAVST") == "animal_001"
+    (tmp_path / "las" / "seqB").mkdir(parents=True)
+    (tmp_path / "las" / "seqA").mkdir(parents=True)
+    (tmp_path / "las" / "note.txt").write_text("")
+    assert ws.sequence_list(str(tmp_path / "las"), "LasHeR") == ["seqA", "seqB"]
+    assert ws.result_name("seqA", "LasHeR") == "seqA"
+
+
+def test_imread_modes(tmp_path):
+    """Colour reads are 3-channel RGB whatever the file mode (cv2.imread IMREAD_COLOR + BGR2RGB); unchanged
+    reads keep 16-bit / grayscale single-channel and expand palettes (cv2.imread(path, -1))."""
+    from PIL import Image
+    from lib.train.dataset.depth_utils import _imread, get_x_frame
+    g = np.arange(48, dtype=np.uint8).reshape(6, 8)
+    Image.fromarray(g, mode="L").save(tmp_path / "g.png")
+    pal = Image.fromarray(g % 4, mode="P")
+    pal.putpalette([0, 0, 0, 255, 0, 0, 0, 255, 0, 0, 0, 255] + [0] * (256 * 3 - 12))
+    pal.save(tmp_path / "p.png")
+    d16 = (np.arange(48, dtype=np.uint16) * 1000).reshape(6, 8)
+    Image.fromarray(d16).save(tmp_path / "d.png")
+    a = _imread(str(tmp_path / "g.png"))
+    assert a.shape == (6, 8, 3) and np.array_equal(a[..., 0], g) and np.array_equal(a[..., 2], g)
+    p = _imread(str(tmp_path / "p.png"))
+    assert p.shape == (6, 8, 3)
+    assert np.array_equal(p[g % 4 == 1], np.tile([255, 0, 0], ((g % 4 == 1).sum(), 1)))
+    assert _imread(str(tmp_path / "g.png"), unchanged=True).shape == (6, 8)
+    assert _imread(str(tmp_path / "p.png"), unchanged=True).shape == (6, 8, 3)
+    d = _imread(str(tmp_path / "d.png"), unchanged=True)
+    assert d.ndim == 2 and int(d.max()) == 47000
+    f = get_x_frame(str(tmp_path / "g.png"), str(tmp_path / "g.png"), dtype="rgbrgb")
+    assert f.shape == (6, 8, 6) and f.dtype == np.uint8

@@ -81,5 +81,28 @@ def test_bench_aggregate_gloo(tmp_path):
     mp.start_processes(_bench_reduce_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     for r in range(world):
-        value, elapsed = eval((tmp_path / f"b{r}.txt").read_text())
-        assert elapsed == 2.0 and value == pytest.approx(2 * 8 * 10 / 2.0)
+        value, elapsed, w = eval((tmp_path / f"b{r}.txt").read_text())
+        assert w == world and elapsed == 2.0 and value == pytest.approx(2 * 8 * 10 / 2.0)
+
+
+def test_bench_spawns_ranks_for_gpus_flag():
+    """`bench.py --gpus 2` without a torchrun environment launches its two rank processes itself (before
+    any GPU call) and rank 0 reports n_gpus = 2 with the whole-job rate; a torchrun world that disagrees
+    with --gpus is refused."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry", "--steps", "20",
+                        "--warmup", "2", "--batch", "8"], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 16
+    assert line["value"] == pytest.approx(2 * 8 * 20 / (line["ms_per_step"] * 20 / 1e3), rel=1e-3)
+    env1 = dict(env, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry"], capture_output=True,
+                       text=True, env=env1, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

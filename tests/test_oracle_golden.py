@@ -39,12 +39,19 @@ def test_oracle_network_matches_reference(name):
     for j, (sz, ss) in enumerate(g["seeds"]):
         z = ocrop.preprocess(synth.make_patch(int(sz), cfg.template_size, spec["C"]))
         x = ocrop.preprocess(synth.make_patch(int(ss), cfg.search_size, spec["C"]))
-        out = ov.forward(sd, z, x, cfg, ov.ce_template_mask(cfg))
+        tr = {}
+        out = ov.forward(sd, z, x, cfg, ov.ce_template_mask(cfg), trace=tr)
         removed = torch.cat(out["removed_indexes_s"], dim=1).numpy()
         np.testing.assert_array_equal(removed, g[f"removed_{j}"])
         for k in ("score_map", "size_map", "offset_map", "pred_boxes"):
             np.testing.assert_allclose(out[k].numpy(), g[f"{k}_{j}"], rtol=1e-4, atol=1e-5)
-        np.testing.assert_allclose(out["backbone_feat"][0, ::8].numpy(), g[f"feat_rows_{j}"], rtol=1e-4, atol=1e-4)
+        if f"feat_rows_{j}" in g.files:
+            np.testing.assert_allclose(out["backbone_feat"][0, ::8].numpy(), g[f"feat_rows_{j}"], rtol=1e-4,
+                                       atol=1e-4)
+        # the CE scores of every slot and the boundary margins the reference recorded
+        np.testing.assert_allclose(np.stack([k.numpy() for k in tr["ce_keys"]]), g[f"ce_keys_{j}"], rtol=1e-4,
+                                   atol=1e-8)
+        np.testing.assert_allclose(tr["ce_margin"], g[f"ce_margin_{j}"], rtol=2e-2, atol=2e-6)
         resp = (ov.hann2d(cfg.feat_sz) * out["score_map"]).flatten()
         assert int(torch.argmax(resp)) == int(g[f"resp_argmax_{j}"][0])
 
@@ -58,8 +65,9 @@ def test_crop_geometry_matches_reference():
         assert rf == g[f"rf_{j}"][0]
 
 
-def test_oracle_tracker_matches_reference():
-    g = np.load(os.path.join(GOLDEN, "tracker_deep_rgbt.npz"))
+@pytest.mark.parametrize("name", ["deep_rgbt", "deep_rgbd"])
+def test_oracle_tracker_matches_reference(name):
+    g = np.load(os.path.join(GOLDEN, f"tracker_{name}.npz"))
     seed, n, H, W, C = [int(v) for v in g["meta"]]
     frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
     sd = synth.make_state_dict(0, kind="vipt", prompt_type="vipt_deep")
