@@ -69,8 +69,11 @@ typedef struct mmt_config {
   int max_batch;           /* sequences (slots) this engine tracks concurrently    */
   int use_graphs;          /* capture the per-frame launch sequence in a hipGraph   */
   int debug_outputs;       /* keep crops / score maps / features for parity tests   */
-  int precision;           /* 0: bf16 GEMM operands (fp32 accumulate, fp32 residual / LN / softmax);
-                              1: fp32-faithful "bf16x3" split products (hi*hi + lo*hi + hi*lo)     */
+  int precision;           /* 1 (parity mode, what the Python tracker uses): fp32-faithful "f16x3"
+                              products -- fp16 hi/lo halves of power-of-two range-scaled operands,
+                              hi*hi + lo*hi + hi*lo on the fp16 MFMA: the fp32 reference's CE decisions
+                              and argmax; 0: plain bf16 operands (fp32 accumulate / residual / LN /
+                              softmax), ~2.3x faster, CE decisions and boxes drift from the reference */
 } mmt_config;
 
 /* lifecycle */

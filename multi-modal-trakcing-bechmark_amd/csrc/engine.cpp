@@ -129,6 +129,7 @@ struct mmt_engine {
         *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
   int *gidx0 = nullptr, *gidx1 = nullptr, *slot2pos = nullptr, *gather = nullptr, *removed = nullptr;
+  float* splitk_ws = nullptr;   // [2 stream halves][kSplitKWsElems] fp32 split-K partials (few-tile GEMMs)
   uint8_t* dbg_patch = nullptr;
   CropParam* params_dev = nullptr;
   SeqState* state_dev = nullptr;      // [max_batch] tracker state per slot (device-resident)
@@ -554,6 +555,7 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->state_dev, (size_t)B * sizeof(SeqState)}, {(void**)&e->out_dev, (size_t)B * sizeof(TrackOut)},
   };
   reqs.push_back({(void**)&e->zero, 256});
+  reqs.push_back({(void**)&e->splitk_ws, (size_t)2 * kSplitKWsElems * 4});
   if (e->split) {
     const std::vector<Req> lo = {
         {(void**)&e->A_rgb_l, (size_t)B * L * C * 2},   {(void**)&e->A_aux_l, (size_t)B * L * C * 2},
@@ -649,9 +651,9 @@ void probe_collect(mmt_engine* e) {
 }
 
 // ---------------------------------------------------------------- the per-frame launch sequence
-GemmArgs dense(mmt_engine* e, const bf16_t* A, const bf16_t* Al, int64_t lda, const bf16_t* W, const bf16_t* Wl,
-               int64_t ldw, const float* bias, void* Cp, void* Cl, int64_t ldc, const float* R, int64_t ldr, int M,
-               int N, int K) {
+GemmArgs dense(mmt_engine* e, float* ws, const bf16_t* A, const bf16_t* Al, int64_t lda, const bf16_t* W,
+               const bf16_t* Wl, int64_t ldw, const float* bias, void* Cp, void* Cl, int64_t ldc, const float* R,
+               int64_t ldr, int M, int N, int K) {
   GemmArgs a{};
   a.g[0] = GemmGroup{A, Al, lda, W, Wl, ldw, bias, Cp, Cl, ldc, R, ldr};
   a.groups = 1;
@@ -661,9 +663,12 @@ GemmArgs dense(mmt_engine* e, const bf16_t* A, const bf16_t* Al, int64_t lda, co
   a.N = N;
   a.K = K;
   a.amode = A_DENSE;
-  // No split-K inside the engine: it would change the fp32 summation order with the batch size, and a
-  // sequence's boxes must not depend on how many sequences share its launch (test_batch_equals_single).
-  a.ws = nullptr;
+  // GEMMs with few 64 x 64 tiles and a long K (small batches: fc2 / proj / head convs at one or two
+  // sequences) split K over workgroups into this stream half's workspace, reduced in a fixed order with the
+  // epilogue (gemm.hip).  The summation order then depends on the batch size: results agree across batch
+  // sizes to fp32 rounding, not bit for bit (test_batch_equals_single).
+  a.ws = ws;
+  a.ws_elems = ws ? kSplitKWsElems : 0;
   return a;
 }
 
@@ -698,6 +703,9 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
   const auto& c = e->cfg;
   const int Lz = e->Lz, Lx = e->Lx, L = e->L;
   // per-launch activation views: this launch covers launch-relative sequences [r0, r0 + n)
+  // split-K workspace per stream half; parity mode only (in bf16 a different summation order can flip a
+  // bf16 rounding and, through CE, a box: that mode keeps batch-size-independent results instead)
+  float* const q_ws = e->split ? e->splitk_ws + (r0 > 0 ? (size_t)kSplitKWsElems : 0) : nullptr;
   auto* const q_X = off(e->X, (size_t)r0 * (size_t)L * C);
   auto* const q_X2 = off(e->X2, (size_t)r0 * (size_t)L * C);
   auto* const q_tok_rgb = off(e->tok_rgb, (size_t)r0 * (size_t)L * C);
@@ -760,7 +768,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
   float* X = q_X;
   float* X2 = q_X2;
   if (vipt) {
-    GemmArgs g = dense(e, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, q_tok_rgb, nullptr, C, nullptr, 0,
+    GemmArgs g = dense(e, q_ws, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, q_tok_rgb, nullptr, C, nullptr, 0,
                        n * L, C, C);
     g.g[1] = GemmGroup{A_aux, A_aux_l, C, e->pep_w, e->pep_wl, C, e->pep_b, q_tok_aux, nullptr, C, nullptr, 0};
     g.groups = 2;
@@ -768,7 +776,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
     g.g[1].inv = 1.0f / (kPixScale * e->pep_s);
     run_gemm(e, s, "patch", g, EPI_F32);
   } else {
-    GemmArgs g = dense(e, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, X, nullptr, C, e->pos, C, n * L, C, C);
+    GemmArgs g = dense(e, q_ws, A_rgb, A_rgb_l, C, e->pe_w, e->pe_wl, C, e->pe_b, X, nullptr, C, e->pos, C, n * L, C, C);
     g.pos_rows = L;
     run_gemm(e, s, "patch", scaled(g, kPixScale * e->pe_s, 1.0f), EPI_POS_F32);
   }
@@ -845,7 +853,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
       layernorm(X, w.n1w, w.n1b, q_Hn, q_Hn_l, w.ln1_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
     }
     run_gemm(e, s, "qkv",
-             scaled(dense(e, q_Hn, q_Hn_l, C, w.qkv_w, w.qkv_wl, C, w.qkv_b, q_QKV, q_QKV_l, 3 * C, nullptr, 0,
+             scaled(dense(e, q_ws, q_Hn, q_Hn_l, C, w.qkv_w, w.qkv_wl, C, w.qkv_b, q_QKV, q_QKV_l, 3 * C, nullptr, 0,
                           n * Na, 3 * C, C),
                     w.ln1_s * w.qkv_s, w.qkv_os),
              EPI_BF16);
@@ -868,7 +876,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
     attention(aa, s);
     probe_end(e, s, "attn");
     run_gemm(e, s, "proj",
-             scaled(dense(e, q_O, q_O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
+             scaled(dense(e, q_ws, q_O, q_O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
                     w.qkv_os * w.proj_s, 1.0f),
              EPI_RESID_F32);
     if (ce) {  // attn_blocks.py:99-101
@@ -904,12 +912,12 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
     }
     const int Nm = Lz + Ls;
     run_gemm(e, s, "fc1",
-             scaled(dense(e, q_Hn, q_Hn_l, C, w.fc1_w, w.fc1_wl, C, w.fc1_b, q_Hm, q_Hm_l, MLPD, nullptr, 0,
+             scaled(dense(e, q_ws, q_Hn, q_Hn_l, C, w.fc1_w, w.fc1_wl, C, w.fc1_b, q_Hm, q_Hm_l, MLPD, nullptr, 0,
                           n * Nm, MLPD, C),
                     w.ln2_s * w.fc1_s, w.fc1_os),
              EPI_GELU_BF16);
     run_gemm(e, s, "fc2",
-             scaled(dense(e, q_Hm, q_Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C, n * Nm, C,
+             scaled(dense(e, q_ws, q_Hm, q_Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C, n * Nm, C,
                           MLPD),
                     w.fc1_os * w.fc2_s, 1.0f),
              EPI_RESID_F32);
@@ -920,7 +928,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
   // CENTER head: conv1 of the three branches fused (N = 3*hc), then per-branch grouped convs
   const int hc = c.head_channels, fs = e->fs, M = n * Lx;
   {
-    GemmArgs g = dense(e, q_feat, q_feat_l, C, e->hw1, e->hw1l, 9 * C, e->hb1, q_h1, q_h1_l, 3 * hc, nullptr, 0,
+    GemmArgs g = dense(e, q_ws, q_feat, q_feat_l, C, e->hw1, e->hw1l, 9 * C, e->hb1, q_h1, q_h1_l, 3 * hc, nullptr, 0,
                        M, 3 * hc, 9 * C);
     g.amode = A_CONV3;
     g.conv_hw = fs;
@@ -930,7 +938,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
   const int ch[4] = {hc, hc / 2, hc / 4, hc / 8};
   for (int j = 0; j < 3; ++j) {   // conv2, conv3, conv4
     const int ci = ch[j], co = ch[j + 1];
-    GemmArgs g = dense(e, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, M, co,
+    GemmArgs g = dense(e, q_ws, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, M, co,
                        9 * ci);
     for (int k = 0; k < 3; ++k) {
       const bf16_t *A, *Al;
@@ -1146,6 +1154,9 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess)
     return MMT_E_HIP;
+  // f16x3 GEMMs are 3x longer, so halves of 16 sequences still fill the chip and the two streams fill each
+  // other's tile-quantisation tails (+8 % at 32 sequences; plain bf16 lost 4 % there)
+  if (e->split) e->overlap_min = 32;
   if (const char* ov = std::getenv("MMT_OVERLAP_MIN")) e->overlap_min = std::atoi(ov);
   build_expected(e.get());
   e->frame_dev.assign((size_t)c.max_batch * kRing, nullptr);

@@ -1014,6 +1014,192 @@ static void launch256_epi(const GemmArgs& a, int epi, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// f16x3 (split) 256 x 256 tile in the 8-phase structure of gemm256_kernel, at BK = 32: a half-tile slot
+// (16 KB) holds 128 rows x 32 k of BOTH halves (hi image, then lo image), so the LDS stays at 128 KB and
+// the per-phase load is still two buffer_load ... lds per lane (hi, lo).  The 2-barrier K-loop of
+// gemm_kernel stalls every K-step on the tile it has just asked for (all its tile shapes measured
+// 240-260 TF/s, 29-31 % of the pipe); here loads run 5-6 phases ahead and the two wave groups (waves 0-3,
+// 4-7, one barrier apart) alternate MFMA and fragment/load work on every SIMD.  Each phase multiplies
+// one 128 x 128 quadrant: per wave 64 x 32 = 4 x 2 fragment pairs x 3 products = 24 MFMAs.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 8192];
+  const GemmGroup& g = args.g[blockIdx.z];
+  const int M = args.M, K = args.K;
+  const int tiles_m = (M + 255) / 256, tiles_n = args.N / 256, ntiles = tiles_m * tiles_n;
+  const int b = blockIdx.x, x = b & 7, j = b >> 3;
+  const int q = ntiles >> 3, r8 = ntiles & 7;
+  const int id = (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + j;
+  int tm, tn;
+  tile_of(id, tiles_m, tiles_n, args.gm, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  GEMM_STAMP(0);
+
+  // half-tile loads: a wave-instruction fills 16 rows x 64 B (swzk<32> image, source chunk pre-swizzled)
+  const int chunk = ((lane & 3) ^ ((lane >> 4) & 2)) * 16;
+  const int lrow = wave * 16 + (lane >> 2);
+  const rsrc_t rA = make_rsrc(g.A + (int64_t)m0 * g.lda, (int64_t)(M - m0) * g.lda * 2);
+  const rsrc_t rAl = make_rsrc(g.A_lo + (int64_t)m0 * g.lda, (int64_t)(M - m0) * g.lda * 2);
+  const rsrc_t rW = make_rsrc(g.W + (int64_t)n0 * g.ldw, (int64_t)256 * g.ldw * 2);
+  const rsrc_t rWl = make_rsrc(g.W_lo + (int64_t)n0 * g.ldw, (int64_t)256 * g.ldw * 2);
+  const uint32_t va = (uint32_t)(lrow * g.lda * 2 + chunk), vw = (uint32_t)(lrow * g.ldw * 2 + chunk);
+  const uint32_t a128 = 128u * g.lda * 2, w128 = 128u * g.ldw * 2;
+  const int nk = K / 32, NL = 4 * nk;
+
+  // half-tile L (pos = L & 3: 0 A rows 0-127, 1 W rows 0-127, 2 W rows 128-255, 3 A rows 128-255)
+  auto issue = [&](int L, auto pos_c) {
+    constexpr int pos = decltype(pos_c)::value;
+    const int kt = L >> 2;
+    bf16_t* dst = smem + ((kt & 1) * 4 + pos) * 8192 + wave * 512;
+    const int soff = kt * 64;
+    const bool isA = pos == 0 || pos == 3;
+    const uint32_t v = pos == 0 ? va : pos == 3 ? va + a128 : pos == 1 ? vw : vw + w128;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rW, (lptr_t)dst, 16, v, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rAl : rWl, (lptr_t)(dst + 4096), 16, v, soff, 0, 0);
+  };
+  auto wait_vm = [&](int n) {   // n half-tiles (2 loads each) may stay in flight
+    if (n >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x4 acc[4][4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[a][i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 Ah[4], Al[4], B0h[2], B0l[2], B1h[2], B1l[2];
+  const int c = lane >> 4;
+  auto read_a = [&](const bf16_t* S) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 64 + i * 16 + (lane & 15);
+      Ah[i] = *reinterpret_cast<const bf16x8*>(S + swzk<32>(row, c));
+      Al[i] = *reinterpret_cast<const bf16x8*>(S + 4096 + swzk<32>(row, c));
+    }
+  };
+  auto read_b = [&](const bf16_t* S, bf16x8 (&Bh)[2], bf16x8 (&Bl)[2]) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = wc * 32 + jj * 16 + (lane & 15);
+      Bh[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<32>(row, c));
+      Bl[jj] = *reinterpret_cast<const bf16x8*>(S + 4096 + swzk<32>(row, c));
+    }
+  };
+  auto mma = [&](f32x4 (&C)[4][2], const bf16x8 (&Bh)[2], const bf16x8 (&Bl)[2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bh[jj], Ah[i], C[i][jj]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bl[jj], Ah[i], C[i][jj]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bh[jj], Al[i], C[i][jj]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // half-tiles that may stay in flight at phase P's wait (before its own load): everything issued
+  // after the last one phase P + 1 reads (p0: B1 = P+2, p1: A1 = P+2, p2: A1 = P+1, p3: B0' = P+2)
+  auto n_after = [&](int P, int p) {
+    const int need = P + (p == 2 ? 1 : 2);
+    return max(min(P + 6, NL) - need - 1, 0);
+  };
+  auto ktile = [&](int kt, auto steady_c) {
+    constexpr bool STEADY = decltype(steady_c)::value;
+    const bf16_t* S = smem + (kt & 1) * 4 * 8192;
+    const int P0 = 4 * kt;
+    read_b(S + 8192, B0h, B0l);
+    read_a(S);
+    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0, 0));
+    if (STEADY || P0 + 6 < NL) issue(P0 + 6, std::integral_constant<int, 2>{});
+    __builtin_amdgcn_s_barrier();
+    mma(acc[0], B0h, B0l);
+    __builtin_amdgcn_s_barrier();
+    read_b(S + 2 * 8192, B1h, B1l);
+    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 1, 1));
+    if (STEADY || P0 + 7 < NL) issue(P0 + 7, std::integral_constant<int, 3>{});
+    __builtin_amdgcn_s_barrier();
+    mma(acc[1], B1h, B1l);
+    __builtin_amdgcn_s_barrier();
+    read_a(S + 3 * 8192);
+    if (STEADY) asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); else wait_vm(n_after(P0 + 2, 2));
+    if (STEADY || P0 + 8 < NL) issue(P0 + 8, std::integral_constant<int, 0>{});
+    __builtin_amdgcn_s_barrier();
+    mma(acc[2], B1h, B1l);
+    __builtin_amdgcn_s_barrier();
+    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 3, 3));
+    if (STEADY || P0 + 9 < NL) issue(P0 + 9, std::integral_constant<int, 1>{});
+    __builtin_amdgcn_s_barrier();
+    mma(acc[3], B0h, B0l);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  issue(0, std::integral_constant<int, 0>{});
+  issue(1, std::integral_constant<int, 1>{});
+  issue(2, std::integral_constant<int, 2>{});
+  issue(3, std::integral_constant<int, 3>{});
+  if (nk > 1) {
+    issue(4, std::integral_constant<int, 0>{});
+    issue(5, std::integral_constant<int, 1>{});
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  GEMM_STAMP(1);
+  if (wr) __builtin_amdgcn_s_barrier();   // stagger: waves 4-7 one barrier behind
+
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) ktile(kt, std::true_type{});
+  for (; kt < nk; ++kt) ktile(kt, std::false_type{});
+  if (!wr) __builtin_amdgcn_s_barrier();  // balance the stagger
+  GEMM_STAMP(2);
+
+  constexpr int QA[4] = {0, 0, 1, 1}, QB[4] = {0, 1, 1, 0};
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + QA[qd] * 128 + wr * 64 + i * 16 + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+        store4<EPI, true>(g, args, m, n0 + QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, acc[qd][i][jj]);
+    }
+  GEMM_STAMP(3);
+}
+
+template <int EPI>
+static void launch256s(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  const int tiles_m = (a.M + 255) / 256;
+  a.gm = tiles_m < 4 ? tiles_m : 4;
+  hipLaunchKernelGGL(gemm256s_kernel<EPI>, dim3(tiles_m * (a.N / 256), 1, a.groups), dim3(512), 0, s, a);
+}
+
+static bool launch256s_epi(const GemmArgs& a, int epi, hipStream_t s) {
+  if (a.N % 256 || a.K % 32 || a.K < 64 || a.amode != A_DENSE) return false;
+  switch (epi) {
+    case EPI_BF16: return launch256s<EPI_BF16>(a, s), true;
+    case EPI_GELU_BF16: return launch256s<EPI_GELU_BF16>(a, s), true;
+    case EPI_RESID_F32: return launch256s<EPI_RESID_F32>(a, s), true;
+    case EPI_F32: return launch256s<EPI_F32>(a, s), true;
+    case EPI_POS_F32: return launch256s<EPI_POS_F32>(a, s), true;
+    default: return false;
+  }
+}
+
 template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int ST, int BK = 64>
 static void launch_one(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
@@ -1112,6 +1298,36 @@ static int g_force_cfg = -1;   // tuning override (mmt_gemm_force_config), -1 = 
 
 template <bool SPLIT>
 static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
+  if constexpr (SPLIT) {   // tuning override of the f16x3 tile (MMT_SPLIT_CFG), dense A only
+    static const int scfg = getenv("MMT_SPLIT_CFG") ? atoi(getenv("MMT_SPLIT_CFG")) : -1;
+    if (scfg >= 0 && a.amode == A_DENSE) {
+      switch (scfg) {
+        case 0: return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);
+        case 1: return launch_cfg<256, 128, 4, 2, true, 3, 32>(a, epi, s);
+        case 2: return launch_cfg<128, 128, 2, 2, true, 2, 64>(a, epi, s);
+        case 3: return launch_cfg<128, 128, 2, 2, true, 3, 32>(a, epi, s);
+        case 4: return launch_cfg<256, 128, 4, 2, true, 2, 32>(a, epi, s);
+        case 5: return launch_cfg<128, 256, 2, 4, true, 3, 32>(a, epi, s);
+        case 6: return launch_cfg<256, 256, 2, 4, true, 2, 32>(a, epi, s);
+        case 7: return launch_cfg<128, 128, 4, 2, true, 3, 32>(a, epi, s);
+        case 8: return launch_cfg<128, 64, 2, 2, true, 2, 64>(a, epi, s);
+        case 9: return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
+        case 10: return launch_cfg<128, 128, 2, 2, true, 2, 32>(a, epi, s);
+        case 11: return launch_cfg<128, 64, 2, 2, true, 2, 32>(a, epi, s);
+        case 12: return launch_cfg<128, 128, 4, 2, true, 4, 32>(a, epi, s);
+        case 13: return launch_cfg<128, 256, 2, 4, true, 2, 32>(a, epi, s);
+        case 14: if (launch256s_epi(a, epi, s)) return; break;
+        case 15: if (a.N >= 2048 && launch256s_epi(a, epi, s)) return; break;
+        default: break;
+      }
+    }
+  }
+  if constexpr (SPLIT) {
+    // f16x3: the 8-phase 256 x 256 kernel where there are enough 256-wide column tiles (qkv, fc1: 250-300
+    // TF/s vs 240-250 for the 2-barrier 128 x 128 kernel); N = 768 stays on 128-row tiles (3 column tiles of
+    // 256 leave most CUs idle)
+    if (a.N >= 2048 && (a.M + 255) / 256 * (a.N / 256) * a.groups >= 128 && launch256s_epi(a, epi, s)) return;
+  }
   if constexpr (!SPLIT) {
     if (g_force_cfg >= 0 && a.amode == A_DENSE) {
       switch (g_force_cfg) {

@@ -35,7 +35,7 @@ class BaseTracker:
 
     def build_engine(self, in_chans=None):
         ecfg = EngineConfig.from_cfg(self.params.cfg, max_batch=1,
-                                     precision=getattr(self.params, 'precision', 'bf16'),
+                                     precision=getattr(self.params, 'precision', 'fp32'),
                                      use_graphs=getattr(self.params, 'use_graphs', True),
                                      debug_outputs=bool(getattr(self.params, 'debug_outputs', False)))
         ecfg.template_factor = self.params.template_factor

@@ -36,7 +36,7 @@ class EngineConfig:
     max_batch: int = 1
     use_graphs: bool = True
     debug_outputs: bool = False
-    precision: str = "bf16"           # "bf16" | "fp32" (fp32-faithful split-bf16 products)
+    precision: str = "fp32"           # "fp32": parity mode, f16x3 split products (common.h); "bf16": plain bf16
 
     @classmethod
     def from_cfg(cls, cfg, **kw):

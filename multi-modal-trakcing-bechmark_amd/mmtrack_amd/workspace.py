@@ -170,7 +170,7 @@ def run_batched_dataset(seqs, yaml_name, batch, modality, out_root, dataset_name
     params = importlib.import_module(f'lib.test.parameter.{script_name}').parameters(yaml_name)
     for k, v in (params_overrides or {}).items():
         setattr(params, k, v)
-    ecfg = EngineConfig.from_cfg(params.cfg, max_batch=batch, precision=getattr(params, 'precision', 'bf16'))
+    ecfg = EngineConfig.from_cfg(params.cfg, max_batch=batch, precision=getattr(params, 'precision', 'fp32'))
     eng = Engine(ecfg, load_net(params), device=current_device())
     save_folder = join(out_root, f'{modality.upper()}_workspace', 'results', dataset_name, yaml_name)
     os.makedirs(save_folder, exist_ok=True)
@@ -205,7 +205,8 @@ def main(modality='rgbt', argv=None):
     ap.add_argument('--synthetic', default=0, type=int, help='use N seeded synthetic sequences')
     ap.add_argument('--frames', default=100, type=int, help='frames per synthetic sequence')
     ap.add_argument('--synthetic_weights', action='store_true', help='seeded weights instead of models/ViPT_<yaml>.pth')
-    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--precision', default='fp32', choices=['bf16', 'fp32'],
+                    help='fp32: parity mode (f16x3 products, the reference CE decisions and argmax); bf16: faster, not parity')
     ap.add_argument('--out_root', default='.', type=str)
     args = ap.parse_args(argv)
     import torch

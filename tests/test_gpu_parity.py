@@ -7,11 +7,13 @@ template crop 128 = output size, search crop 256 = output size; the resize at sc
 the input bit for bit, see test_oracle_golden.py).  Tolerances (bf16 GEMM operands, fp32
 accumulation, fp32 residual / LayerNorm / softmax / CE scores):
 
+parity mode (precision "fp32", f16x3 products -- the default):
+* CE kept sets identical to the reference's (its recorded boundary margins are >= 2.5e-4 relative; the
+  engine's CE scores agree to < 1e-4 relative);
 * argmax of the Hann-windowed score map: exact;
-* score / size / offset maps: |d| <= 2e-2;
-* CE kept sets: Jaccard reported, >= 0.9 asserted (the reference's own CE margins are as small
-  as 2e-3 relative, below bf16 resolution -- SURVEY.md §7.3 #1);
-* predicted box: IoU >= 0.99 against the reference.
+* score / size maps |d| <= 1e-3, offset maps <= 3e-3;
+* predicted boxes: IoU >= 0.999 against the reference (tracker sequences and random pairs).
+The bf16 mode is checked only with teacher-forced CE (its arithmetic error, not parity).
 """
 import os
 
@@ -123,35 +125,64 @@ def test_network_matches_reference_golden(engines, name):
             np.testing.assert_allclose(feat[::8], g[f"feat_rows_{j}"], atol=5e-3)
 
 
-@pytest.mark.parametrize("name", ["deep_rgbt", "ostrack384"])
-def test_network_bf16_statistics(engines, name):
-    """bf16 mode vs the fp32 oracle over 12 random crop pairs (statistical: CE flips are expected when
-    the reference's own CE margin is below bf16 resolution)."""
+@pytest.mark.parametrize("name,n", [("deep_rgbt", 24), ("deep_rgbd", 12), ("shaw_rgbt", 12), ("ostrack384", 12)])
+def test_parity_random_pairs(engines, name, n):
+    """The default (parity) mode against the fp32 CPU oracle on random crop pairs beyond the goldens, at the
+    north star's thresholds: CE kept sets identical, windowed argmax identical, box IoU >= 0.999.  A CE
+    flip is excused only where the reference's own boundary margin is below 4x the measured CE-score error
+    of that pair (fp32 noise of both sides); none of these pairs comes near that."""
     cfg = _cfg(name)
-    eng = engines(name, "bf16")
+    eng = engines(name, "fp32")
     sd = synth.make_state_dict(0, **SHAPES[name])
     ocfg = ov.NetCfg(kind=SHAPES[name]["kind"], prompt_type=SHAPES[name].get("prompt_type", "vipt_deep"),
                      search_size=cfg.search_size, template_size=cfg.template_size)
-    agree, ious = 0, []
-    n = int(os.environ.get("MMT_STAT_N", "32"))   # 12 samples measured too noisy for the thresholds
+    Lx = ocfg.lens_x
     for j in range(n):
-        zp = synth.make_patch(500 + j, cfg.template_size, cfg.in_chans)
-        xp = synth.make_patch(600 + j, cfg.search_size, cfg.in_chans)
+        zp = synth.make_patch(900 + j, cfg.template_size, cfg.in_chans)
+        xp = synth.make_patch(1900 + j, cfg.search_size, cfg.in_chans)
         f0, f1, box = identity_frames(zp, xp, cfg.search_factor)
         eng.initialize(0, f0, box)
         eng.track(0, f1)
-        res = eng.debug("result")
-        out = ov.forward(sd, ocrop.preprocess(zp), ocrop.preprocess(xp), ocfg, ov.ce_template_mask(ocfg))
-        resp = (ov.hann2d(ocfg.feat_sz) * out["score_map"]).flatten()
-        ref_idx = int(torch.argmax(resp))
-        agree += int(res[5]) == ref_idx
-        pb = ov.cal_bbox(resp.view(1, 1, ocfg.feat_sz, ocfg.feat_sz), out["size_map"], out["offset_map"],
-                         ocfg.feat_sz)[0].numpy()
-        to_xywh = lambda b: [b[0] - b[2] / 2, b[1] - b[3] / 2, b[2], b[3]]
-        ious.append(iou(to_xywh(res[:4]), to_xywh(pb)))
-    print(f"{name} bf16: argmax agreement {agree}/{n}, box IoU median {np.median(ious):.4f} min {min(ious):.4f}")
-    assert agree >= n * 0.5
-    assert np.median(ious) >= 0.9
+        res, removed, keys = eng.debug("result"), eng.debug("removed"), eng.debug("ce_keys")
+        tr = {}
+        out = ov.forward(sd, ocrop.preprocess(zp), ocrop.preprocess(xp), ocfg, ov.ce_template_mask(ocfg), trace=tr)
+        kerr = max(float(np.max(np.abs(keys[st][k > 0] - k[k > 0]) / k[k > 0])) for st, k in
+                   enumerate(t.numpy() for t in tr["ce_keys"]))
+        if min(tr["ce_margin"]) > 4 * kerr:
+            ref_rm = torch.cat(out["removed_indexes_s"], dim=1)[0].numpy()
+            np.testing.assert_array_equal(np.sort(removed[:len(ref_rm)]), np.sort(ref_rm))
+            resp = (ov.hann2d(ocfg.feat_sz) * out["score_map"]).flatten()
+            assert int(res[5]) == int(torch.argmax(resp)), (name, j)
+            pb = ov.cal_bbox(resp.view(1, 1, ocfg.feat_sz, ocfg.feat_sz), out["size_map"], out["offset_map"],
+                             ocfg.feat_sz)[0].numpy()
+            to_xywh = lambda b: [b[0] - b[2] / 2, b[1] - b[3] / 2, b[2], b[3]]
+            assert iou(to_xywh(res[:4]), to_xywh(pb)) >= 0.999
+        else:
+            print(f"{name}[{j}]: reference CE margin {min(tr['ce_margin']):.2e} within 4x the score error {kerr:.2e}")
+        assert kerr < 2e-4, kerr
+        assert Lx == keys.shape[1]
+
+
+def test_bf16_mode_teacher_forced(engines):
+    """The opt-in bf16 mode is not a parity mode (its CE decisions flip against the
+    reference).  With the reference's CE decisions injected (mmt_debug_force_ce) what remains is the bf16
+    arithmetic itself: score maps within 3e-2 of the golden, the kept sets the forced ones."""
+    eng = engines("deep_rgbt", "bf16")
+    cfg = _cfg("deep_rgbt")
+    g = np.load(os.path.join(GOLDEN, "net_deep_rgbt.npz"))
+    for j, (sz, ss) in enumerate(g["seeds"]):
+        zp = synth.make_patch(int(sz), cfg.template_size, cfg.in_chans)
+        xp = synth.make_patch(int(ss), cfg.search_size, cfg.in_chans)
+        f0, f1, box = identity_frames(zp, xp, cfg.search_factor)
+        eng.force_ce(0, g[f"ce_keys_{j}"])
+        eng.initialize(0, f0, box)
+        eng.track(0, f1)
+        eng.force_ce(0, None)
+        ref_removed = g[f"removed_{j}"][0]
+        np.testing.assert_array_equal(np.sort(eng.debug("removed")[:len(ref_removed)]), np.sort(ref_removed))
+        d = np.abs(eng.debug("maps")[0] - g[f"score_map_{j}"][0, 0]).max()
+        print(f"bf16 teacher-forced [{j}] score max|d| {d:.3e}")
+        assert d < 3e-2
 
 
 @pytest.mark.parametrize("seq", ["deep_rgbt", "deep_rgbd"])
@@ -188,7 +219,8 @@ def test_crop_kernel_bit_exact_vs_oracle(engines):
 
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_batch_equals_single(engines, precision):
-    """track_batch over N sequences (graph-captured) == N independent single-sequence tracks."""
+    """track_batch over N sequences (graph-captured) == N independent single-sequence tracks (parity mode: to
+    fp32 rounding, one sequence alone runs its few-tile GEMMs split-K, which changes the summation order)."""
     cfg = EngineConfig(max_batch=3, debug_outputs=True, use_graphs=True, precision=precision)
     eng = Engine(cfg, synth.make_state_dict(0, **SHAPES["deep_rgbt"]))
     single = engines("deep_rgbt", precision)
@@ -204,7 +236,10 @@ def test_batch_equals_single(engines, precision):
         single.initialize(0, fr[0], list(gt[0]))
         for t in range(1, 4):
             box, _ = single.track(0, fr[t])
-            np.testing.assert_allclose(outs_b[t - 1][i], box, rtol=1e-6, atol=1e-4)
+            if precision == "bf16":   # no split-K in bf16 mode: batch-size independent bit for bit
+                np.testing.assert_allclose(outs_b[t - 1][i], box, rtol=1e-6, atol=1e-4)
+            else:
+                np.testing.assert_allclose(outs_b[t - 1][i], box, rtol=1e-5, atol=1e-3)
     eng.close()
 
 
