@@ -7,8 +7,8 @@ CENTER head, windowed argmax decode, box back-mapping.  Frames are synthetic 640
 (RGB + thermal-like aux) already resident in HBM; weights are the seeded synthetic law of
 mmtrack_amd.synth (no checkpoint ships with the reference).
 
-Precision (--precision): "fp32" (default) is the parity mode -- every MFMA product split into bf16
-hi/lo halves (hi*hi + lo*hi + hi*lo, "bf16x3"), which reproduces the fp32 reference's candidate-
+Precision (--precision): "fp32" (default) is the parity mode -- every MFMA operand split into fp16
+hi/lo halves of range-scaled values (Wh*Ah + Wl*Ah + Wh*Al, "f16x3"), which reproduces the fp32 reference's candidate-
 elimination decisions and windowed argmax (tests/test_gpu_parity.py); "bf16" is plain bf16 operands,
 faster, but its CE decisions flip against the reference.
 
@@ -190,7 +190,7 @@ def roofline_from(classes, precision, workload, batch):
     dom = max(classes, key=lambda c: classes[c]["ms_per_step"])
     c = classes[dom]
     split = precision == "fp32"
-    # bf16x3: three bf16 MFMAs per product, so the arithmetic's dense peak is the bf16 peak / 3
+    # f16x3: three fp16 MFMAs (bf16 rate) per product, so the arithmetic's dense peak is the bf16 peak / 3
     peak = PEAK_BF16_TFLOPS / 3 if split else PEAK_BF16_TFLOPS
     traffic, src = pmc_traffic(dom, precision) if (batch == 32 and workload == "vipt_deep_rgbt") else (None, None)
     for k, v in classes.items():
@@ -201,7 +201,7 @@ def roofline_from(classes, precision, workload, batch):
             "traffic_source": src, "algorithmic_bytes_per_launch": c["algorithmic_bytes_per_launch"],
             "avg_launch_us": c["avg_launch_us"], "flop_per_launch": c["flop_per_launch"],
             "launches": c["launches"],
-            "peak_note": ("bf16x3 split products (hi*hi + lo*hi + hi*lo): dense bf16 2500 TF/s / 3; achieved counts "
+            "peak_note": ("f16x3 split products (Wh*Ah + Wl*Ah + Wh*Al, fp16 MFMA at the bf16 rate): dense 2500 TF/s / 3; achieved counts "
                           "algorithmic 2MNK flops, the MFMA pipe issues 3x that") if split else "dense bf16",
             "mfma_pipe_frac": round(c["achieved_tflops"] * (3 if split else 1) / PEAK_BF16_TFLOPS, 4),
             "classes": classes}
@@ -215,7 +215,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="sequences tracked per GPU per step")
     ap.add_argument("--workload", default="vipt_deep_rgbt", choices=list(WORKLOADS))
     ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16"),
-                    help="fp32: parity mode (bf16x3 split products); bf16: plain bf16 operands")
+                    help="fp32: parity mode (f16x3 split products); bf16: plain bf16 operands")
     ap.add_argument("--frames", type=int, default=8, help="distinct synthetic frames per sequence (cycled)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--sync", action="store_true", help="blocking per-frame calls (no frame pipelining)")
@@ -319,7 +319,7 @@ def main():
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16x3" if args.precision == "fp32" else "bf16", "data": "synthetic",
+            "dtype": "f16x3" if args.precision == "fp32" else "bf16", "data": "synthetic",
             "config": {"workload": args.workload, "description": desc, "sequences_per_gpu": B,
                        "global_batch": B * world, "frame": f"{W}x{H}x{C} uint8 (HBM-resident)",
                        "template": cfg.template_size, "search": cfg.search_size, "parallelism": f"seq-shard x{world}",
