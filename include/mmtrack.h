@@ -97,6 +97,11 @@ int mmt_track_batch(mmt_engine* e, int first_slot, int n, const uint8_t* const* 
                     const int* W, int C, const int64_t* row_stride, int is_device, double* out_xywh,
                     float* out_score);
 int mmt_get_state(const mmt_engine* e, int slot, double out_xywh[4]);
+/* device frames (is_device = 1) are read in place on the engine's own stream: after this call every
+ * initialize / track / submit with device frames first waits for the work queued so far on hip_stream
+ * (the caller's producer stream, e.g. the one mmt_rgbd_assemble / mmt_rgbx_merge ran on; NULL is the
+ * legacy default stream).  Without this call device frames must be complete when they are passed. */
+int mmt_set_frame_stream(mmt_engine* e, void* hip_stream);
 int mmt_set_state(mmt_engine* e, int slot, const double xywh[4]);
 
 /* pipelined tracking.  The tracker state machine of ViPTTrack.track (crop geometry from the last box,
@@ -157,6 +162,13 @@ size_t mmt_rgbd_workspace_bytes(void);
 int mmt_rgbd_assemble(const uint8_t* rgb, int64_t rgb_stride, const uint16_t* depth, int64_t depth_stride, int H,
                       int W, int depth_clip, const uint8_t* lut_bgr, uint8_t* out, int64_t out_stride,
                       void* workspace, size_t ws_bytes, void* hip_stream);
+
+/* RGB-T / RGB-E frame assembly (get_x_frame(color, aux, dtype='rgbrgb'), depth_utils.py:71-132, as the
+ * RGB-T / RGB-E workspaces call it, test_rgbt_mgpus.py:106, test_rgbe_mgpus.py:74): device RGB
+ * (H x W x 3 uint8) + device aux (H x W x aux_channels uint8, 1 or 3; 1 is replicated) -> device
+ * H x W x 6 uint8 frame (R G B | aux).  Asynchronous on hip_stream.                               */
+int mmt_rgbx_merge(const uint8_t* rgb, int64_t rgb_stride, const uint8_t* aux, int64_t aux_stride, int aux_channels,
+                   int H, int W, uint8_t* out, int64_t out_stride, void* hip_stream);
 
 /* ---- DiMP / mfDiMP target classifier (device pointers, fp32) ------------------------------------
  *  feat [I][S][C][H][W] (I training images x S sequences), filter [S][C][fh][fw] (fh*fw <= 25).

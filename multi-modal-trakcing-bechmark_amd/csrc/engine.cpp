@@ -155,6 +155,9 @@ struct mmt_engine {
   std::vector<size_t> frame_cap;
   hipStream_t cstream = nullptr;
   hipEvent_t copy_ev[kRing] = {};
+  hipStream_t frame_stream = nullptr;  // caller's stream that produces device frames (mmt_set_frame_stream;
+  bool frame_wait = false;             // null = the legacy default stream)
+  hipEvent_t frame_ev = nullptr;
 
   // tracker state (vipt.py:57, 88) in doubles
   std::vector<std::array<double, 4>> state;
@@ -1151,6 +1154,7 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   if (hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
   for (auto& ev : e->copy_ev)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
+  if (hipEventCreateWithFlags(&e->frame_ev, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
   if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess)
     return MMT_E_HIP;
@@ -1200,6 +1204,7 @@ void mmt_destroy(mmt_engine* e) {
   }
   for (auto& ev : e->copy_ev)
     if (ev) hipEventDestroy(ev);
+  if (e->frame_ev) hipEventDestroy(e->frame_ev);
   if (e->fork_ev) hipEventDestroy(e->fork_ev);
   if (e->join_ev) hipEventDestroy(e->join_ev);
   delete e;
@@ -1255,6 +1260,23 @@ int mmt_finalize(mmt_engine* e) {
   return MMT_OK;
 }
 
+// device frames are read in place: order the engine stream after the work queued so far on the
+// caller's producer stream (e.g. the GPU frame assembly of mmt_rgbd_assemble / mmt_rgbx_merge)
+static int wait_frame_stream(mmt_engine* e) {
+  if (!e->frame_wait) return MMT_OK;
+  HIPCHECK(e, hipEventRecord(e->frame_ev, e->frame_stream));
+  HIPCHECK(e, hipStreamWaitEvent(e->stream, e->frame_ev, 0));
+  return MMT_OK;
+}
+
+int mmt_set_frame_stream(mmt_engine* e, void* hip_stream) {
+  int r = check_engine(e);
+  if (r) return r;
+  e->frame_stream = (hipStream_t)hip_stream;
+  e->frame_wait = true;
+  return MMT_OK;
+}
+
 int mmt_initialize(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride,
                    int is_device, const double init_xywh[4]) {
   int r = check_engine(e);
@@ -1265,6 +1287,7 @@ int mmt_initialize(mmt_engine* e, int slot, const uint8_t* frame, int Hh, int Ww
   double rf;
   TRY(geometry(e, init_xywh, e->cfg.template_factor, e->cfg.template_size, &x1, &y1, &cs, &rf));
   const uint8_t* dev;
+  if (is_device) TRY(wait_frame_stream(e));
   TRY(stage_frame(e, slot, 0, frame, Hh, Ww, Cc, row_stride, is_device, &dev, e->stream));
   CropParam p{dev, row_stride, Hh, Ww, Cc, x1, y1, cs, 0};
   e->params_host[0] = p;
@@ -1316,6 +1339,7 @@ int mmt_track_batch_submit(mmt_engine* e, int first_slot, int n, const uint8_t* 
                     &dev, e->cstream));
     ph[i] = CropParam{dev, row_stride[i], Hs[i], Ws[i], Cc, 0, 0, 0, 0};   // geometry: crop_geometry()
   }
+  if (is_device) TRY(wait_frame_stream(e));
   if (!is_device) {   // the launch waits for this frame's copies only (copy stream, overlapping compute)
     hipEvent_t ce = e->copy_ev[e->next_ticket % kRing];
     HIPCHECK(e, hipEventRecord(ce, e->cstream));

@@ -140,6 +140,29 @@ __global__ __launch_bounds__(256) void rgbd_map_kernel(const uint8_t* rgb, int64
   }
 }
 
+// RGB-T / RGB-E frame assembly: get_x_frame(color, aux, dtype='rgbrgb') (depth_utils.py:71-132 as the
+// RGB-T / RGB-E workspaces call it, test_rgbt_mgpus.py:98): both images are read as colour and converted
+// BGR -> RGB by the reference (cv2.imread + cvtColor); the host decoders here hand over RGB already, so
+// the device step is the channel merge into the HBM frame the tracker reads (a 1-channel aux is
+// replicated, as IMREAD_COLOR expands a grayscale file).  One thread per pixel, 6 bytes out.
+__global__ __launch_bounds__(256) void rgbx_merge_kernel(const uint8_t* __restrict__ rgb, int64_t rgb_stride,
+                                                         const uint8_t* __restrict__ aux, int64_t aux_stride,
+                                                         int aux_ch, int H, int W, uint8_t* __restrict__ out,
+                                                         int64_t out_stride) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)H * W) return;
+  const int y = (int)(i / W), x = (int)(i - (int64_t)y * W);
+  const uint8_t* c = rgb + (int64_t)y * rgb_stride + (int64_t)x * 3;
+  const uint8_t* a = aux + (int64_t)y * aux_stride + (int64_t)x * aux_ch;
+  uint8_t* o = out + (int64_t)y * out_stride + (int64_t)x * 6;
+  o[0] = c[0]; o[1] = c[1]; o[2] = c[2];
+  if (aux_ch == 3) {
+    o[3] = a[0]; o[4] = a[1]; o[5] = a[2];
+  } else {
+    o[3] = a[0]; o[4] = a[0]; o[5] = a[0];
+  }
+}
+
 }  // namespace mmt
 
 using namespace mmt;
@@ -164,6 +187,17 @@ int mmt_rgbd_assemble(const uint8_t* rgb, int64_t rgb_stride, const uint16_t* de
   hipLaunchKernelGGL(depth_stats_kernel, dim3(1), dim3(256), 0, s, st, n, depth_clip);
   hipLaunchKernelGGL(rgbd_map_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rgb, rgb_stride, depth,
                      depth_stride, H, W, st, lut_bgr, out, out_stride);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_rgbx_merge(const uint8_t* rgb, int64_t rgb_stride, const uint8_t* aux, int64_t aux_stride, int aux_channels,
+                   int H, int W, uint8_t* out, int64_t out_stride, void* stream_) {
+  if (!rgb || !aux || !out || H <= 0 || W <= 0 || (aux_channels != 1 && aux_channels != 3) ||
+      rgb_stride < (int64_t)W * 3 || aux_stride < (int64_t)W * aux_channels || out_stride < (int64_t)W * 6)
+    return MMT_E_ARG;
+  const int64_t n = (int64_t)H * W;
+  hipLaunchKernelGGL(rgbx_merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream_, rgb,
+                     rgb_stride, aux, aux_stride, aux_channels, H, W, out, out_stride);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 

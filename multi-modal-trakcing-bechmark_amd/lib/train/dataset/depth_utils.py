@@ -96,3 +96,13 @@ def get_rgbd_frame_device(color_path, depth_path, depth_clip=True, device=None):
         dp = dp[..., 0]
     return assemble_rgbd(rgb, dp.astype(np.uint16, copy=False), depth_clip=depth_clip, device=device)
 
+
+
+def get_x_frame_device(color_path, aux_path, dtype='rgbrgb', device=None):
+    """get_x_frame(color, aux, dtype='rgbrgb') with the merge done on the GPU (mmtrack_amd.frames.merge_rgbx):
+    returns the H x W x 6 frame as a CUDA tensor the tracker reads in place (the RGB-T / RGB-E workspace
+    path, test_rgbt_mgpus.py:106).  Other dtypes are host-assembled (get_x_frame)."""
+    if dtype != 'rgbrgb':
+        return get_x_frame(color_path, aux_path, dtype=dtype)
+    from mmtrack_amd.frames import merge_rgbx
+    return merge_rgbx(_imread(color_path), _imread(aux_path, unchanged=True), device=device)

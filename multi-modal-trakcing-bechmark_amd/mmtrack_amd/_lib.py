@@ -86,6 +86,8 @@ SIGNATURES = {
     "mmt_rgbd_workspace_bytes": (ctypes.c_size_t, []),
     "mmt_rgbd_assemble": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _I, _I, _I, _P, _P, ctypes.c_int64, _P,
                                ctypes.c_size_t, _P]),
+    "mmt_set_frame_stream": (_I, [_P, _P]),
+    "mmt_rgbx_merge": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _I, _I, _I, _P, ctypes.c_int64, _P]),
     "mmt_dimp_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I]),
     "mmt_dimp_apply_filter": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_dimp_feat_transpose": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -153,13 +153,25 @@ class Engine:
         self._check(self.lib.mmt_finalize(self.h))
 
     # -- tracking
+    def _order_device_frames(self, dev):
+        """Device frames are read in place on the engine stream: order it after torch's current stream
+        (where the caller produced the frame, e.g. frames.assemble_rgbd / merge_rgbx)."""
+        if dev:
+            import torch
+            s = torch.cuda.current_stream(self.device).cuda_stream
+            if s != getattr(self, "_frame_stream", None):
+                self._check(self.lib.mmt_set_frame_stream(self.h, ctypes.c_void_p(s)))
+                self._frame_stream = s
+
     def initialize(self, slot: int, image, box: Sequence[float]):
         keep, ptr, H, W, C, stride, dev = _frame_arg(image)
+        self._order_device_frames(dev)
         b = (ctypes.c_double * 4)(*[float(v) for v in box])
         self._check(self.lib.mmt_initialize(self.h, slot, ptr, H, W, C, stride, dev, b))
 
     def track(self, slot: int, image):
         keep, ptr, H, W, C, stride, dev = _frame_arg(image)
+        self._order_device_frames(dev)
         out = (ctypes.c_double * 4)()
         sc = ctypes.c_float()
         self._check(self.lib.mmt_track(self.h, slot, ptr, H, W, C, stride, dev, out, ctypes.byref(sc)))
@@ -174,6 +186,7 @@ class Engine:
         strides = (ctypes.c_int64 * n)(*[a[5] for a in args])
         C = args[0][4]
         dev = args[0][6]
+        self._order_device_frames(dev)
         out = (ctypes.c_double * (4 * n))()
         sc = (ctypes.c_float * n)()
         self._check(self.lib.mmt_track_batch(self.h, first_slot, n, ptrs, Hs, Ws, C, strides, dev, out, sc))
@@ -189,6 +202,7 @@ class Engine:
         Ws = (ctypes.c_int * n)(*[a[3] for a in args])
         strides = (ctypes.c_int64 * n)(*[a[5] for a in args])
         ticket = ctypes.c_int64()
+        self._order_device_frames(args[0][6])
         self._check(self.lib.mmt_track_batch_submit(self.h, first_slot, n, ptrs, Hs, Ws, args[0][4], strides,
                                                     args[0][6], ctypes.byref(ticket)))
         self._pending[ticket.value] = (n, args)   # keep host frames alive until their copy has run

@@ -1,8 +1,10 @@
-"""Multi-modal frame assembly on the GPU (mmt_rgbd_assemble).
+"""Multi-modal frame assembly on the GPU (mmt_rgbd_assemble, mmt_rgbx_merge).
 
 ``assemble_rgbd`` is get_rgbd_frame(color, depth, dtype='rgbcolormap', depth_clip=...) of
 ViPT/lib/train/dataset/depth_utils.py:7-58 (median-based depth clip, cv2 NORM_MINMAX, JET colormap,
 merge) producing the H x W x 6 uint8 frame directly in HBM, where the tracker reads it.
+``merge_rgbx`` is get_x_frame(color, aux, dtype='rgbrgb') (depth_utils.py:71-132, the RGB-T / RGB-E
+workspaces' call, test_rgbt_mgpus.py:106): the two decoded RGB images merged into the HBM frame.
 """
 from __future__ import annotations
 
@@ -57,4 +59,28 @@ def assemble_rgbd(rgb, depth, depth_clip: bool = True, lut_bgr=None, out=None, d
         raise ValueError("mmt_rgbd_assemble: invalid argument")
     if rc != 0:
         raise RuntimeError(f"mmt_rgbd_assemble failed ({rc})")
+    return out
+
+
+def merge_rgbx(rgb, aux, out=None, device=None):
+    """rgb: H x W x 3 uint8, aux: H x W x 3 (or H x W, replicated) uint8 -> CUDA H x W x 6 uint8 frame."""
+    lib = _lib.load()
+    if not torch.cuda.is_available():
+        raise RuntimeError("merge_rgbx needs an MI355X (HIP device); there is no CPU path")
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    r, a = _dev(rgb, torch.uint8, dev), _dev(aux, torch.uint8, dev)
+    if r.dim() != 3 or r.shape[2] != 3:
+        raise ValueError("rgb must be H x W x 3")
+    ach = 1 if a.dim() == 2 else a.shape[2]
+    if a.dim() not in (2, 3) or ach not in (1, 3) or tuple(a.shape[:2]) != tuple(r.shape[:2]):
+        raise ValueError("aux must be H x W x 3 or H x W with rgb's H x W")
+    H, W = r.shape[:2]
+    if out is None:
+        out = torch.empty(H, W, 6, dtype=torch.uint8, device=dev)
+    rc = lib.mmt_rgbx_merge(r.data_ptr(), r.stride(0), a.data_ptr(), a.stride(0), ach, H, W, out.data_ptr(),
+                            out.stride(0), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    if rc == -1:
+        raise ValueError("mmt_rgbx_merge: invalid argument")
+    if rc != 0:
+        raise RuntimeError(f"mmt_rgbx_merge failed ({rc})")
     return out

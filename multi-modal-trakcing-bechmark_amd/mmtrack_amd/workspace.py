@@ -94,6 +94,21 @@ def default_xtype(dataset_name, script_name='vipt'):
     return 'rgbcolormap' if dataset_name in ('DepthTrack', 'depthtrack', 'CDTB', 'cdtb') else 'rgbrgb'
 
 
+def frame_getter(rgb, aux, xtype):
+    """Frame i of a dataset sequence as the tracker's input: RGB-D ('rgbcolormap') clip / normalise /
+    colormap / merge on the GPU (vipt_class.py:79 flags), RGB-T / RGB-E ('rgbrgb') merged on the GPU
+    (test_rgbt_mgpus.py:106), other layouts host-assembled (depth_utils.get_x_frame)."""
+    import torch
+    from lib.train.dataset.depth_utils import get_rgbd_frame_device, get_x_frame, get_x_frame_device
+    if xtype == 'rgbcolormap':
+        return lambda i: get_rgbd_frame_device(rgb[i], aux[i], depth_clip=True)
+    if xtype == 'rgbrgb' and torch.cuda.is_available():
+        return lambda i: get_x_frame_device(rgb[i], aux[i], dtype='rgbrgb')
+    if xtype == 'color':
+        return lambda i: get_x_frame(rgb[i], None, dtype='color')
+    return lambda i: get_x_frame(rgb[i], aux[i], dtype=xtype)
+
+
 def synthetic_state_dict(script_name, yaml_name):
     from mmtrack_amd import synth
     if script_name == 'ostrack':
@@ -134,13 +149,8 @@ def run_sequence(seq_name, seq_home, dataset_name, yaml_name, num_gpu=1, epoch=6
         get = lambda i: frames[i]
         n = len(frames)
     else:
-        from lib.train.dataset.depth_utils import get_rgbd_frame_device, get_x_frame
         rgb, aux, gt = gen_config(join(seq_home, seq_name), dataset_name)
-        xtype = default_xtype(dataset_name, script_name)
-        if xtype == 'rgbcolormap':   # RGB-D: clip / normalise / colormap on the GPU (vipt_class.py:79 flags)
-            get = lambda i: get_rgbd_frame_device(rgb[i], aux[i], depth_clip=True)
-        else:
-            get = lambda i: get_x_frame(rgb[i], aux[i], dtype=xtype)
+        get = frame_getter(rgb, aux, default_xtype(dataset_name, script_name))
         n = len(rgb)
     result = np.zeros((n, 4), dtype=np.float64)
     result[0] = np.copy(gt[0])
@@ -235,14 +245,9 @@ def main(modality='rgbt', argv=None):
                 name, fr, gt = syn[i]
                 seqs.append((name, len(fr), (lambda f: (lambda k: f[k]))(fr), gt))
             else:
-                from lib.train.dataset.depth_utils import get_rgbd_frame_device, get_x_frame
                 rgb, aux, gt = gen_config(join(args.seq_home, names[i]), args.dataset_name)
-                xt = default_xtype(args.dataset_name, args.script_name)
-                if xt == 'rgbcolormap':
-                    getf = (lambda r, a: (lambda k: get_rgbd_frame_device(r[k], a[k], depth_clip=True)))(rgb, aux)
-                else:
-                    getf = (lambda r, a: (lambda k: get_x_frame(r[k], a[k], dtype=xt)))(rgb, aux)
-                seqs.append((names[i], len(rgb), getf, gt))
+                seqs.append((names[i], len(rgb), frame_getter(rgb, aux, default_xtype(args.dataset_name,
+                                                                                      args.script_name)), gt))
         run_batched_dataset(seqs, args.yaml_name, args.batch, modality, args.out_root, args.dataset_name, overrides,
                             script_name=args.script_name)
     else:

@@ -225,3 +225,35 @@ def test_imread_modes(tmp_path):
     assert d.ndim == 2 and int(d.max()) == 47000
     f = get_x_frame(str(tmp_path / "g.png"), str(tmp_path / "g.png"), dtype="rgbrgb")
     assert f.shape == (6, 8, 6) and f.dtype == np.uint8
+
+
+def test_vot_handle_offline_source():
+    """lib/test/vot/vot.py handle semantics (vot.py:22-111) over the offline SequenceSource: the first
+    frame() returns the initialisation image, reports keep the confidence property, None ends."""
+    import builtins
+
+    from lib.test.vot import vot
+    src = vot.SequenceSource([10, 20, 30, 40], ["a.png", ["b.png", "b_d.png"]])
+    h = vot.VOT("rectangle", channels="rgbd", source=src)
+    assert h.region() == vot.Rectangle(10.0, 20.0, 30.0, 40.0)
+    assert h.channels == ["color", "depth"]
+    assert h.frame() == "a.png"
+    assert h.frame() == ["b.png", "b_d.png"]
+    h.report(vot.Rectangle(1, 2, 3, 4), 0.5)
+    h.report(vot.Rectangle(1, 2, 3, 4))
+    assert h.frame() is None
+    assert src.reports == [(vot.Rectangle(1, 2, 3, 4), {"confidence": 0.5}), (vot.Rectangle(1, 2, 3, 4), {})]
+    with pytest.raises(Exception, match="Illegal configuration"):
+        vot.VOT("rectangle", channels="rgbx", source=src)
+    real_import = builtins.__import__
+
+    def no_trax(name, *a, **k):
+        if name == "trax":
+            raise ImportError(name)
+        return real_import(name, *a, **k)
+    builtins.__import__ = no_trax
+    try:
+        with pytest.raises(Exception, match="TraX support not found"):
+            vot.VOT("rectangle", channels="rgbd")
+    finally:
+        builtins.__import__ = real_import
