@@ -170,6 +170,49 @@ int mmt_rgbd_assemble(const uint8_t* rgb, int64_t rgb_stride, const uint16_t* de
 int mmt_rgbx_merge(const uint8_t* rgb, int64_t rgb_stride, const uint8_t* aux, int64_t aux_stride, int aux_channels,
                    int H, int W, uint8_t* out, int64_t out_stride, void* hip_stream);
 
+/* ---- mfDiMP / DeT-DiMP feature path (fp32, device pointers; asynchronous on hip_stream) -----------
+ * The image -> classification-feature chain of DiMPnet_DeT (RGBD/models/DeT/ltr/models/tracking/
+ * dimpnet.py:15-156, merge 'max') and pytracking's patch sampling; host orchestration in
+ * mmtrack_amd/dimpnet.py.  Activations NHWC, conv weights [Cout][kh][kw][Cin] (BN folded).        */
+#define MMT_CONV_RELU 1   /* y = max(y, 0) after bias / residual                                    */
+#define MMT_CONV_MAX 2    /* y = max(y_old, y): the 'max' merge of the two backbones (dimpnet.py:103) */
+/* nn.Conv2d (+ folded BN, + residual, ReLU): y [N*Ho*Wo][Cout] = conv(x [N][H][W][Cin]); Cout % 64 == 0 */
+int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w, const float* bias, int Cout, int kh,
+                   int kw, int stride, int pad, const float* resid, float* y, int flags, void* hip_stream);
+/* nn.MaxPool2d(k, stride, pad) over NHWC                                                           */
+int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y,
+                      void* hip_stream);
+/* NetWithBackbone.preprocess_image (net_wrappers.py:55-79): NCHW pixel values [N][C][H][W] (C = 3 or 6)
+ * -> ((v / 255) - mean) / std as NHWC [N][H][W][3] per 3-channel half (out_b: the aux half)       */
+int mmt_image_normalize(const float* im, int N, int C, int H, int W, const float mean[3], const float std_[3],
+                        float* out_a, float* out_b, void* hip_stream);
+/* InstanceL2Norm(size_average, eps, scale) (normalization.py:6-21) of NHWC x; y_nhwc / y_nchw may be NULL */
+int mmt_instance_l2norm(const float* x, int N, int H, int W, int C, float scale, float eps, float* y_nhwc,
+                        float* y_nchw, void* hip_stream);
+/* PrRoIPool2D(PH, PW, spatial_scale) (ltr/external/PreciseRoIPooling), roi n on image n:
+ * feat NHWC, rois device [N][4] = x0, y0, x1, y1 (image coordinates) -> out [N][C][PH][PW]          */
+int mmt_prroi_pool(const float* feat, int N, int H, int W, int C, const float* rois, float spatial_scale, int PH,
+                   int PW, float* out, void* hip_stream);
+/* sample_patch (pytracking/features/preprocessing.py:49-125) from an H x W x C uint8 device frame:
+ * geom = {df, os_y, os_x, tl_y, tl_x, sz_h, sz_w} (pre-downsample factor and offset, crop top-left and
+ * size in the downsampled image, replicate padding) -> bilinear resize -> float NCHW [C][out_h][out_w] */
+int mmt_sample_patch(const uint8_t* frame, int H, int W, int C, int64_t row_stride, const int geom[7], int out_h,
+                     int out_w, float* out, void* hip_stream);
+/* one init-sample augmentation (pytracking/features/augmentation.py) of a float [C][E_h][E_w] patch,
+ * cropped to out_h x out_w by crop_to_output (top / left = pad_top / pad_left, replicate)          */
+#define MMT_TF_IDENTITY 0 /* Identity, Translation                                                   */
+#define MMT_TF_FLIP 1     /* FlipHorizontal                                                          */
+#define MMT_TF_BLUR 2     /* Blur: separable Gaussian taps fy[2 ry + 1] (vertical), fx[2 rx + 1]     */
+#define MMT_TF_ROTATE 3   /* Rotate: cv2.warpAffine INTER_LINEAR / BORDER_REPLICATE, affine = the
+                             inverted (dst -> src) 2 x 3 matrix                                      */
+typedef struct mmt_patch_tf {
+  int kind, top, left, blur_ry, blur_rx;
+  float blur_fy[33], blur_fx[33];
+  double affine[6];
+} mmt_patch_tf;
+int mmt_patch_transform(const float* img, int C, int E_h, int E_w, const mmt_patch_tf* tf, int out_h, int out_w,
+                        float* out, void* hip_stream);
+
 /* ---- DiMP / mfDiMP target classifier (device pointers, fp32) ------------------------------------
  *  feat [I][S][C][H][W] (I training images x S sequences), filter [S][C][fh][fw] (fh*fw <= 25).
  *  mmt_dimp_optimize runs num_iter steepest-descent Gauss-Newton steps in place on `weights`
@@ -183,10 +226,10 @@ typedef struct mmt_dimp_params {
   float min_filter_reg;     /* 1e-3                                          */
   float alpha_eps;          /* 0                                             */
   float bin_displacement;   /* DistanceMap bin displacement                  */
-  int num_dist_bins;        /* <= 32                                         */
-  float label_w[32];        /* label_map_predictor.weight                    */
-  float mask_w[32];         /* target_mask_predictor.0.weight                */
-  float spatial_w[32];      /* spatial_weight_predictor.weight               */
+  int num_dist_bins;        /* <= 128 (DiMP-50: 100)                         */
+  float label_w[128];       /* label_map_predictor.weight                    */
+  float mask_w[128];        /* target_mask_predictor.0.weight                */
+  float spatial_w[128];     /* spatial_weight_predictor.weight               */
 } mmt_dimp_params;
 
 size_t mmt_dimp_workspace_bytes(int I, int S, int C, int H, int W, int fh, int fw, int num_iter);

@@ -39,7 +39,7 @@ WsLayout layout(int I, int S, int C, int H, int W, int fh, int fw, int num_iter)
   L.loss = take(num_iter + 1);
   L.centers = take(IS * 2);
   L.sqrtsw = take(IS);
-  L.params = take(3 * 32);
+  L.params = take(3 * 128);
   L.total = off;
   return L;
 }
@@ -115,7 +115,7 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
                       const float* bb, const float* sample_weight, const mmt_dimp_params* p, int num_iter,
                       void* workspace, size_t ws_bytes, float* losses, void* stream_) {
   if (!feat || !weights || !bb || !p || !workspace || num_iter < 0 || bad_dims(I, S, C, H, W, fh, fw) ||
-      p->num_dist_bins <= 0 || p->num_dist_bins > 32)
+      p->num_dist_bins <= 0 || p->num_dist_bins > 128)
     return MMT_E_ARG;
   const WsLayout L = layout(I, S, C, H, W, fh, fw, num_iter);
   if (ws_bytes < L.total) return MMT_E_ARG;
@@ -125,7 +125,7 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
   const int IS = I * S;
   const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, n = Ho * Wo, nby = (n + 255) / 256;
   // host-side per-sample constants (optimizer.py:108-125, same fp32 arithmetic)
-  std::vector<float> centers(2 * IS), sqrtsw(IS), params(96, 0.f);
+  std::vector<float> centers(2 * IS), sqrtsw(IS), params(3 * 128, 0.f);
   const float off0 = (float)(fh % 2) / 2.0f, off1 = (float)(fw % 2) / 2.0f;
   for (int k = 0; k < IS; ++k) {
     const float* b = bb + 4 * k;
@@ -133,9 +133,9 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
     centers[2 * k + 1] = (b[0] + b[2] / 2) / p->feat_stride - off1;
     sqrtsw[k] = sample_weight ? std::sqrt(sample_weight[k]) : (float)std::sqrt(1.0 / I);
   }
-  std::memcpy(params.data(), p->label_w, 32 * 4);
-  std::memcpy(params.data() + 32, p->mask_w, 32 * 4);
-  std::memcpy(params.data() + 64, p->spatial_w, 32 * 4);
+  std::memcpy(params.data(), p->label_w, 128 * 4);
+  std::memcpy(params.data() + 128, p->mask_w, 128 * 4);
+  std::memcpy(params.data() + 256, p->spatial_w, 128 * 4);
   // the constants travel from a pinned staging buffer (never from these stack vectors: the copies are
   // asynchronous); the buffer is reused only after the previous call's copies have completed
   const size_t nconst = centers.size() + sqrtsw.size() + params.size();
@@ -155,7 +155,7 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
   const float reg = std::fmax(p->filter_reg * p->filter_reg, p->min_filter_reg * p->min_filter_reg);
 
   DimpMaps m{IS, Ho, Wo, p->num_dist_bins, p->bin_displacement, F(L.centers), F(L.sqrtsw), F(L.params),
-             F(L.params) + 32, F(L.params) + 64, F(L.label), F(L.mask), F(L.sw)};
+             F(L.params) + 128, F(L.params) + 256, F(L.label), F(L.mask), F(L.sw)};
   dimp_maps(m, st);
 
   DimpFilter fa{};

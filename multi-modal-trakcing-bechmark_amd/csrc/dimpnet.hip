@@ -1,0 +1,493 @@
+// mfDiMP / DeT-DiMP feature path on gfx950 (fp32): the per-frame image -> classification-feature chain
+// of DiMPnet_DeT (RGBD/models/DeT/ltr/models/tracking/dimpnet.py:15-156, merge_type 'max') and its
+// classifier initialiser, plus pytracking's patch sampling.
+//
+//   sample_patch          pytracking/features/preprocessing.py:49-125 (pre-downsample, replicate pad, bilinear)
+//   patch transforms      pytracking/features/augmentation.py (Identity / Translation / FlipHorizontal / Blur /
+//                         Rotate, each cropped to the output with replicate padding, crop_to_output)
+//   preprocess_image      pytracking/features/net_wrappers.py:55-79 (/255, -mean, /std per 3-channel half)
+//   ResNet-50 conv/BN     ltr/models/backbone/resnet.py (convs as implicit GEMMs, BN folded on the host)
+//   maxpool 3x3 s2 p1     resnet.py (ResNet stem)
+//   InstanceL2Norm        ltr/models/layers/normalization.py:6-21
+//   PrRoIPool2D           ltr/external/PreciseRoIPooling (exact integral of the bilinear surface per bin)
+//
+// Arithmetic: fp32 throughout, the convolutions on v_mfma_f32_16x16x4_f32 (fp32 products, fp32 accumulate --
+// the feature net feeds a Gauss-Newton optimiser and a 19 x 19 argmax, so it runs at the reference's own
+// precision; 157 TF/s dense fp32 matrix peak).  Activations NHWC, weights [Cout][kh][kw][Cin].
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mmtrack.h"
+
+// no FMA contraction: the elementwise float ops restate the reference's separate multiplies and adds
+#pragma clang fp contract(off)
+
+namespace mmt {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+struct ConvArgs {
+  const float* x;       // [N][H][W][Cin]
+  const float* w;       // [Cout][kh][kw][Cin]
+  const float* bias;    // [Cout] or null
+  const float* resid;   // [M][Cout] or null
+  float* y;             // [M][Cout], M = N * Ho * Wo
+  int N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, flags;
+};
+
+// ---------------------------------------------------------------------------------------------------
+// Implicit-GEMM convolution: C[m][n] = sum_k A[m][k] W[n][k], m = output pixel, n = output channel,
+// k = (ky, kx, c).  64 x 64 output tile, 4 waves (2 x 2, each 32 pixels x 32 channels = 2 x 2 MFMA blocks),
+// K-tiles of 16 staged through LDS k-major ([k][64 + 4], conflict-free fragment reads), the next K-tile's
+// global loads held in registers while the current one is multiplied.  The MFMA is issued W x A so a lane
+// ends with 4 consecutive output channels of one pixel: 16-B NHWC stores with bias / residual / ReLU /
+// running-max epilogues.  FAST: Cin % 16 == 0, a K-tile is 16 channels of one tap (float4 loads);
+// otherwise (the 3-channel stem) each k is decoded separately.
+template <bool FAST>
+__global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
+  __shared__ float sA[16][68];
+  __shared__ float sB[16][68];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int M = a.N * a.Ho * a.Wo, K = a.kh * a.kw * a.Cin;
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  // this thread's load slot: row (pixel / channel) t >> 2, k quad (t & 3) * 4
+  const int lr = t >> 2, kq = (t & 3) * 4;
+  const int m = m0 + lr;
+  const bool mval = m < M;
+  int nimg = 0, oy = 0, ox = 0;
+  if (mval) {
+    nimg = m / (a.Ho * a.Wo);
+    const int r = m - nimg * a.Ho * a.Wo;
+    oy = r / a.Wo;
+    ox = r - oy * a.Wo;
+  }
+  const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
+  const float* xb = a.x + (int64_t)nimg * a.H * a.W * a.Cin;
+  const float* wrow = a.w + (int64_t)(n0 + lr) * K;
+  const int nk = (K + 15) / 16;
+  const int cpt = FAST ? a.Cin / 16 : 1;   // K-tiles per tap
+
+  f32x4v ra, rb;
+  auto load = [&](int kt) {
+    if constexpr (FAST) {
+      const int tap = kt / cpt, c0 = (kt - tap * cpt) * 16 + kq;
+      const int ky = tap / a.kw, kx = tap - ky * a.kw;
+      const int iy = iy0 + ky, ix = ix0 + kx;
+      if (mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+        ra = *reinterpret_cast<const f32x4v*>(xb + ((int64_t)iy * a.W + ix) * a.Cin + c0);
+      else
+        ra = f32x4v{0.f, 0.f, 0.f, 0.f};
+      rb = *reinterpret_cast<const f32x4v*>(wrow + kt * 16 + kq);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = kt * 16 + kq + j;
+        float va = 0.f, vb = 0.f;
+        if (k < K) {
+          const int tap = k / a.Cin, c = k - tap * a.Cin;
+          const int ky = tap / a.kw, kx = tap - ky * a.kw;
+          const int iy = iy0 + ky, ix = ix0 + kx;
+          if (mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) va = xb[((int64_t)iy * a.W + ix) * a.Cin + c];
+          vb = wrow[k];
+        }
+        ra[j] = va;
+        rb[j] = vb;
+      }
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sA[kq + j][lr] = ra[j];
+      sB[kq + j][lr] = rb[j];
+    }
+  };
+
+  f32x4v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  stash();
+  __syncthreads();
+  const int li = lane & 15, lk = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load(kt + 1);
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const int kk = k4 * 4 + lk;
+      float fa[2], fb[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) fa[p] = sA[kk][wr * 32 + p * 16 + li];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) fb[c] = sB[kk][wc * 32 + c * 16 + li];
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[c], fa[p], acc[p][c], 0, 0, 0);
+    }
+    __syncthreads();
+    if (kt + 1 < nk) {
+      stash();
+      __syncthreads();
+    }
+  }
+  // lane holds channels n0 + wc*32 + c*16 + 4*lk + (0..3) of pixel m0 + wr*32 + p*16 + li
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int mo = m0 + wr * 32 + p * 16 + li;
+    if (mo >= M) continue;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int no = n0 + wc * 32 + c * 16 + 4 * lk;
+      f32x4v v = acc[p][c];
+      if (a.bias) v += *reinterpret_cast<const f32x4v*>(a.bias + no);
+      if (a.resid) v += *reinterpret_cast<const f32x4v*>(a.resid + (int64_t)mo * a.Cout + no);
+      if (a.flags & MMT_CONV_RELU)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+      f32x4v* dst = reinterpret_cast<f32x4v*>(a.y + (int64_t)mo * a.Cout + no);
+      if (a.flags & MMT_CONV_MAX) {
+        const f32x4v o = *dst;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(o[j], v[j]);   // torch.max(color, depth) (dimpnet.py:103)
+      }
+      *dst = v;
+    }
+  }
+}
+
+// max over a k x k window, stride s, zero-free padding (padded taps never win: -inf), NHWC
+__global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ x, int N, int H, int W, int C, int k,
+                                                      int s, int pad, int Ho, int Wo, float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * Ho * Wo * C;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  int64_t r = i / C;
+  const int ox = (int)(r % Wo);
+  r /= Wo;
+  const int oy = (int)(r % Ho);
+  const int n = (int)(r / Ho);
+  float m = -INFINITY;
+  for (int dy = 0; dy < k; ++dy) {
+    const int iy = oy * s - pad + dy;
+    if (iy < 0 || iy >= H) continue;
+    for (int dx = 0; dx < k; ++dx) {
+      const int ix = ox * s - pad + dx;
+      if (ix < 0 || ix >= W) continue;
+      m = fmaxf(m, x[(((int64_t)n * H + iy) * W + ix) * C + c]);
+    }
+  }
+  y[i] = m;
+}
+
+// NCHW [N][C][H][W] pixel values (0..255) -> per 3-channel half NHWC ((v / 255) - mean) / std
+// (net_wrappers.py:62-72: color and depth halves normalised with the same ImageNet constants)
+__global__ __launch_bounds__(256) void normalize_kernel(const float* __restrict__ im, int N, int C, int H, int W,
+                                                        float m0, float m1, float m2, float s0, float s1, float s2,
+                                                        float* __restrict__ outa, float* __restrict__ outb) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t HW = (int64_t)H * W;
+  if (i >= (int64_t)N * HW) return;
+  const int n = (int)(i / HW);
+  const int64_t p = i - n * HW;
+  const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    if (c >= C) break;
+    float v = im[((int64_t)n * C + c) * HW + p] / 255.f;
+    v = v - mean[c % 3];
+    v = v / sd[c % 3];
+    float* o = c < 3 ? outa : outb;
+    o[(n * HW + p) * 3 + (c % 3)] = v;
+  }
+}
+
+// InstanceL2Norm (size_average): y = x * (scale * sqrt((1 / (sum x^2 + eps)) * C*H*W)); one workgroup per
+// sample, fixed-order tree reduction; writes NHWC and/or NCHW
+__global__ __launch_bounds__(1024) void l2norm_kernel(const float* __restrict__ x, int HW, int C, float scale,
+                                                      float eps, float* __restrict__ y_nhwc, float* __restrict__ y_nchw) {
+  __shared__ float red[1024];
+  const int n = blockIdx.x;
+  const int64_t L = (int64_t)HW * C;
+  const float* xs = x + n * L;
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < L; i += 1024) s += xs[i] * xs[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float f = sqrtf((1.0f / (red[0] + eps)) * (float)L) * scale;
+  for (int64_t i = threadIdx.x; i < L; i += 1024) {
+    const float v = xs[i] * f;
+    if (y_nhwc) y_nhwc[n * L + i] = v;
+    if (y_nchw) {
+      const int c = (int)(i % C);
+      const int64_t p = i / C;
+      y_nchw[n * L + (int64_t)c * HW + p] = v;
+    }
+  }
+}
+
+// ---- PrRoIPool2D (prroi_pooling_gpu_impl.cu forward, restated): the integral of the bilinear surface
+// through the feature cells over each bin, / bin area; cells outside the map read as 0
+__device__ __forceinline__ float prroi_get(const float* d, int h, int w, int H, int W, int C) {
+  return (h < 0 || w < 0 || h >= H || w >= W) ? 0.f : d[((int64_t)h * W + w) * C];
+}
+__device__ __forceinline__ float prroi_cell(const float* d, int sh, int sw, int eh, int ew, float y0, float x0,
+                                            float y1, float x1, int H, int W, int C) {
+  float alpha = x0 - (float)sw, beta = y0 - (float)sh;
+  float la = x1 - (float)sw, lb = y1 - (float)sh;
+  float sum = 0.f, tmp;
+  tmp = (la - 0.5f * la * la - alpha + 0.5f * alpha * alpha) * (lb - 0.5f * lb * lb - beta + 0.5f * beta * beta);
+  sum += prroi_get(d, sh, sw, H, W, C) * tmp;
+  alpha = (float)ew - x1;
+  la = (float)ew - x0;
+  tmp = (la - 0.5f * la * la - alpha + 0.5f * alpha * alpha) * (lb - 0.5f * lb * lb - beta + 0.5f * beta * beta);
+  sum += prroi_get(d, sh, ew, H, W, C) * tmp;
+  alpha = x0 - (float)sw;
+  beta = (float)eh - y1;
+  la = x1 - (float)sw;
+  lb = (float)eh - y0;
+  tmp = (la - 0.5f * la * la - alpha + 0.5f * alpha * alpha) * (lb - 0.5f * lb * lb - beta + 0.5f * beta * beta);
+  sum += prroi_get(d, eh, sw, H, W, C) * tmp;
+  alpha = (float)ew - x1;
+  la = (float)ew - x0;
+  tmp = (la - 0.5f * la * la - alpha + 0.5f * alpha * alpha) * (lb - 0.5f * lb * lb - beta + 0.5f * beta * beta);
+  sum += prroi_get(d, eh, ew, H, W, C) * tmp;
+  return sum;
+}
+
+// feat NHWC [N][H][W][C]; rois [N][4] (x0, y0, x1, y1) image coordinates; out [N][C][PH][PW]
+__global__ __launch_bounds__(256) void prroi_kernel(const float* __restrict__ feat, int N, int H, int W, int C,
+                                                    const float* __restrict__ rois, float scale, int PH, int PW,
+                                                    float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)N * C * PH * PW) return;
+  const int pw = (int)(i % PW), ph = (int)((i / PW) % PH), c = (int)((i / PW / PH) % C), n = (int)(i / PW / PH / C);
+  const float* r = rois + n * 4;
+  const float rsw = r[0] * scale, rsh = r[1] * scale, rew = r[2] * scale, reh = r[3] * scale;
+  const float rw = fmaxf(rew - rsw, 0.f), rh = fmaxf(reh - rsh, 0.f);
+  const float bh = rh / (float)PH, bw = rw / (float)PW;
+  const float ws = rsw + bw * pw, hs = rsh + bh * ph;
+  const float we = ws + bw, he = hs + bh;
+  const float area = fmaxf(0.f, bw * bh);
+  if (area == 0.f) {
+    out[i] = 0.f;
+    return;
+  }
+  const float* d = feat + (int64_t)n * H * W * C + c;
+  float sum = 0.f;
+  const int sw = (int)floorf(ws), ew = (int)ceilf(we), sh = (int)floorf(hs), eh = (int)ceilf(he);
+  for (int wi = sw; wi < ew; ++wi)
+    for (int hi = sh; hi < eh; ++hi)
+      sum += prroi_cell(d, hi, wi, hi + 1, wi + 1, fmaxf(hs, (float)hi), fmaxf(ws, (float)wi), fminf(he, (float)hi + 1.0f),
+                        fminf(we, (float)(wi + 1)), H, W, C);
+  out[i] = sum / area;
+}
+
+// ---- sample_patch: crop rows [tl_y, tl_y + sz_h) x cols [tl_x, tl_x + sz_w) of the df-strided image
+// (im[..., os::df, os::df]) with replicate padding, resized to out_h x out_w by F.interpolate(bilinear,
+// align_corners=False); float NCHW out [C][out_h][out_w].  The float ops follow ATen's CPU upsample
+// (scale = in / out in float, src = max(scale * (dst + 0.5) - 0.5, 0), (x00*w0 + x01*w1)*h0 + (...)*h1).
+struct PatchGeom {
+  int df, os_y, os_x, tl_y, tl_x, sz_h, sz_w, H2, W2;
+};
+__device__ __forceinline__ float frame_px(const uint8_t* f, int64_t rs, int C, const PatchGeom& g, int cy, int cx, int c) {
+  int r = g.tl_y + cy, q = g.tl_x + cx;
+  r = min(max(r, 0), g.H2 - 1);
+  q = min(max(q, 0), g.W2 - 1);
+  return (float)f[(int64_t)(g.os_y + r * g.df) * rs + (int64_t)(g.os_x + q * g.df) * C + c];
+}
+__global__ __launch_bounds__(256) void sample_patch_kernel(const uint8_t* __restrict__ f, int64_t rs, int C, PatchGeom g,
+                                                           int oh, int ow, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)oh * ow) return;
+  const int oy = (int)(i / ow), ox = (int)(i - (int64_t)oy * ow);
+  if (g.sz_h == oh && g.sz_w == ow) {
+    for (int c = 0; c < C; ++c) out[(int64_t)c * oh * ow + i] = frame_px(f, rs, C, g, oy, ox, c);
+    return;
+  }
+  // ATen's CPU kernel (UpSampleKernel.cpp, built with FMA contraction): src = scale * (dst + 0.5) - 0.5 as
+  // one fma, t = x0 * w0 then += x1 * w1 as an fma, likewise across rows
+  const float sy = (float)g.sz_h / (float)oh, sx = (float)g.sz_w / (float)ow;
+  float fy = __builtin_fmaf(sy, (float)oy + 0.5f, -0.5f), fx = __builtin_fmaf(sx, (float)ox + 0.5f, -0.5f);
+  fy = fy < 0.f ? 0.f : fy;
+  fx = fx < 0.f ? 0.f : fx;
+  const int y0 = (int)fy, x0 = (int)fx;
+  const int y1 = y0 + (y0 < g.sz_h - 1 ? 1 : 0), x1 = x0 + (x0 < g.sz_w - 1 ? 1 : 0);
+  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+  for (int c = 0; c < C; ++c) {
+    const float t0 = __builtin_fmaf(frame_px(f, rs, C, g, y0, x1, c), lx1, frame_px(f, rs, C, g, y0, x0, c) * lx0);
+    const float t1 = __builtin_fmaf(frame_px(f, rs, C, g, y1, x1, c), lx1, frame_px(f, rs, C, g, y1, x0, c) * lx0);
+    out[(int64_t)c * oh * ow + i] = __builtin_fmaf(t1, ly1, t0 * ly0);
+  }
+}
+
+// ---- init-sample transforms (augmentation.py): out[c][oy][ox] = T(img)[clamp(oy - top)][clamp(ox - left)]
+// (crop_to_output: replicate pad / crop by floor / ceil of (out - in) / 2 plus the transform's shift)
+struct PatchTf {
+  int kind;            // MMT_TF_*
+  int top, left;       // crop_to_output offsets (pad_top, pad_left)
+  int ry, rx;          // blur radii
+  float fy[33], fx[33];
+  double m[6];         // rotate: OpenCV warpAffine matrix (dst -> src, inverted on the host), row-major 2 x 3
+};
+__device__ __forceinline__ float img_at(const float* im, int E_h, int E_w, int y, int x) {
+  return im[(int64_t)y * E_w + x];
+}
+__global__ __launch_bounds__(256) void patch_tf_kernel(const float* __restrict__ img, int C, int E_h, int E_w, PatchTf t,
+                                                       int oh, int ow, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)C * oh * ow) return;
+  const int c = (int)(i / ((int64_t)oh * ow));
+  const int64_t p = i - (int64_t)c * oh * ow;
+  const int oy = (int)(p / ow), ox = (int)(p - (int64_t)oy * ow);
+  const int y = min(max(oy - t.top, 0), E_h - 1), x = min(max(ox - t.left, 0), E_w - 1);
+  const float* im = img + (int64_t)c * E_h * E_w;
+  float v;
+  if (t.kind == MMT_TF_FLIP) {
+    v = img_at(im, E_h, E_w, y, E_w - 1 - x);
+  } else if (t.kind == MMT_TF_BLUR) {
+    // vertical pass then horizontal (F.conv2d with zero padding, augmentation.py Blur)
+    v = 0.f;
+    for (int kx = -t.rx; kx <= t.rx; ++kx) {
+      const int xx = x + kx;
+      if (xx < 0 || xx >= E_w) continue;
+      float col = 0.f;
+      for (int ky = -t.ry; ky <= t.ry; ++ky) {
+        const int yy = y + ky;
+        if (yy < 0 || yy >= E_h) continue;
+        col += img_at(im, E_h, E_w, yy, xx) * t.fy[ky + t.ry];
+      }
+      v += col * t.fx[kx + t.rx];
+    }
+  } else if (t.kind == MMT_TF_ROTATE) {
+    // cv2.warpAffine(INTER_LINEAR, BORDER_REPLICATE) on a float image: source coordinates in 1/32 pixel
+    // fixed point (AB_BITS 10, INTER_BITS 5, round_delta 16), bilinear weights from the 32 x 32 table
+    const int X0 = __double2int_rn((t.m[1] * y + t.m[2]) * 1024.0) + 16;
+    const int Y0 = __double2int_rn((t.m[4] * y + t.m[5]) * 1024.0) + 16;
+    const int X = (X0 + __double2int_rn(t.m[0] * x * 1024.0)) >> 5;
+    const int Y = (Y0 + __double2int_rn(t.m[3] * x * 1024.0)) >> 5;
+    const int sx = X >> 5, sy = Y >> 5;
+    const float ax = (float)(X & 31) * (1.0f / 32), ay = (float)(Y & 31) * (1.0f / 32);
+    const float w00 = (1.f - ay) * (1.f - ax), w01 = (1.f - ay) * ax, w10 = ay * (1.f - ax), w11 = ay * ax;
+    const int x0 = min(max(sx, 0), E_w - 1), x1 = min(max(sx + 1, 0), E_w - 1);
+    const int y0 = min(max(sy, 0), E_h - 1), y1 = min(max(sy + 1, 0), E_h - 1);
+    v = img_at(im, E_h, E_w, y0, x0) * w00 + img_at(im, E_h, E_w, y0, x1) * w01 + img_at(im, E_h, E_w, y1, x0) * w10 +
+        img_at(im, E_h, E_w, y1, x1) * w11;
+  } else {
+    v = img_at(im, E_h, E_w, y, x);
+  }
+  out[i] = v;
+}
+
+}  // namespace mmt
+
+using namespace mmt;
+
+static inline unsigned blocks_for(int64_t n, int per = 256) { return (unsigned)((n + per - 1) / per); }
+static inline int last_err() { return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP; }
+
+extern "C" {
+
+int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w, const float* bias, int Cout, int kh,
+                   int kw, int stride, int pad, const float* resid, float* y, int flags, void* stream) {
+  if (!x || !w || !y || N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || Cout % 64 || kh <= 0 || kw <= 0 ||
+      stride <= 0 || pad < 0 || (flags & ~(MMT_CONV_RELU | MMT_CONV_MAX)))
+    return MMT_E_ARG;
+  ConvArgs a{x, w, bias, resid, y, N, H, W, Cin, Cout, kh, kw, stride, pad, 0, 0, flags};
+  a.Ho = (H + 2 * pad - kh) / stride + 1;
+  a.Wo = (W + 2 * pad - kw) / stride + 1;
+  if (a.Ho <= 0 || a.Wo <= 0) return MMT_E_ARG;
+  const int64_t M = (int64_t)N * a.Ho * a.Wo;
+  if (M > (int64_t)1 << 30 || (int64_t)Cout * kh * kw * Cin > (int64_t)1 << 30) return MMT_E_ARG;
+  const dim3 grid(blocks_for(M, 64), Cout / 64);
+  if (Cin % 16 == 0)
+    hipLaunchKernelGGL(conv_f32_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(conv_f32_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  return last_err();
+}
+
+int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y, void* stream) {
+  if (!x || !y || N <= 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || stride <= 0 || pad < 0 || 2 * pad > k)
+    return MMT_E_ARG;
+  const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return MMT_E_ARG;
+  hipLaunchKernelGGL(maxpool_kernel, dim3(blocks_for((int64_t)N * Ho * Wo * C)), dim3(256), 0, (hipStream_t)stream, x, N,
+                     H, W, C, k, stride, pad, Ho, Wo, y);
+  return last_err();
+}
+
+int mmt_image_normalize(const float* im, int N, int C, int H, int W, const float mean[3], const float std_[3],
+                        float* out_a, float* out_b, void* stream) {
+  if (!im || !mean || !std_ || !out_a || N <= 0 || H <= 0 || W <= 0 || (C != 3 && C != 6) || (C == 6 && !out_b))
+    return MMT_E_ARG;
+  hipLaunchKernelGGL(normalize_kernel, dim3(blocks_for((int64_t)N * H * W)), dim3(256), 0, (hipStream_t)stream, im, N, C,
+                     H, W, mean[0], mean[1], mean[2], std_[0], std_[1], std_[2], out_a, out_b);
+  return last_err();
+}
+
+int mmt_instance_l2norm(const float* x, int N, int H, int W, int C, float scale, float eps, float* y_nhwc, float* y_nchw,
+                        void* stream) {
+  if (!x || (!y_nhwc && !y_nchw) || N <= 0 || H <= 0 || W <= 0 || C <= 0) return MMT_E_ARG;
+  hipLaunchKernelGGL(l2norm_kernel, dim3(N), dim3(1024), 0, (hipStream_t)stream, x, H * W, C, scale, eps, y_nhwc, y_nchw);
+  return last_err();
+}
+
+int mmt_prroi_pool(const float* feat, int N, int H, int W, int C, const float* rois, float spatial_scale, int PH, int PW,
+                   float* out, void* stream) {
+  if (!feat || !rois || !out || N <= 0 || H <= 0 || W <= 0 || C <= 0 || PH <= 0 || PW <= 0) return MMT_E_ARG;
+  hipLaunchKernelGGL(prroi_kernel, dim3(blocks_for((int64_t)N * C * PH * PW)), dim3(256), 0, (hipStream_t)stream, feat, N,
+                     H, W, C, rois, spatial_scale, PH, PW, out);
+  return last_err();
+}
+
+int mmt_sample_patch(const uint8_t* frame, int H, int W, int C, int64_t row_stride, const int geom[7], int out_h,
+                     int out_w, float* out, void* stream) {
+  if (!frame || !geom || !out || H <= 0 || W <= 0 || C <= 0 || row_stride < (int64_t)W * C || out_h <= 0 || out_w <= 0)
+    return MMT_E_ARG;
+  PatchGeom g{geom[0], geom[1], geom[2], geom[3], geom[4], geom[5], geom[6], 0, 0};
+  if (g.df < 1 || g.os_y < 0 || g.os_x < 0 || g.os_y >= g.df || g.os_x >= g.df || g.sz_h < 1 || g.sz_w < 1)
+    return MMT_E_ARG;
+  g.H2 = (H - g.os_y + g.df - 1) / g.df;
+  g.W2 = (W - g.os_x + g.df - 1) / g.df;
+  if (g.H2 <= 0 || g.W2 <= 0) return MMT_E_ARG;
+  hipLaunchKernelGGL(sample_patch_kernel, dim3(blocks_for((int64_t)out_h * out_w)), dim3(256), 0, (hipStream_t)stream,
+                     frame, row_stride, C, g, out_h, out_w, out);
+  return last_err();
+}
+
+int mmt_patch_transform(const float* img, int C, int E_h, int E_w, const mmt_patch_tf* tf, int out_h, int out_w,
+                        float* out, void* stream) {
+  if (!img || !tf || !out || C <= 0 || E_h <= 0 || E_w <= 0 || out_h <= 0 || out_w <= 0) return MMT_E_ARG;
+  PatchTf t{};
+  t.kind = tf->kind;
+  t.top = tf->top;
+  t.left = tf->left;
+  if (t.kind == MMT_TF_BLUR) {
+    if (tf->blur_ry < 0 || tf->blur_ry > 16 || tf->blur_rx < 0 || tf->blur_rx > 16) return MMT_E_ARG;
+    t.ry = tf->blur_ry;
+    t.rx = tf->blur_rx;
+    for (int k = 0; k < 33; ++k) {
+      t.fy[k] = tf->blur_fy[k];
+      t.fx[k] = tf->blur_fx[k];
+    }
+  } else if (t.kind == MMT_TF_ROTATE) {
+    for (int k = 0; k < 6; ++k) t.m[k] = tf->affine[k];
+  } else if (t.kind != MMT_TF_IDENTITY && t.kind != MMT_TF_FLIP) {
+    return MMT_E_ARG;
+  }
+  hipLaunchKernelGGL(patch_tf_kernel, dim3(blocks_for((int64_t)C * out_h * out_w)), dim3(256), 0, (hipStream_t)stream, img,
+                     C, E_h, E_w, t, out_h, out_w, out);
+  return last_err();
+}
+
+}  // extern "C"

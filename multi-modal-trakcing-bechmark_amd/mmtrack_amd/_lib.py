@@ -46,9 +46,22 @@ class MmtDimpParams(ctypes.Structure):
         ("alpha_eps", ctypes.c_float),
         ("bin_displacement", ctypes.c_float),
         ("num_dist_bins", ctypes.c_int),
-        ("label_w", ctypes.c_float * 32),
-        ("mask_w", ctypes.c_float * 32),
-        ("spatial_w", ctypes.c_float * 32),
+        ("label_w", ctypes.c_float * 128),
+        ("mask_w", ctypes.c_float * 128),
+        ("spatial_w", ctypes.c_float * 128),
+    ]
+
+
+class MmtPatchTf(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int),
+        ("top", ctypes.c_int),
+        ("left", ctypes.c_int),
+        ("blur_ry", ctypes.c_int),
+        ("blur_rx", ctypes.c_int),
+        ("blur_fy", ctypes.c_float * 33),
+        ("blur_fx", ctypes.c_float * 33),
+        ("affine", ctypes.c_double * 6),
     ]
 
 
@@ -87,6 +100,13 @@ SIGNATURES = {
     "mmt_rgbd_assemble": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _I, _I, _I, _P, _P, ctypes.c_int64, _P,
                                ctypes.c_size_t, _P]),
     "mmt_set_frame_stream": (_I, [_P, _P]),
+    "mmt_conv2d_f32": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "mmt_maxpool2d_f32": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "mmt_image_normalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "mmt_instance_l2norm": (_I, [_P, _I, _I, _I, _I, _F, _F, _P, _P, _P]),
+    "mmt_prroi_pool": (_I, [_P, _I, _I, _I, _I, _P, _F, _I, _I, _P, _P]),
+    "mmt_sample_patch": (_I, [_P, _I, _I, _I, ctypes.c_int64, _P, _I, _I, _P, _P]),
+    "mmt_patch_transform": (_I, [_P, _I, _I, _I, ctypes.POINTER(MmtPatchTf), _I, _I, _P, _P]),
     "mmt_rgbx_merge": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _I, _I, _I, _P, ctypes.c_int64, _P]),
     "mmt_dimp_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I]),
     "mmt_dimp_apply_filter": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -71,8 +71,8 @@ class DiMPSteepestDescentGN:
 
     def __init__(self, state_dict, num_iter=1, feat_stride=16, min_filter_reg=1e-3, alpha_eps=0.0,
                  num_dist_bins=10, bin_displacement=0.5, detach_length=float("inf")):
-        if num_dist_bins > 32:
-            raise ValueError("num_dist_bins must be <= 32")
+        if num_dist_bins > 128:
+            raise ValueError("num_dist_bins must be <= 128")
         self.num_iter = num_iter
         p = _lib.MmtDimpParams()
         p.feat_stride = feat_stride

@@ -1,0 +1,259 @@
+"""DeT / mfDiMP DiMP-50 classification path on the HIP kernels (mmt_conv2d_f32 & co, include/mmtrack.h).
+
+``DiMPNet`` is DiMPnet_DeT with merge_type 'max' (RGBD/models/DeT/ltr/models/tracking/dimpnet.py:15-156,
+built by dimp50_DeT, :421-476) as the DiMP tracker uses it (pytracking/tracker/dimp/dimp.py):
+
+* ``extract_backbone(patches)``      NetWithBackbone.extract_backbone (net_wrappers.py:81-85): normalise
+  each 3-channel half, two ResNet-50 backbones to layer3 (resnet.py), torch.max merge (dimpnet.py:103);
+* ``extract_classification_feat``    the clf feature block (features.py:47-66: 3x3 conv 1024 -> 512 without
+  bias, InstanceL2Norm) -> [N, 512, 18, 18] fp32 (NCHW, what the DiMP optimiser reads);
+* ``init_filter(feat, bb)``          FilterInitializerLinear (initializer.py:118-170): 3x3 conv, PrRoIPool2D
+  4 x 4 of the target box at 1/16, mean over the samples;
+* ``classify``                       LinearFilter.classify (linear_filter.py:78-83) = dimp.apply_filter.
+
+Weights load from the reference state_dict keys (load_state_dict strict on the keys this path reads;
+IoU-Net ``bb_regressor.*``, ``layer4`` and ``fc`` keys are accepted and unused).  BatchNorm (eval) is
+folded into each conv in float64 on the host.  Everything runs in fp32 on the device (the convolutions on
+v_mfma_f32_16x16x4_f32); there is no CPU fallback: a missing libmmtrack.so raises ImportError.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .synth import RESNET50_LAYERS, dimp_shapes
+
+MEAN = (0.485, 0.456, 0.406)
+STD = (0.229, 0.224, 0.225)
+
+
+def _rc(rc, what):
+    if rc == -1:
+        raise ValueError(f"{what}: invalid argument")
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc})")
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _Conv:
+    """One conv (+ folded BN): weight [Cout][kh][kw][Cin] and bias [Cout] fp32 on the device."""
+
+    def __init__(self, w, bn=None, bias=None, stride=1, pad=0, dev=None):
+        w = w.detach().double()
+        co = w.shape[0]
+        b = bias.detach().double() if bias is not None else torch.zeros(co, dtype=torch.float64)
+        if bn is not None:
+            g, beta, mean, var = (t.detach().double() for t in bn)
+            s = g / torch.sqrt(var + 1e-5)
+            w = w * s.view(-1, 1, 1, 1)
+            b = (b - mean) * s + beta
+        self.w = w.permute(0, 2, 3, 1).contiguous().float().to(dev)
+        self.b = b.float().to(dev) if (bn is not None or bias is not None) else None
+        self.cout, self.cin, self.kh, self.kw = co, w.shape[1], w.shape[2], w.shape[3]
+        self.stride, self.pad = stride, pad
+
+    def out_hw(self, H, W):
+        return (H + 2 * self.pad - self.kh) // self.stride + 1, (W + 2 * self.pad - self.kw) // self.stride + 1
+
+    def __call__(self, lib, x, N, H, W, out, stream, relu=False, resid=None, merge_max=False):
+        flags = (1 if relu else 0) | (2 if merge_max else 0)
+        _rc(lib.mmt_conv2d_f32(_p(x), N, H, W, self.cin, _p(self.w), _p(self.b), self.cout, self.kh, self.kw,
+                               self.stride, self.pad, _p(resid), _p(out), flags, stream), "mmt_conv2d_f32")
+        return out
+
+
+class DiMPNet:
+    def __init__(self, state_dict, device=None, out_dim=512, filter_size=4, feat_stride=16):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("DiMPNet needs an MI355X (HIP device); there is no CPU path")
+        self.dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        missing = [k for k in dimp_shapes() if not k.endswith("num_batches_tracked") and k not in state_dict]
+        if missing:
+            raise RuntimeError("Error(s) in loading state_dict: missing keys " + ", ".join(missing[:8]))
+        for k, shp in dimp_shapes().items():
+            if k in state_dict and tuple(state_dict[k].shape) != tuple(shp) and not k.endswith("predictor.weight") \
+                    and not k.endswith("predictor.0.weight"):
+                raise RuntimeError(f"Error(s) in loading state_dict: size mismatch for {k}: "
+                                   f"{tuple(state_dict[k].shape)} vs {tuple(shp)}")
+        sd = {k: torch.as_tensor(v) for k, v in state_dict.items()}
+        self.sd_opt = {k[len("classifier.filter_optimizer."):]: v for k, v in sd.items()
+                       if k.startswith("classifier.filter_optimizer.")}
+        self.out_dim, self.filter_size, self.feat_stride = out_dim, filter_size, feat_stride
+        self.norm_scale = math.sqrt(1.0 / (out_dim * filter_size * filter_size))
+
+        def bn(pre):
+            return [sd[pre + s] for s in (".weight", ".bias", ".running_mean", ".running_var")]
+        self.backbones = []
+        for fe in ("feature_extractor", "feature_extractor_depth"):
+            stem = _Conv(sd[fe + ".conv1.weight"], bn(fe + ".bn1"), stride=2, pad=3, dev=self.dev)
+            blocks = []
+            for li, (planes, nb, stride) in enumerate(RESNET50_LAYERS):
+                for b in range(nb):
+                    pre = f"{fe}.layer{li + 1}.{b}"
+                    s = stride if b == 0 else 1
+                    c1 = _Conv(sd[pre + ".conv1.weight"], bn(pre + ".bn1"), dev=self.dev)
+                    c2 = _Conv(sd[pre + ".conv2.weight"], bn(pre + ".bn2"), stride=s, pad=1, dev=self.dev)
+                    c3 = _Conv(sd[pre + ".conv3.weight"], bn(pre + ".bn3"), dev=self.dev)
+                    ds = _Conv(sd[pre + ".downsample.0.weight"], bn(pre + ".downsample.1"), stride=s, dev=self.dev) \
+                        if b == 0 else None
+                    blocks.append((c1, c2, c3, ds))
+            self.backbones.append((stem, blocks))
+        self.clf = _Conv(sd["classifier.feature_extractor.0.weight"], pad=1, dev=self.dev)
+        self.fconv = _Conv(sd["classifier.filter_initializer.filter_conv.weight"], pad=1,
+                           bias=sd["classifier.filter_initializer.filter_conv.bias"], dev=self.dev)
+        self._mean = (ctypes.c_float * 3)(*MEAN)
+        self._std = (ctypes.c_float * 3)(*STD)
+        self._bufs = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _buf(self, name, n):
+        b = self._bufs.get(name)
+        if b is None or b.numel() < n:
+            b = self._bufs[name] = torch.empty(n, dtype=torch.float32, device=self.dev)
+        return b[:n]
+
+    def _resnet(self, bb, x, N, H, W, out, merge_max, s):
+        """One ResNet-50 to layer3 of NHWC x [N, H, W, 3]; writes (or max-merges into) out [N, H/16, W/16, 1024]."""
+        lib = self.lib
+        stem, blocks = bb
+        h, w = stem.out_hw(H, W)
+        t0 = self._buf("stem", N * h * w * 64)
+        stem(lib, x, N, H, W, t0, s, relu=True)
+        H2, W2 = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
+        cur = self._buf("ping", N * H2 * W2 * 256)
+        _rc(lib.mmt_maxpool2d_f32(_p(t0), N, h, w, 64, 3, 2, 1, _p(cur), s), "mmt_maxpool2d_f32")
+        H, W, C = H2, W2, 64
+        nxt_name = "pong"
+        for i, (c1, c2, c3, ds) in enumerate(blocks):
+            Ho, Wo = c2.out_hw(H, W)
+            a = self._buf("a", N * H * W * c1.cout)
+            c1(lib, cur, N, H, W, a, s, relu=True)
+            b = self._buf("b", N * Ho * Wo * c2.cout)
+            c2(lib, a, N, H, W, b, s, relu=True)
+            if ds is not None:
+                res = self._buf("res", N * Ho * Wo * ds.cout)
+                ds(lib, cur, N, H, W, res, s)
+            else:
+                res = cur
+            last = i == len(blocks) - 1
+            o = out if last else self._buf(nxt_name, N * Ho * Wo * c3.cout)
+            c3(lib, b, N, Ho, Wo, o, s, relu=True, resid=res, merge_max=merge_max and last)
+            cur, nxt_name = o, ("ping" if nxt_name == "pong" else "pong")
+            H, W, C = Ho, Wo, c3.cout
+        return H, W
+
+    # ------------------------------------------------------------------ the network's tracker-side entry points
+    def extract_backbone(self, im):
+        """im: [N, 6, H, W] fp32 CUDA pixel values (0..255) -> merged layer3 NHWC [N, H/16, W/16, 1024]."""
+        if not (isinstance(im, torch.Tensor) and im.is_cuda and im.dtype == torch.float32 and im.dim() == 4
+                and im.shape[1] == 6):
+            raise ValueError("im must be an [N, 6, H, W] float32 CUDA tensor")
+        im = im.contiguous()
+        N, _, H, W = im.shape
+        s = self._stream()
+        xa = self._buf("xa", N * H * W * 3)
+        xb = self._buf("xb", N * H * W * 3)
+        _rc(self.lib.mmt_image_normalize(_p(im), N, 6, H, W, self._mean, self._std, _p(xa), _p(xb), s),
+            "mmt_image_normalize")
+        Hf, Wf = (H + 15) // 16, (W + 15) // 16
+        out = torch.empty(N, Hf, Wf, 1024, dtype=torch.float32, device=self.dev)
+        # the aux backbone's last conv max-merges into the RGB backbone's layer3 (dimpnet.py:103)
+        h, w = self._resnet(self.backbones[0], xa, N, H, W, out, False, s)
+        self._resnet(self.backbones[1], xb, N, H, W, out, True, s)
+        assert (h, w) == (Hf, Wf)
+        return out
+
+    def extract_classification_feat(self, layer3, nhwc=False):
+        """layer3 NHWC [N, h, w, 1024] -> clf features [N, 512, h, w] (and the NHWC copy when nhwc=True)."""
+        N, h, w, _ = layer3.shape
+        s = self._stream()
+        t = self._buf("clf", N * h * w * self.out_dim)
+        self.clf(self.lib, layer3, N, h, w, t, s)
+        out = torch.empty(N, self.out_dim, h, w, dtype=torch.float32, device=self.dev)
+        out_nhwc = torch.empty(N, h, w, self.out_dim, dtype=torch.float32, device=self.dev) if nhwc else None
+        _rc(self.lib.mmt_instance_l2norm(_p(t), N, h, w, self.out_dim, self.norm_scale, 1e-5, _p(out_nhwc), _p(out), s),
+            "mmt_instance_l2norm")
+        return (out, out_nhwc) if nhwc else out
+
+    def init_filter(self, feat_nhwc, bb):
+        """feat_nhwc [N, h, w, 512] (extract_classification_feat(..., nhwc=True)[1]); bb [N, 4] xywh (sample
+        coordinates) -> filter [1, 512, fs, fs]."""
+        N, h, w, C = feat_nhwc.shape
+        s = self._stream()
+        f = self._buf("fconv", N * h * w * C)
+        self.fconv(self.lib, feat_nhwc, N, h, w, f, s)
+        bb = torch.as_tensor(bb, dtype=torch.float32).reshape(-1, 4).clone()
+        bb[:, 2:4] = bb[:, 0:2] + bb[:, 2:4]
+        rois = bb.to(self.dev)
+        fs = self.filter_size
+        pooled = torch.empty(N, C, fs, fs, dtype=torch.float32, device=self.dev)
+        _rc(self.lib.mmt_prroi_pool(_p(f), N, h, w, C, _p(rois), 1.0 / self.feat_stride, fs, fs, _p(pooled), s),
+            "mmt_prroi_pool")
+        return pooled.mean(0, keepdim=True) if N > 1 else pooled
+
+    def classify(self, weights, feat):
+        from .dimp import apply_filter
+        return apply_filter(feat.reshape(-1, 1, *feat.shape[-3:]), weights)
+
+
+def sample_patch_device(frame, geom, out_hw):
+    """mmt_sample_patch: frame H x W x C uint8 CUDA tensor, geom (df, os_y, os_x, tl_y, tl_x, sz_h, sz_w)
+    -> [1, C, out_h, out_w] fp32 CUDA tensor."""
+    lib = _lib.load()
+    H, W, C = frame.shape
+    out = torch.empty(1, C, int(out_hw[0]), int(out_hw[1]), dtype=torch.float32, device=frame.device)
+    g = (ctypes.c_int * 7)(*[int(v) for v in geom])
+    _rc(lib.mmt_sample_patch(_p(frame), H, W, C, frame.stride(0), g, int(out_hw[0]), int(out_hw[1]), _p(out),
+                             ctypes.c_void_p(torch.cuda.current_stream(frame.device).cuda_stream)), "mmt_sample_patch")
+    return out
+
+
+def patch_transform_device(img, tf, out_hw):
+    """mmt_patch_transform of a [1, C, E_h, E_w] fp32 CUDA patch with one _lib.MmtPatchTf -> [1, C, oh, ow]."""
+    lib = _lib.load()
+    _, C, Eh, Ew = img.shape
+    img = img.contiguous()
+    out = torch.empty(1, C, int(out_hw[0]), int(out_hw[1]), dtype=torch.float32, device=img.device)
+    _rc(lib.mmt_patch_transform(_p(img), C, Eh, Ew, ctypes.byref(tf), int(out_hw[0]), int(out_hw[1]), _p(out),
+                                ctypes.c_void_p(torch.cuda.current_stream(img.device).cuda_stream)),
+        "mmt_patch_transform")
+    return out
+
+
+def conv2d(x_nchw, w, bias=None, stride=1, pad=0, resid=None, relu=False):
+    """Test / tool helper: torch NCHW conv through mmt_conv2d_f32 (weights nn.Conv2d layout)."""
+    lib = _lib.load()
+    conv = _Conv(w, bias=bias, stride=stride, pad=pad, dev=x_nchw.device)
+    N, C, H, W = x_nchw.shape
+    Ho, Wo = conv.out_hw(H, W)
+    x = x_nchw.permute(0, 2, 3, 1).contiguous()
+    out = torch.empty(N, Ho, Wo, conv.cout, dtype=torch.float32, device=x.device)
+    r = resid.permute(0, 2, 3, 1).contiguous() if resid is not None else None
+    conv(lib, x, N, H, W, out, ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream), relu=relu, resid=r)
+    return out.permute(0, 3, 1, 2)
+
+
+def prroi_pool(feat_nchw, rois_xyxy, spatial_scale, ph, pw):
+    """Test helper: PrRoIPool2D of roi n on image n."""
+    lib = _lib.load()
+    N, C, H, W = feat_nchw.shape
+    f = feat_nchw.permute(0, 2, 3, 1).contiguous()
+    out = torch.empty(N, C, ph, pw, dtype=torch.float32, device=f.device)
+    r = torch.as_tensor(rois_xyxy, dtype=torch.float32).reshape(N, 4).to(f.device)
+    _rc(lib.mmt_prroi_pool(_p(f), N, H, W, C, _p(r), spatial_scale, ph, pw, _p(out),
+                           ctypes.c_void_p(torch.cuda.current_stream(f.device).cuda_stream)), "mmt_prroi_pool")
+    return out
+
+
+__all__ = ["DiMPNet", "sample_patch_device", "patch_transform_device", "conv2d", "prroi_pool", "np"]

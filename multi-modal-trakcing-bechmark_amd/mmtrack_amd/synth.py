@@ -279,3 +279,125 @@ def make_patch(seed: int, size: int, C: int = 6) -> np.ndarray:
     col = rng.integers(0, 256, size=(C,)).astype(np.float32)
     img = bg * (1 - m) + col * m + rng.integers(-10, 11, size=(size, size, C))
     return np.clip(img, 0, 255).astype(np.uint8)
+
+
+# ----------------------------------------------------------------------------- DeT / mfDiMP DiMP-50
+RESNET50_LAYERS = ((64, 3, 1), (128, 4, 2), (256, 6, 2))   # (planes, blocks, stride) of layer1..layer3
+
+
+def dimp_shapes(num_dist_bins: int = 100, feature_dim: int = 256, out_dim: int = 512, filter_size: int = 4):
+    """The DiMPnet_DeT state_dict keys the classification path reads (dimpnet.py:421-476: two ResNet-50
+    backbones to layer3, the clf feature conv, FilterInitializerLinear, DiMPSteepestDescentGN)."""
+    shp = OrderedDict()
+    for fe in ("feature_extractor", "feature_extractor_depth"):
+        shp[f"{fe}.conv1.weight"] = (64, 3, 7, 7)
+        for t in ("weight", "bias", "running_mean", "running_var"):
+            shp[f"{fe}.bn1.{t}"] = (64,)
+        shp[f"{fe}.bn1.num_batches_tracked"] = ()
+        inplanes = 64
+        for li, (planes, blocks, stride) in enumerate(RESNET50_LAYERS):
+            for b in range(blocks):
+                pre = f"{fe}.layer{li + 1}.{b}"
+                cin = inplanes if b == 0 else planes * 4
+                for ci, (co, k, i) in enumerate(((planes, 1, cin), (planes, 3, planes), (planes * 4, 1, planes))):
+                    shp[f"{pre}.conv{ci + 1}.weight"] = (co, i, k, k)
+                    for t in ("weight", "bias", "running_mean", "running_var"):
+                        shp[f"{pre}.bn{ci + 1}.{t}"] = (co,)
+                    shp[f"{pre}.bn{ci + 1}.num_batches_tracked"] = ()
+                if b == 0:
+                    shp[f"{pre}.downsample.0.weight"] = (planes * 4, cin, 1, 1)
+                    for t in ("weight", "bias", "running_mean", "running_var"):
+                        shp[f"{pre}.downsample.1.{t}"] = (planes * 4,)
+                    shp[f"{pre}.downsample.1.num_batches_tracked"] = ()
+            inplanes = planes * 4
+    shp["classifier.feature_extractor.0.weight"] = (out_dim, 4 * feature_dim, 3, 3)
+    shp["classifier.filter_initializer.filter_conv.weight"] = (out_dim, out_dim, 3, 3)
+    shp["classifier.filter_initializer.filter_conv.bias"] = (out_dim,)
+    shp["classifier.filter_optimizer.log_step_length"] = (1,)
+    shp["classifier.filter_optimizer.filter_reg"] = (1,)
+    shp["classifier.filter_optimizer.label_map_predictor.weight"] = (1, num_dist_bins, 1, 1)
+    shp["classifier.filter_optimizer.target_mask_predictor.0.weight"] = (1, num_dist_bins, 1, 1)
+    shp["classifier.filter_optimizer.spatial_weight_predictor.weight"] = (1, num_dist_bins, 1, 1)
+    return shp
+
+
+def make_dimp_state_dict(seed: int = 0, num_dist_bins: int = 100, bin_displacement: float = 0.1,
+                         init_gauss_sigma: float = 0.9, mask_init_factor: float = 3.0, init_step_length: float = 0.9,
+                         init_filter_reg: float = 0.1) -> "OrderedDict[str, torch.Tensor]":
+    """Seeded fp32 DiMP-50 (DeT) weights: He-normal convs as the reference initialises them
+    (resnet.py: normal(0, sqrt(2 / (k*k*out)))), non-trivial BatchNorm statistics so the host-side BN
+    folding is exercised, and the optimiser's learnt maps at their constructor values for the DeT
+    training settings (train_settings/dimp/DeT_DiMP50_Max.py:101-106: 100 bins of 0.1, sigma 0.9,
+    mask factor 3, step 0.9, reg 0.1; optimizer.py:37-64).
+
+    A trained ResNet's BatchNorm statistics are its data's statistics; random convs with arbitrary
+    statistics give near-constant (all-positive, DC-dominated) layer3 maps that no filter can localise on.
+    So the running mean / variance of every BN are calibrated in float64 on a seeded 96 x 96 synthetic
+    image (``_calibrate_bn``), which makes each conv's output unit-normalised before its affine, as in a
+    trained network; and the clf feature conv's filters are zero-mean (a trained one responds to the
+    post-ReLU features' variation, so the 19 x 19 scores of the synthetic tracker peak near 0.3-0.7)."""
+    sd = OrderedDict()
+    d = torch.arange(num_dist_bins, dtype=torch.float32).reshape(1, -1, 1, 1) * bin_displacement
+    gauss = torch.exp(-1 / 2 * (d / init_gauss_sigma) ** 2)
+    fixed = {
+        "classifier.filter_optimizer.log_step_length": math.log(init_step_length) * torch.ones(1),
+        "classifier.filter_optimizer.filter_reg": init_filter_reg * torch.ones(1),
+        "classifier.filter_optimizer.label_map_predictor.weight": gauss - gauss.min(),
+        "classifier.filter_optimizer.target_mask_predictor.0.weight": mask_init_factor * torch.tanh(2.0 - d),
+        "classifier.filter_optimizer.spatial_weight_predictor.weight": torch.ones(1, num_dist_bins, 1, 1),
+    }
+    for k, shp in dimp_shapes(num_dist_bins).items():
+        g = _gen(seed, k)
+        if k in fixed:
+            v = fixed[k]
+        elif k.endswith("num_batches_tracked"):
+            v = torch.tensor(0, dtype=torch.int64)
+        elif k.endswith("running_var"):
+            v = torch.rand(shp, generator=g) + 0.5
+        elif k.endswith("running_mean"):
+            v = torch.randn(shp, generator=g) * 0.1
+        elif ".bn" in k or ".downsample.1." in k:
+            v = torch.rand(shp, generator=g) * 0.4 + 0.4 if k.endswith("weight") else torch.randn(shp, generator=g) * 0.1
+        elif k.endswith("filter_conv.bias"):
+            v = torch.zeros(shp)
+        else:   # conv weights
+            v = torch.randn(shp, generator=g) * math.sqrt(2.0 / (shp[0] * shp[2] * shp[3]))
+            if k == "classifier.feature_extractor.0.weight":   # respond to feature variation, not the DC
+                v = v - v.mean(dim=(1, 2, 3), keepdim=True)
+        sd[k] = v.float().contiguous() if v.dtype != torch.int64 else v
+    _calibrate_bn(sd, seed)
+    return sd
+
+
+def _calibrate_bn(sd, seed, size=96):
+    """Set every backbone BN's running_mean / running_var to its conv output's per-channel mean / variance
+    (float64, one seeded synthetic 6-channel image, ImageNet normalisation as net_wrappers.py:62-72)."""
+    import torch.nn.functional as F
+    im = torch.from_numpy(make_patch(seed + 9001, size, 6)).double().permute(2, 0, 1)[None]
+    mean = torch.tensor((0.485, 0.456, 0.406), dtype=torch.float64).view(1, -1, 1, 1)
+    std = torch.tensor((0.229, 0.224, 0.225), dtype=torch.float64).view(1, -1, 1, 1)
+
+    def bn(x, pre):
+        m = x.mean(dim=(0, 2, 3))
+        v = x.var(dim=(0, 2, 3), unbiased=False) + 1e-3
+        sd[pre + ".running_mean"] = m.float()
+        sd[pre + ".running_var"] = v.float()
+        g, b = sd[pre + ".weight"].double(), sd[pre + ".bias"].double()
+        return (x - m.view(1, -1, 1, 1)) / torch.sqrt(sd[pre + ".running_var"].double().view(1, -1, 1, 1) + 1e-5) * \
+            g.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+
+    def conv(x, key, stride=1, pad=0):
+        return F.conv2d(x, sd[key].double(), stride=stride, padding=pad)
+    for fe, half in (("feature_extractor", im[:, :3]), ("feature_extractor_depth", im[:, 3:])):
+        x = ((half / 255) - mean) / std
+        x = F.relu(bn(conv(x, fe + ".conv1.weight", 2, 3), fe + ".bn1"))
+        x = F.max_pool2d(x, 3, 2, 1)
+        for li, (planes, blocks, stride) in enumerate(RESNET50_LAYERS):
+            for b in range(blocks):
+                pre = f"{fe}.layer{li + 1}.{b}"
+                s = stride if b == 0 else 1
+                out = F.relu(bn(conv(x, pre + ".conv1.weight"), pre + ".bn1"))
+                out = F.relu(bn(conv(out, pre + ".conv2.weight", s, 1), pre + ".bn2"))
+                out = bn(conv(out, pre + ".conv3.weight"), pre + ".bn3")
+                res = bn(conv(x, pre + ".downsample.0.weight", s), pre + ".downsample.1") if b == 0 else x
+                x = F.relu(out + res)

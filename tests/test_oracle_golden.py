@@ -198,3 +198,24 @@ def test_frames_oracle_properties():
     np.testing.assert_array_equal(fr[..., :3], rgb)
     # after the clip the far rows share the top code with the 3x-median clip value
     assert (fr[:5, :, 3:] == lut[255]).all()
+
+
+def test_dimpnet_oracle_matches_reference_golden():
+    """oracle/dimpnet.py (backbones + max merge, clf features, FilterInitializerLinear) == the reference
+    DiMPnet_DeT on the seeded weights (tests/golden/dimpnet_det.npz, make_golden_dimp.py)."""
+    import torch
+
+    from mmtrack_amd import synth
+    from oracle import dimpnet as odn
+    gd = np.load(os.path.join(GOLDEN, "dimpnet_det.npz"))
+    sd = synth.make_dimp_state_dict(0)
+    ims = torch.stack([torch.from_numpy(synth.make_patch(int(s), 288, 6)).float().permute(2, 0, 1)
+                       for s in gd["seeds"]])
+    with torch.no_grad():
+        l3 = odn.backbone(odn.preprocess(ims), sd)
+        clf = odn.clf_features(l3, sd)
+        filt = odn.init_filter(clf, torch.from_numpy(gd["boxes"]), sd)
+    np.testing.assert_allclose(l3.double().sum(dim=(1, 2, 3)).numpy(), gd["layer3_sum"], rtol=1e-5)
+    np.testing.assert_allclose(l3[:, ::32].numpy(), gd["layer3_ch"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(clf[:, ::8].numpy(), gd["clf_ch"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(filt.numpy(), gd["init_filter"], rtol=1e-4, atol=1e-7)
