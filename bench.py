@@ -50,6 +50,8 @@ WORKLOADS = {
                    "OSTrack RGB ViT-B, template 192 / search 384 (BASELINE configs[3])"),
 }
 GFLOP_PER_FRAME = {"vipt_deep_rgbt": 45.80, "vipt_deep_rgbd": 45.80, "ostrack384": 109.34}
+PEAK_FP32_MATRIX_TFLOPS = 157.3   # MI355X dense fp32 MFMA (v_mfma_f32_*_f32), MI355X_MICROARCH.md
+DIMP_WORKLOAD = "mfdimp_rgbt"     # BASELINE configs[4]: mfDiMP RGB-T, ResNet-50 features + DiMP inner loop
 PROBE_CLASSES = ("qkv", "proj", "fc1", "fc2", "attn", "conv1", "patch")
 
 
@@ -212,8 +214,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=32, help="sequences tracked per GPU per step")
-    ap.add_argument("--workload", default="vipt_deep_rgbt", choices=list(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=None, help="sequences tracked per GPU per step (32; mfdimp: 8)")
+    ap.add_argument("--workload", default="vipt_deep_rgbt", choices=list(WORKLOADS) + [DIMP_WORKLOAD])
     ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16"),
                     help="fp32: parity mode (f16x3 split products); bf16: plain bf16 operands")
     ap.add_argument("--frames", type=int, default=8, help="distinct synthetic frames per sequence (cycled)")
@@ -238,9 +240,13 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")
+    if args.batch is None:
+        args.batch = 8 if args.workload == DIMP_WORKLOAD else 32
     if args.dry:
         return dry_main(args, rank, world, dist)
     torch.cuda.set_device(local)
+    if args.workload == DIMP_WORKLOAD:
+        return dimp_main(args, rank, world, dist)
 
     from mmtrack_amd import Engine, EngineConfig, synth
     ekw, skw, H, W, C, desc = WORKLOADS[args.workload]
@@ -334,6 +340,92 @@ def main():
         }
         print(json.dumps(line), flush=True)
     eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def dimp_main(args, rank, world, dist):
+    """C5: DeT/mfDiMP DiMP-50 tracking of B synthetic RGB-T sequences per GPU (mmtrack_amd.dimp_tracker):
+    a step = one frame of every sequence (patch sampling, two ResNet-50 backbones + clf features for the
+    batch, grouped filter application, per-sequence localisation / memory / Gauss-Newton updates)."""
+    from mmtrack_amd import synth
+    from mmtrack_amd.dimp_tracker import DiMP, parameters, track_batch
+    from mmtrack_amd.dimpnet import DiMPNet
+    B, H, W, C = args.batch, 480, 640, 6
+    sd = synth.make_dimp_state_dict(0)
+    net = DiMPNet(sd)
+    video_np, gts = synth.make_frames(1000 + rank, args.frames + 1, H, W, C)
+    video = torch.from_numpy(video_np).cuda()
+    trackers = [DiMP(parameters(), net=net) for _ in range(B)]
+    torch.manual_seed(rank)
+    for i, t in enumerate(trackers):
+        t.initialize(video[0], {"init_bbox": [60.0 + (37 * i) % (W - 160), 40.0 + (23 * i) % (H - 120),
+                                               40.0 + (i % 5) * 6, 32.0 + (i % 3) * 8]})
+    torch.cuda.synchronize()
+
+    def run(k0, n):
+        for k in range(k0, k0 + n):
+            track_batch(trackers, [video[1 + k % args.frames]] * B)
+
+    run(0, max(args.warmup, 2))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run(args.warmup, args.steps)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    value, elapsed, world = aggregate_throughput(B, args.steps, t1 - t0)
+    # roofline: the feature net (fp32 MFMA convs, >99 % of the step's FLOPs) timed with HIP events on the
+    # stream its kernels run on (torch's current stream)
+    patches = torch.rand(B, 6, 288, 288, device="cuda") * 255
+    net.extract_classification_feat(net.extract_backbone(patches))
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    ev0.record()
+    for _ in range(reps):
+        net.extract_classification_feat(net.extract_backbone(patches))
+    ev1.record()
+    torch.cuda.synchronize()
+    feat_ms = ev0.elapsed_time(ev1) / reps
+    flops = net.flops() * B
+    achieved = flops / (feat_ms * 1e-3) / 1e12
+    roof = {"bound": "mfma", "kernel": "conv_f32_kernel (2 x ResNet-50 to layer3 + clf conv, per batch)",
+            "achieved": round(achieved, 1), "peak": PEAK_FP32_MATRIX_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_MATRIX_TFLOPS, 4), "traffic": None,
+            "flop_per_launch_group": flops, "avg_batch_ms": round(feat_ms, 4),
+            "peak_note": "dense fp32 matrix (v_mfma_f32_16x16x4_f32): the DiMP path runs at the reference's fp32"}
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            from oracle import dimp as od
+            from oracle import dimpnet as odn
+            torch.set_num_threads(cpu_quota())
+            im = torch.rand(1, 6, 288, 288) * 255
+            filt = torch.randn(1, 512, 4, 4) * 0.01
+            n, tc = 0, time.perf_counter()
+            with torch.no_grad():
+                while time.perf_counter() - tc < args.cpu_seconds or n == 0:
+                    f = odn.clf_features(odn.backbone(odn.preprocess(im), sd), sd)
+                    od.apply_filter(f.unsqueeze(1), filt)
+                    n += 1
+            dt = time.perf_counter() - tc
+            cpu = {"value": round(n / dt, 3), "unit": "frames/s", "cores": cpu_quota(), "kind": "port",
+                   "sample": f"{n} frames of the fp32 CPU oracle DiMP-50 feature net + classifier "
+                             f"(oracle/dimpnet.py, {cpu_quota()} threads, {dt:.1f} s)"}
+        line = {"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "config": {"workload": DIMP_WORKLOAD, "description": "mfDiMP RGB-T (DeT DiMP-50, merge max): "
+                           "ResNet-50 x2 features + DiMP online optimiser (BASELINE configs[4])",
+                           "sequences_per_gpu": B, "global_batch": B * world, "frame": f"{W}x{H}x{C} uint8 (HBM)",
+                           "image_sample_size": 288, "parallelism": f"seq-shard x{world}",
+                           "weights": "synthetic seeded (no checkpoint ships)"},
+                "per_gpu_fps": round(value / world, 2), "model_tflops": round(value * net.flops() / 1e12, 2),
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
 

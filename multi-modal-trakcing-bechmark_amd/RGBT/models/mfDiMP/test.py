@@ -1,11 +1,15 @@
-"""mfDiMP classifier inner loop on RGB-T features (the RGBT/benchmark.py 'mfDiMP' entry).
+"""mfDiMP RGB-T tracking (the RGBT/benchmark.py 'mfDiMP' entry) on the MI355X path.
 
-The reference's mfDiMP source is an empty submodule (RGBT/models/end2end_rgbt_tracking/); what this
-build provides is DiMP's target-classifier optimiser (DeT's ltr filter.py / optimizer.py restated as
-HIP, mmtrack_amd.dimp). This driver times that inner loop at the DiMP tracker's shapes
-(pytracking/parameter/dimp/DeT_DiMP50_Max.py:10-28: 512-d clf features, 18x18 at 288^2 input,
-4x4 filter, sample memory 50, net_opt_iter 10 at init / 2 per update), with seeded fused RGB-T
-features standing in for the ResNet-50 layer3 + clf-feature extractor (not built this round).
+The reference's mfDiMP source is an empty submodule (RGBT/models/end2end_rgbt_tracking/); the in-tree
+multi-modal DiMP is DeT's DiMP-50 (two ResNet-50 backbones, 'max' feature merge, DiMP classifier), which
+this build runs as HIP kernels (mmtrack_amd.dimpnet / dimp / dimp_tracker).  This driver tracks seeded
+synthetic RGB-T sequences -- or a LasHeR / RGBT234 / GTOT folder with --seq_home -- one sequence per
+tracker, several sequences per GPU per launch (dimp_tracker.track_batch), sequences sharded over ranks
+(torchrun: sequence i on rank i % world, no collective), and writes one result file per sequence in the
+RGB-T workspace format (np.savetxt, test_rgbt_mgpus.py:116).
+
+    python RGBT/models/mfDiMP/test.py --synthetic 8 --frames 100 --batch 8
+    torchrun --nproc-per-node 4 --master-addr 127.0.0.1 RGBT/models/mfDiMP/test.py --synthetic 32
 """
 import argparse
 import os
@@ -13,39 +17,65 @@ import sys
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.normpath(os.path.join(HERE, "..", "..", "..")))
+PRJ = os.path.normpath(os.path.join(HERE, "..", "..", ".."))
+sys.path.insert(0, PRJ)
 
 
 def main(argv=None):
+    import numpy as np
     import torch
-    from mmtrack_amd.dimp import DiMPSteepestDescentGN, apply_filter
+
+    from mmtrack_amd import synth
+    from mmtrack_amd.dimp_tracker import DiMP, parameters, track_batch
+    from mmtrack_amd.dimpnet import DiMPNet
+    from mmtrack_amd.sharding import rank_world, shard_indices
+    from mmtrack_amd.workspace import frame_getter, gen_config, sequence_list
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sequences", type=int, default=8, help="sequences optimised together (S)")
+    ap.add_argument("--synthetic", type=int, default=8, help="seeded synthetic sequences (0: use --seq_home)")
     ap.add_argument("--frames", type=int, default=100)
-    ap.add_argument("--memory", type=int, default=50)
+    ap.add_argument("--seq_home", default="")
+    ap.add_argument("--dataset_name", default="LasHeR")
+    ap.add_argument("--batch", type=int, default=8, help="sequences tracked per launch")
+    ap.add_argument("--out_root", default=".")
     args = ap.parse_args(argv)
-    g = torch.Generator().manual_seed(0)
-    S, C, H, W = args.sequences, 512, 18, 18
-    sd = {"log_step_length": torch.tensor([0.0]), "filter_reg": torch.tensor([0.1]),
-          "label_map_predictor.weight": torch.linspace(1.0, -0.2, 10).view(1, 10, 1, 1),
-          "target_mask_predictor.0.weight": torch.linspace(3.0, -3.0, 10).view(1, 10, 1, 1),
-          "spatial_weight_predictor.weight": torch.ones(1, 10, 1, 1)}
-    opt = DiMPSteepestDescentGN(sd, num_iter=2)
-    dev = torch.device("cuda")
-    feat = (torch.randn(args.memory, S, C, H, W, generator=g) * 0.3).to(dev)
-    bb = torch.tensor([[[128.0, 128.0, 40.0, 30.0]] * S] * args.memory)
-    w = torch.zeros(S, C, 4, 4, device=dev)
-    w = opt.optimize(w, feat[:15], bb[:15], num_iter=10)          # initial filter (15 augmented samples)
+    rank, world = rank_world()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+    if args.synthetic:
+        seqs = []
+        for i in range(args.synthetic):
+            box = (150.0 + 31 * (i % 9), 100.0 + 17 * (i % 7), 40.0 + 4 * (i % 5), 32.0 + 3 * (i % 4))
+            fr, gt = synth.make_frames(i, args.frames, 480, 640, 6, box=box)
+            seqs.append((f"synthetic_{i:03d}", len(fr), (lambda f: (lambda k: f[k]))(fr), gt))
+    else:
+        seqs = []
+        for name in sequence_list(args.seq_home, args.dataset_name):
+            rgb, aux, gt = gen_config(os.path.join(args.seq_home, name), args.dataset_name)
+            seqs.append((name, len(rgb), frame_getter(rgb, aux, 'rgbrgb'), gt))
+    mine = [seqs[i] for i in shard_indices(len(seqs), rank, world)]
+    net = DiMPNet(synth.make_dimp_state_dict(0))
+    out_dir = os.path.join(args.out_root, "RGBT_workspace", "results", args.dataset_name, "mfDiMP")
+    os.makedirs(out_dir, exist_ok=True)
+    t0, tracked = time.perf_counter(), 0
+    for b0 in range(0, len(mine), args.batch):
+        group = mine[b0:b0 + args.batch]
+        trackers = [DiMP(parameters(), net=net) for _ in group]
+        results = [np.zeros((n, 4)) for _, n, _, _ in group]
+        for tr, (name, n, get, gt), res in zip(trackers, group, results):
+            tr.initialize(get(0), {"init_bbox": list(np.asarray(gt[0], dtype=np.float64))})
+            res[0] = gt[0]
+        for k in range(1, max(n for _, n, _, _ in group)):
+            live = [i for i, (_, n, _, _) in enumerate(group) if k < n]
+            outs = track_batch([trackers[i] for i in live], [group[i][2](k) for i in live])
+            for i, o in zip(live, outs):
+                results[i][k] = o["target_bbox"]
+            tracked += len(live)
+        for (name, _, _, _), res in zip(group, results):
+            np.savetxt(os.path.join(out_dir, name + ".txt"), res)
     torch.cuda.synchronize()
-    t0 = time.time()
-    for f in range(1, args.frames):
-        test = feat[f % args.memory].unsqueeze(0)
-        scores = apply_filter(test, w)                           # classify the new frame
-        w = opt.optimize(w, feat, bb, num_iter=2)                 # update_classifier
-    torch.cuda.synchronize()
-    dt = time.time() - t0
-    print(f"mfDiMP classifier: {S} sequences x {args.frames - 1} frames in {dt:.3f}s -> "
-          f"{S * (args.frames - 1) / dt:.1f} frame-updates/s (scores {tuple(scores.shape)})")
+    dt = time.perf_counter() - t0
+    print(f"mfDiMP rank {rank}/{world}: {len(mine)} sequences, {tracked} tracked frames in {dt:.2f}s -> "
+          f"{tracked / max(dt, 1e-9):.1f} frames/s (init included)")
 
 
 if __name__ == "__main__":

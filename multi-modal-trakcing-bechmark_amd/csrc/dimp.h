@@ -5,6 +5,8 @@
 
 namespace mmt {
 
+constexpr int kDimpPosPerBlock = 32;   // output positions per dimp_filter workgroup (partial-sum granularity)
+
 struct DimpMaps {                 // label / target-mask / sample-weight maps from the distance bins
   int IS, Ho, Wo, nbins;
   float bin_disp;

@@ -31,23 +31,27 @@ __global__ __launch_bounds__(256) void dimp_maps_kernel(DimpMaps m) {
   m.sw[idx] = m.sqrt_sw[is] * spw;
 }
 
-// scores[i,s,y,x] = sum_c,ky,kx feat[i,s,c,y+ky-P,x+kx-P] * w[s,c,ky,kx]; mode 1/2 epilogues below
+// scores[i,s,y,x] = sum_c,ky,kx feat[i,s,c,y+ky-P,x+kx-P] * w[s,c,ky,kx]; mode 1/2 epilogues below.
+// One workgroup per (image * sequence, tile of kDimpPosPerBlock output positions): the 8 wave halves
+// (32 lanes each) take interleaved channel slices (c = group + 8 k) of the same 32 positions, so a frame's
+// 15-50 samples still spread over hundreds of workgroups; the 8 partial sums combine in a fixed order.
 __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   extern __shared__ float wsh[];
+  __shared__ float part[8][kDimpPosPerBlock];
   const int is = blockIdx.x;                  // image * S + sequence
   const int s = is % a.S;
   const int T = a.fh * a.fw;
   for (int k = threadIdx.x; k < a.C * T; k += 256) wsh[k] = a.w[(int64_t)s * a.C * T + k];
   __syncthreads();
   const int n = a.Ho * a.Wo;
-  const int p = blockIdx.y * 256 + threadIdx.x;
-  float r2 = 0.f;
+  const int lp = threadIdx.x & (kDimpPosPerBlock - 1), cg = threadIdx.x / kDimpPosPerBlock;
+  const int p = blockIdx.y * kDimpPosPerBlock + lp;
+  float acc = 0.f;
   if (p < n) {
     const int y = p / a.Wo, x = p - y * a.Wo;
     const int P0 = a.fh / 2, P1 = a.fw / 2;
     const float* f = a.feat + (int64_t)is * a.C * a.H * a.W;
-    float acc = 0.f;
-    for (int c = 0; c < a.C; ++c) {
+    for (int c = cg; c < a.C; c += 8) {
       const float* fc = f + (int64_t)c * a.H * a.W;
       const float* wc = wsh + c * T;
       for (int ky = 0; ky < a.fh; ++ky) {
@@ -60,6 +64,14 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
         }
       }
     }
+  }
+  part[cg][lp] = acc;
+  __syncthreads();
+  float r2 = 0.f;
+  if (cg == 0 && p < n) {
+    acc = part[0][lp];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) acc += part[g][lp];
     const int64_t o = (int64_t)is * n + p;
     if (a.mode == 0) {
       a.out[o] = acc;
@@ -77,15 +89,14 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
       r2 = g * g;
     }
   }
-  if (a.partial) {
-    __shared__ float red[256];
-    red[threadIdx.x] = r2;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-      if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) a.partial[(int64_t)is * gridDim.y + blockIdx.y] = red[0];
+  if (!a.partial) return;   // uniform over the workgroup
+  __syncthreads();          // every group has read its sums
+  if (cg == 0) part[0][lp] = r2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < kDimpPosPerBlock; ++k) t += part[0][k];
+    a.partial[(int64_t)is * gridDim.y + blockIdx.y] = t;
   }
 }
 
@@ -195,7 +206,7 @@ void dimp_maps(const DimpMaps& m, hipStream_t s) {
   hipLaunchKernelGGL(dimp_maps_kernel, dim3((n + 255) / 256), dim3(256), 0, s, m);
 }
 void dimp_filter(const DimpFilter& a, hipStream_t s) {
-  const int nby = (a.Ho * a.Wo + 255) / 256;
+  const int nby = (a.Ho * a.Wo + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
   hipLaunchKernelGGL(dimp_filter_kernel, dim3(a.I * a.S, nby), dim3(256), a.C * a.fh * a.fw * sizeof(float), s, a);
 }
 void dimp_transpose(const DimpTranspose& a, hipStream_t s) {

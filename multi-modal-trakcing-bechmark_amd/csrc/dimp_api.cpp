@@ -18,7 +18,7 @@ struct WsLayout {
 
 WsLayout layout(int I, int S, int C, int H, int W, int fh, int fw, int num_iter) {
   const size_t Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, n = Ho * Wo, IS = (size_t)I * S;
-  const size_t nby = (n + 255) / 256;
+  const size_t nby = (n + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
   WsLayout L{};
   size_t off = 0;
   auto take = [&](size_t floats) {
@@ -123,7 +123,7 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
   char* ws = static_cast<char*>(workspace);
   auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
   const int IS = I * S;
-  const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, n = Ho * Wo, nby = (n + 255) / 256;
+  const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, n = Ho * Wo, nby = (n + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
   // host-side per-sample constants (optimizer.py:108-125, same fp32 arithmetic)
   std::vector<float> centers(2 * IS), sqrtsw(IS), params(3 * 128, 0.f);
   const float off0 = (float)(fh % 2) / 2.0f, off1 = (float)(fw % 2) / 2.0f;

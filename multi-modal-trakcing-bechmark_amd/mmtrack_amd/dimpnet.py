@@ -153,6 +153,23 @@ class DiMPNet:
             H, W, C = Ho, Wo, c3.cout
         return H, W
 
+    def flops(self, H=288, W=288):
+        """Algorithmic FLOPs (2 x MACs) of extract_backbone + extract_classification_feat for one [6, H, W] image."""
+        total = 0
+        for stem, blocks in self.backbones:
+            h, w = stem.out_hw(H, W)
+            total += 2 * h * w * stem.cout * stem.kh * stem.kw * stem.cin
+            h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
+            for c1, c2, c3, ds in blocks:
+                ho, wo = c2.out_hw(h, w)
+                total += 2 * h * w * c1.cout * c1.cin
+                total += 2 * ho * wo * c2.cout * 9 * c2.cin
+                total += 2 * ho * wo * c3.cout * c3.cin
+                if ds is not None:
+                    total += 2 * ho * wo * ds.cout * ds.cin
+                h, w = ho, wo
+        return total + 2 * h * w * self.clf.cout * 9 * self.clf.cin
+
     # ------------------------------------------------------------------ the network's tracker-side entry points
     def extract_backbone(self, im):
         """im: [N, 6, H, W] fp32 CUDA pixel values (0..255) -> merged layer3 NHWC [N, H/16, W/16, 1024]."""
