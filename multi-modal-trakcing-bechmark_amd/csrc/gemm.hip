@@ -1200,12 +1200,23 @@ static bool launch256s_epi(const GemmArgs& a, int epi, hipStream_t s) {
   }
 }
 
+// super-tile height (tile rows walked together, column-major inside): 8 rows x all columns keeps a short-K
+// GEMM's weight slab shared per XCD; a long-K GEMM (fc2: K = 3072; the head conv: K = 6912) re-fetches its
+// large A row blocks once per column tile unless the row's column tiles run close together (gm = 2: head
+// conv 359 -> 339 us at 32 sequences, fc2 level, tests/sweep_gm_b32.sh)
+static int super_rows(int tiles_m, int K) {
+  static const int gm_env = getenv("MMT_GM") ? atoi(getenv("MMT_GM")) : 0;
+  static const int gm_long = getenv("MMT_GM_LONGK") ? atoi(getenv("MMT_GM_LONGK")) : 2;
+  const int gm = gm_env > 0 ? gm_env : (K >= 2048 ? gm_long : 8);
+  return tiles_m < gm ? tiles_m : gm;
+}
+
 template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int ST, int BK = 64>
 static void launch_one(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = a.N / BN;
   (void)tiles_n;
-  a.gm = tiles_m < 8 ? tiles_m : 8;
+  a.gm = super_rows(tiles_m, a.K);
   dim3 grid(tiles_m * tiles_n, 1, a.groups);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI, AM, SPLIT, ST, BK>), grid, dim3(WMW * WNW * 64), 0, s, a);
 }
@@ -1378,6 +1389,17 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
   // a little under one 128 x 128 tile per CU (the N = 768 GEMMs of the CE-pruned layers): 128 x 64 tiles
   // with 8 waves put two workgroups on most CUs (fc2 at M = 4896: 41.4 -> 34.8 us)
   const int t128n = t128 * (a.N / 128) * a.groups;
+  if constexpr (SPLIT) {
+    // f16x3 N = 768 GEMMs (proj, fc2, patch): 128 x 128 tiles at every M of the path (the 128 x 64 tiles
+    // that suit bf16's under-filled launches are slower here: the split GEMMs are 3x longer per tile); a short
+    // K streams 32-deep K-tiles (proj 51 -> 48 us, patch 98 -> 85 us at 32 sequences, tests/sweep_split_cfg_b32.sh),
+    // fc2's K = 3072 keeps 64-deep ones (144 -> 135 us)
+    static const bool old_rule = getenv("MMT_SPLIT_OLD") != nullptr;
+    if (!old_rule && a.amode == A_DENSE && a.N % 128 == 0 && t128n >= target) {
+      if (a.K <= 1024) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
+      return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);
+    }
+  }
   if (a.N % 128 == 0 && t128n >= target && t128n < num_cus()) return launch_cfg<128, 64, 4, 2, SPLIT>(a, epi, s);
   if (a.N % 128 == 0 && t128n >= target) return launch_cfg<128, 128, 4, 2, SPLIT>(a, epi, s);
   if (a.N % 64 == 0) {
@@ -1385,10 +1407,14 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // few 64 x 64 tiles and a long K (small batches): split K over workgroups (fp32 partials in the
     // workspace, fixed-order reduction with the epilogue), at least 4 K-tiles per split
     const int tiles = t64 * (a.N / 64) * a.groups, nk = a.K / 64;
-    if (a.ws && tiles < 128 && nk >= 8) {
-      int ks = (256 + tiles - 1) / tiles;
-      ks = ks < nk / 4 ? ks : nk / 4;
-      ks = ks < 8 ? ks : 8;
+    static const int sk_tiles = getenv("MMT_SPLITK_TILES") ? atoi(getenv("MMT_SPLITK_TILES")) : 128;
+    static const int sk_target = getenv("MMT_SPLITK_TARGET") ? atoi(getenv("MMT_SPLITK_TARGET")) : 256;
+    static const int sk_minkt = getenv("MMT_SPLITK_MINKT") ? atoi(getenv("MMT_SPLITK_MINKT")) : 4;
+    static const int sk_max = getenv("MMT_SPLITK_MAX") ? atoi(getenv("MMT_SPLITK_MAX")) : 8;
+    if (a.ws && tiles < sk_tiles && nk >= 2 * sk_minkt) {
+      int ks = (sk_target + tiles - 1) / tiles;
+      ks = ks < nk / sk_minkt ? ks : nk / sk_minkt;
+      ks = ks < sk_max ? ks : sk_max;
       while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems) --ks;
       if (ks > 1) {
         if (a.amode == A_CONV3) return launch_splitk<64, 64, 2, 2, A_CONV3, SPLIT, 4>(a, epi, ks, s);
