@@ -363,9 +363,20 @@ def dimp_main(args, rank, world, dist):
                                                40.0 + (i % 5) * 6, 32.0 + (i % 3) * 8]})
     torch.cuda.synchronize()
 
+    from mmtrack_amd.dimp_tracker import PipelinedBatch
+    pipe = PipelinedBatch(trackers) if not args.sync else None
+
     def run(k0, n):
+        """n frames of every sequence, all results on the host before returning (--sync: track_batch per
+        frame; default: two groups of sequences pipelined, host updates of one under the other's network)."""
         for k in range(k0, k0 + n):
-            track_batch(trackers, [video[1 + k % args.frames]] * B)
+            frames = [video[1 + k % args.frames]] * B
+            if pipe is None:
+                track_batch(trackers, frames)
+            else:
+                pipe.step(frames)
+        if pipe is not None:
+            pipe.flush()
 
     run(0, max(args.warmup, 2))
     torch.cuda.synchronize()

@@ -470,4 +470,59 @@ def track_batch(trackers, frames):
     return [t.track_update(test_x[i:i + 1], scores[i:i + 1], c) for i, (t, c) in enumerate(zip(trackers, coords))]
 
 
-__all__ = ["DiMP", "parameters", "TrackerParams", "track_batch", "ctypes"]
+class PipelinedBatch:
+    """track_batch with the host half of one group of sequences overlapped with the device half of the other:
+    the trackers are split into two groups; group g's frame k is sampled and its network launched
+    (asynchronously, its scores copied to pinned host memory behind an event) while the host localises and
+    updates group 1 - g from frame k - 1.  Per-sequence results are identical to track_batch (each tracker
+    still sees its frames in order; only the interleaving of different sequences' host work changes)."""
+
+    def __init__(self, trackers, groups=2):
+        self.trackers = trackers
+        n = len(trackers)
+        bounds = [round(i * n / groups) for i in range(groups + 1)]
+        self.groups = [list(range(bounds[i], bounds[i + 1])) for i in range(groups) if bounds[i + 1] > bounds[i]]
+        self.pending = [None] * len(self.groups)
+
+    def _start(self, g, frames):
+        idx = self.groups[g]
+        trs = [self.trackers[i] for i in idx]
+        net = trs[0].net
+        sz = trs[0].img_sample_sz.long().tolist()
+        patches = torch.empty(len(idx), 6, sz[0], sz[1], dtype=torch.float32, device=net.dev)
+        coords = [t.track_sample(frames[i], out=patches[j])[1] for j, (i, t) in enumerate(zip(idx, trs))]
+        test_x = net.extract_classification_feat(net.extract_backbone(patches))
+        from .dimp import apply_filter
+        scores = apply_filter(test_x.unsqueeze(0), torch.cat([t.target_filter for t in trs]))[0]
+        host = torch.empty(scores.shape, dtype=torch.float32, pin_memory=True)
+        host.copy_(scores, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending[g] = (idx, test_x, host, ev, coords)
+
+    def _finish(self, g, outs):
+        idx, test_x, host, ev, coords = self.pending[g]
+        self.pending[g] = None
+        ev.synchronize()
+        for j, i in enumerate(idx):
+            outs[i] = self.trackers[i].track_update(test_x[j:j + 1], host[j:j + 1], coords[j])
+
+    def step(self, frames):
+        """Submit frame k for every sequence; returns the outputs of frame k - 1 (None on the first call)."""
+        outs = [None] * len(self.trackers)
+        had = self.pending[0] is not None
+        for g in range(len(self.groups)):
+            if self.pending[g] is not None:
+                self._finish(g, outs)
+            self._start(g, frames)
+        return outs if had else None
+
+    def flush(self):
+        outs = [None] * len(self.trackers)
+        for g in range(len(self.groups)):
+            if self.pending[g] is not None:
+                self._finish(g, outs)
+        return outs
+
+
+__all__ = ["DiMP", "parameters", "TrackerParams", "track_batch", "PipelinedBatch", "ctypes"]

@@ -203,3 +203,35 @@ def test_dimp_tracker_matches_reference_sequence():
         dconf.append(abs(out["confidence"] - gd["confidence"][t]) / gd["confidence"][t])
         assert dconf[-1] < 1e-2, (t, out["confidence"], gd["confidence"][t])
     print("relative confidence differences per frame:", np.round(dconf, 5).tolist())
+
+
+def test_pipelined_batch_equals_sequential():
+    """PipelinedBatch (two groups, host updates overlapped with the other group's network) gives every
+    sequence exactly the results of tracking it alone with DiMP.track."""
+    from mmtrack_amd import synth
+    from mmtrack_amd.dimp_tracker import DiMP, PipelinedBatch, parameters
+    from mmtrack_amd.dimpnet import DiMPNet
+    net = DiMPNet(synth.make_dimp_state_dict(0))
+    seqs = [synth.make_frames(70 + i, 6, 360, 480, 6, box=(150.0 + 20 * i, 120.0, 44.0, 36.0)) for i in range(3)]
+
+    def fresh(i):
+        t = DiMP(parameters(), net=net)
+        torch.manual_seed(100 + i)
+        t.initialize(seqs[i][0][0], {"init_bbox": list(seqs[i][1][0])})
+        return t
+    ref = []
+    for i in range(3):
+        t = fresh(i)
+        ref.append([t.track(seqs[i][0][k])["target_bbox"] for k in range(1, 6)])
+    trs = [fresh(i) for i in range(3)]
+    pipe = PipelinedBatch(trs)
+    got = [[] for _ in range(3)]
+    for k in range(1, 6):
+        outs = pipe.step([seqs[i][0][k] for i in range(3)])
+        if outs is not None:
+            for i in range(3):
+                got[i].append(outs[i]["target_bbox"])
+    for i, o in enumerate(pipe.flush()):
+        got[i].append(o["target_bbox"])
+    for i in range(3):
+        np.testing.assert_allclose(np.array(got[i]), np.array(ref[i]), rtol=0, atol=1e-3)
