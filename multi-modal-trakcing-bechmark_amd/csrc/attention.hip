@@ -28,12 +28,16 @@ constexpr int CE_MAX = 1024;   // max tokens for the exported CE row
 #ifndef ATTN_WPE
 #define ATTN_WPE 4
 #endif
+// f16x3 4-wave kernel: no cap (145 VGPRs + 16 AGPRs, 3 waves per SIMD); 4 waves per SIMD spills 13 VGPRs
+#ifndef ATTN_WPE_SPLIT
+#define ATTN_WPE_SPLIT 1
+#endif
 
 // byte offset of 16-B chunk c of row r in a [64][64] bf16 tile (128-B rows, chunk XOR row)
 __device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 
 template <int WAVES, bool SPLIT, int RB = 1>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((SPLIT || WAVES < 4) ? 1 : ATTN_WPE))) void attn_kernel(const AttnArgs a) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVES < 4 ? 1 : (SPLIT ? ATTN_WPE_SPLIT : ATTN_WPE)))) void attn_kernel(const AttnArgs a) {
   // SPLIT (fp32-faithful f16x3, common.h): every operand is an (hi, lo) fp16 pair of a range-scaled
   // value and each product is hi*hi + lo*hi + hi*lo; the LDS images of K and V^T hold both halves.
   // RB: 16-query row blocks per wave, multiplied together against each K / V fragment (fragment
