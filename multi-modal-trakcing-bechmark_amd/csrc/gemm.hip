@@ -1395,7 +1395,8 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // K streams 32-deep K-tiles (proj 51 -> 48 us, patch 98 -> 85 us at 32 sequences, tests/sweep_split_cfg_b32.sh),
     // fc2's K = 3072 keeps 64-deep ones (144 -> 135 us)
     static const bool old_rule = getenv("MMT_SPLIT_OLD") != nullptr;
-    if (!old_rule && a.amode == A_DENSE && a.N % 128 == 0 && t128n >= target) {
+    static const int t128_min = getenv("MMT_SPLIT_T128") ? atoi(getenv("MMT_SPLIT_T128")) : target;
+    if (!old_rule && a.amode == A_DENSE && a.N % 128 == 0 && t128n >= t128_min) {
       if (a.K <= 1024) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
       return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);
     }
