@@ -1337,7 +1337,8 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // f16x3: the 8-phase 256 x 256 kernel where there are enough 256-wide column tiles (qkv, fc1: 250-300
     // TF/s vs 240-250 for the 2-barrier 128 x 128 kernel); N = 768 stays on 128-row tiles (3 column tiles of
     // 256 leave most CUs idle)
-    if (a.N >= 2048 && (a.M + 255) / 256 * (a.N / 256) * a.groups >= 128 && launch256s_epi(a, epi, s)) return;
+    static const int t256_min = getenv("MMT_256S_MIN") ? atoi(getenv("MMT_256S_MIN")) : 128;
+    if (a.N >= 2048 && (a.M + 255) / 256 * (a.N / 256) * a.groups >= t256_min && launch256s_epi(a, epi, s)) return;
   }
   if constexpr (!SPLIT) {
     if (g_force_cfg >= 0 && a.amode == A_DENSE) {
@@ -1390,12 +1391,13 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
   // with 8 waves put two workgroups on most CUs (fc2 at M = 4896: 41.4 -> 34.8 us)
   const int t128n = t128 * (a.N / 128) * a.groups;
   if constexpr (SPLIT) {
-    // f16x3 N = 768 GEMMs (proj, fc2, patch): 128 x 128 tiles at every M of the path (the 128 x 64 tiles
-    // that suit bf16's under-filled launches are slower here: the split GEMMs are 3x longer per tile); a short
+    // f16x3 N = 768 GEMMs (proj, fc2, patch): 128 x 128 tiles from 128 tiles up -- every M of the path in a
+    // two-stream half (the 128 x 64 tiles that suit bf16's under-filled launches are slower here: the split
+    // GEMMs are 3x longer per tile, and the other half fills the tail; +1.8 % vs from 200, sweep_t128.sh); a short
     // K streams 32-deep K-tiles (proj 51 -> 48 us, patch 98 -> 85 us at 32 sequences, tests/sweep_split_cfg_b32.sh),
     // fc2's K = 3072 keeps 64-deep ones (144 -> 135 us)
     static const bool old_rule = getenv("MMT_SPLIT_OLD") != nullptr;
-    static const int t128_min = getenv("MMT_SPLIT_T128") ? atoi(getenv("MMT_SPLIT_T128")) : target;
+    static const int t128_min = getenv("MMT_SPLIT_T128") ? atoi(getenv("MMT_SPLIT_T128")) : 128;
     if (!old_rule && a.amode == A_DENSE && a.N % 128 == 0 && t128n >= t128_min) {
       if (a.K <= 1024) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
       return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);

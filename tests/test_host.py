@@ -257,3 +257,32 @@ def test_vot_handle_offline_source():
             vot.VOT("rectangle", channels="rgbd")
     finally:
         builtins.__import__ = real_import
+
+
+def test_dimp_transform_structs():
+    """DiMP init augmentations (mmtrack_amd.dimp_tracker._Tf): crop_to_output offsets (augmentation.py
+    Transform.crop_to_output), normalised Gaussian blur taps, and the Rotate matrix inverted exactly as
+    cv2.warpAffine inverts it (the oracle's restatement) -- host logic only, no GPU."""
+    import math
+
+    import numpy as np
+    import torch
+
+    from mmtrack_amd.dimp_tracker import _Tf, parameters
+    t = _Tf(0, (288, 288), (86, -86)).c_struct((576, 576))
+    assert (t.top, t.left) == (-144 + 86, -144 - 86)
+    b = _Tf(2, (288, 288), None, sigma=(3, 1)).c_struct((576, 576))
+    assert (b.blur_ry, b.blur_rx) == (6, 2)
+    fy = np.array(b.blur_fy[:13])
+    np.testing.assert_allclose(fy.sum(), 1.0, rtol=1e-6)
+    np.testing.assert_allclose(fy, fy[::-1])
+    r = _Tf(3, (288, 288), None, angle=45).c_struct((576, 576))
+    a = math.pi / 4
+    c = (np.array([[576.0], [576.0]]) - 1) / 2
+    R = np.array([[math.cos(a), math.sin(a)], [-math.sin(a), math.cos(a)]])
+    H = np.vstack([np.concatenate([R, c - R @ c], 1), [0, 0, 1]])
+    inv = np.linalg.inv(H)[:2].reshape(-1)
+    np.testing.assert_allclose(np.array(r.affine[:]), inv, rtol=0, atol=1e-9)
+    p = parameters()
+    assert p.use_iou_net is False and p.net_opt_iter == 10 and p.sample_memory_size == 50
+    assert torch.is_tensor(torch.zeros(1))
