@@ -1398,8 +1398,10 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // fc2's K = 3072 keeps 64-deep ones (144 -> 135 us)
     static const bool old_rule = getenv("MMT_SPLIT_OLD") != nullptr;
     static const int t128_min = getenv("MMT_SPLIT_T128") ? atoi(getenv("MMT_SPLIT_T128")) : 128;
-    if (!old_rule && a.amode == A_DENSE && a.N % 128 == 0 && t128n >= t128_min) {
-      if (a.K <= 1024) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
+    static const bool conv_old = getenv("MMT_SPLIT_CONV_OLD") != nullptr;
+    if (!old_rule && (a.amode == A_DENSE || !conv_old) && a.N % 128 == 0 && t128n >= t128_min) {
+      // the head's implicit 3x3 conv (A_CONV3, K = 6912) gathers 64-channel K-tiles
+      if (a.K <= 1024 && a.amode == A_DENSE) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
       return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);
     }
   }

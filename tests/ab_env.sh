@@ -1,13 +1,9 @@
-# A/B of environment knobs on ONE box (box-to-box spread exceeds most single changes): runs bench.py
-# alternately under each "VAR=value ..." setting of AB_SETS (separated by ';'), ROUNDS times.
-# usage: ROUNDS=3 AB_SETS="MMT_X=0;MMT_X=1" ARGS="--batch 32" bash tests/ab_env.sh
+# A/B of an environment switch on one box (tuning tool): ENV_B="VAR=1" runs arm B with it, arm A without; 3 rounds
 set -e
-ROUNDS=${ROUNDS:-3}
-mkdir -p gpurun_out
-IFS=';' read -ra SETS <<< "$AB_SETS"
-for r in $(seq 1 $ROUNDS); do
-  for set in "${SETS[@]}"; do
-    v=$(env $set timeout -k 10 200 python bench.py --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline --probe none ${ARGS:-} 2>>gpurun_out/ab_err.log | python -c "import json,sys; print(json.loads(sys.stdin.read().strip().splitlines()[-1])['value'])")
-    echo "[$set] round $r: $v" | tee -a gpurun_out/ab.log
+for r in 1 2 3; do
+  for arm in A B; do
+    if [ $arm = B ]; then envs="$ENV_B"; else envs=""; fi
+    env $envs timeout -k 10 150 python bench.py --steps 50 --warmup 10 --no-cpu-baseline --host-frames 0 --probe none ${ARGS:-} > gpurun_out/abenv.json 2>/dev/null
+    python -c "import json; d=json.load(open('gpurun_out/abenv.json')); print('$arm round $r fps', d['value'])"
   done
 done
