@@ -307,6 +307,12 @@ static void attention_t(const AttnArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((attn_kernel<8, false>), dim3((a.N + 127) / 128 * bh), dim3(512), 0, s, a);
     return;
   }
+  // f16x3: 8 waves share one K / V (hi + lo) staging -- 116 VGPRs (4 waves per SIMD, no spills) against 145 +
+  // 16 AGPRs for 4 waves (+0.6 % end to end at 32 sequences, tests/ab_env.sh)
+  if (SPLIT && bh >= 128 && (w8 == 8 || w8 == 0)) {
+    hipLaunchKernelGGL((attn_kernel<8, true>), dim3((a.N + 127) / 128 * bh), dim3(512), 0, s, a);
+    return;
+  }
   if (per4 >= 240) {
     hipLaunchKernelGGL((attn_kernel<4, SPLIT>), dim3((a.N + 63) / 64 * bh), dim3(256), 0, s, a);
   } else if (per4 * 2 >= 240) {

@@ -1393,11 +1393,12 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
   if constexpr (SPLIT) {
     // f16x3 N = 768 GEMMs (proj, fc2, patch): 128 x 128 tiles from 128 tiles up -- every M of the path in a
     // two-stream half (the 128 x 64 tiles that suit bf16's under-filled launches are slower here: the split
-    // GEMMs are 3x longer per tile, and the other half fills the tail; +1.8 % vs from 200, sweep_t128.sh); a short
+    // GEMMs are 3x longer per tile, and the other half fills the tail; from 64 tiles: +1.8 % vs 200 and +1.9 %
+    // more vs 128 once the head convs (grouped, N = 3 x 128) take it too, sweep_t128.sh / ab_env.sh); a short
     // K streams 32-deep K-tiles (proj 51 -> 48 us, patch 98 -> 85 us at 32 sequences, tests/sweep_split_cfg_b32.sh),
     // fc2's K = 3072 keeps 64-deep ones (144 -> 135 us)
     static const bool old_rule = getenv("MMT_SPLIT_OLD") != nullptr;
-    static const int t128_min = getenv("MMT_SPLIT_T128") ? atoi(getenv("MMT_SPLIT_T128")) : 128;
+    static const int t128_min = getenv("MMT_SPLIT_T128") ? atoi(getenv("MMT_SPLIT_T128")) : 64;
     static const bool conv_old = getenv("MMT_SPLIT_CONV_OLD") != nullptr;
     if (!old_rule && (a.amode == A_DENSE || !conv_old) && a.N % 128 == 0 && t128n >= t128_min) {
       // the head's implicit 3x3 conv (A_CONV3, K = 6912) gathers 64-channel K-tiles
