@@ -1202,11 +1202,11 @@ static bool launch256s_epi(const GemmArgs& a, int epi, hipStream_t s) {
 
 // super-tile height (tile rows walked together, column-major inside): 8 rows x all columns keeps a short-K
 // GEMM's weight slab shared per XCD; a long-K GEMM (fc2: K = 3072; the head conv: K = 6912) re-fetches its
-// large A row blocks once per column tile unless the row's column tiles run close together (gm = 2: head
-// conv 359 -> 339 us at 32 sequences, fc2 level, tests/sweep_gm_b32.sh)
+// large A row blocks once per column tile unless the row's column tiles run close together (gm = 4: head
+// conv 359 -> 331 us at 32 sequences, fc2 level, tests/sweep_gm_b32.sh; +0.5 % over gm = 2, ab_env.sh)
 static int super_rows(int tiles_m, int K) {
   static const int gm_env = getenv("MMT_GM") ? atoi(getenv("MMT_GM")) : 0;
-  static const int gm_long = getenv("MMT_GM_LONGK") ? atoi(getenv("MMT_GM_LONGK")) : 2;
+  static const int gm_long = getenv("MMT_GM_LONGK") ? atoi(getenv("MMT_GM_LONGK")) : 4;
   const int gm = gm_env > 0 ? gm_env : (K >= 2048 ? gm_long : 8);
   return tiles_m < gm ? tiles_m : gm;
 }
