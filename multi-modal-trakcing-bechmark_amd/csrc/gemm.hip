@@ -1329,6 +1329,10 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         case 13: return launch_cfg<128, 256, 2, 4, true, 2, 32>(a, epi, s);
         case 14: if (launch256s_epi(a, epi, s)) return; break;
         case 15: if (a.N >= 2048 && launch256s_epi(a, epi, s)) return; break;
+        case 16: return launch_cfg<64, 64, 2, 2, true, 8, 32>(a, epi, s);
+        case 17: return launch_cfg<64, 64, 2, 2, true, 4, 32>(a, epi, s);
+        case 18: return launch_cfg<64, 64, 2, 2, true, 6, 32>(a, epi, s);
+        case 19: return launch_cfg<64, 64, 2, 2, true, 3, 64>(a, epi, s);
         default: break;
       }
     }
