@@ -1404,7 +1404,8 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     static const bool old_rule = getenv("MMT_SPLIT_OLD") != nullptr;
     static const int t128_min = getenv("MMT_SPLIT_T128") ? atoi(getenv("MMT_SPLIT_T128")) : 64;
     static const bool conv_old = getenv("MMT_SPLIT_CONV_OLD") != nullptr;
-    if (!old_rule && (a.amode == A_DENSE || !conv_old) && a.N % 128 == 0 && t128n >= t128_min) {
+    // (not for one sequence's few rows: fc1 at M = 320 keeps 240 64 x 64 workgroups instead of 72)
+    if (!old_rule && (a.amode == A_DENSE || !conv_old) && a.N % 128 == 0 && t128n >= t128_min && t128 >= 8) {
       // the head's implicit 3x3 conv (A_CONV3, K = 6912) gathers 64-channel K-tiles
       if (a.K <= 1024 && a.amode == A_DENSE) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
       return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);
@@ -1427,13 +1428,16 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
       ks = ks < sk_max ? ks : sk_max;
       while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems) --ks;
       if (ks > 1) {
-        if (a.amode == A_CONV3) return launch_splitk<64, 64, 2, 2, A_CONV3, SPLIT, 4>(a, epi, ks, s);
-        return launch_splitk<64, 64, 2, 2, A_DENSE, SPLIT, 4>(a, epi, ks, s);
+        // f16x3: a 3-deep ring (96 KB of LDS) beat 4-deep at one sequence (tests/sweep_ring_b1.sh)
+        constexpr int SKST = SPLIT ? 3 : 4;
+        if (a.amode == A_CONV3) return launch_splitk<64, 64, 2, 2, A_CONV3, SPLIT, SKST>(a, epi, ks, s);
+        return launch_splitk<64, 64, 2, 2, A_DENSE, SPLIT, SKST>(a, epi, ks, s);
       }
     }
-    // few tiles (small batches): each workgroup walks the whole K serially, so keep three K-tiles in
-    // flight (4-deep LDS ring; an 8-deep ring measured no better at M = 320)
-    if (a.K >= 6 * 64) return launch_cfg<64, 64, 2, 2, SPLIT, 4>(a, epi, s);
+    // few tiles (small batches): each workgroup walks the whole K serially, so keep K-tiles in flight
+    // (bf16: 4-deep LDS ring, an 8-deep one measured no better at M = 320; f16x3: 3-deep, qkv 17.3 ->
+    // 15.4 us and fc1 16.8 -> 16.5 us at one sequence, tests/sweep_ring_b1.sh)
+    if (a.K >= 6 * 64) return launch_cfg<64, 64, 2, 2, SPLIT, SPLIT ? 3 : 4>(a, epi, s);
     return launch_cfg<64, 64, 2, 2, SPLIT>(a, epi, s);
   }
   if (t64 * (a.N / 32) * a.groups >= target) return launch_cfg<64, 32, 4, 1, SPLIT>(a, epi, s);
