@@ -16,6 +16,7 @@
 // precision; 157 TF/s dense fp32 matrix peak).  Activations NHWC, weights [Cout][kh][kw][Cin].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/mmtrack.h"
 
@@ -38,21 +39,23 @@ struct ConvArgs {
 // ---------------------------------------------------------------------------------------------------
 // Implicit-GEMM convolution: C[m][n] = sum_k A[m][k] W[n][k], m = output pixel, n = output channel,
 // k = (ky, kx, c).  64 x 64 output tile, 4 waves (2 x 2, each 32 pixels x 32 channels = 2 x 2 MFMA blocks),
-// K-tiles of 16 staged through LDS k-major ([k][64 + 4], conflict-free fragment reads), the next K-tile's
+// K-tiles of 32 (16 when Cin % 32 != 0) staged through LDS k-major ([k][64 + 4], conflict-free fragment
+// reads), the next K-tile's
 // global loads held in registers while the current one is multiplied.  The MFMA is issued W x A so a lane
 // ends with 4 consecutive output channels of one pixel: 16-B NHWC stores with bias / residual / ReLU /
-// running-max epilogues.  FAST: Cin % 16 == 0, a K-tile is 16 channels of one tap (float4 loads);
+// running-max epilogues.  FAST: a K-tile is BK channels of one tap (float4 loads);
 // otherwise (the 3-channel stem) each k is decoded separately.
-template <bool FAST>
+template <bool FAST, int BK>
 __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
-  __shared__ float sA[16][68];
-  __shared__ float sB[16][68];
+  constexpr int VPT = BK / 4;   // K values per thread per K-tile (A and W each)
+  __shared__ float sA[BK][68];
+  __shared__ float sB[BK][68];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int M = a.N * a.Ho * a.Wo, K = a.kh * a.kw * a.Cin;
   const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
-  // this thread's load slot: row (pixel / channel) t >> 2, k quad (t & 3) * 4
-  const int lr = t >> 2, kq = (t & 3) * 4;
+  // this thread's load slot: row (pixel / channel) t >> 2, K offset (t & 3) * VPT
+  const int lr = t >> 2, kq = (t & 3) * VPT;
   const int m = m0 + lr;
   const bool mval = m < M;
   int nimg = 0, oy = 0, ox = 0;
@@ -65,24 +68,26 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
   const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
   const float* xb = a.x + (int64_t)nimg * a.H * a.W * a.Cin;
   const float* wrow = a.w + (int64_t)(n0 + lr) * K;
-  const int nk = (K + 15) / 16;
-  const int cpt = FAST ? a.Cin / 16 : 1;   // K-tiles per tap
+  const int nk = (K + BK - 1) / BK;
+  const int cpt = FAST ? a.Cin / BK : 1;   // K-tiles per tap
 
-  f32x4v ra, rb;
+  f32x4v ra[VPT / 4], rb[VPT / 4];
   auto load = [&](int kt) {
     if constexpr (FAST) {
-      const int tap = kt / cpt, c0 = (kt - tap * cpt) * 16 + kq;
+      const int tap = kt / cpt, c0 = (kt - tap * cpt) * BK + kq;
       const int ky = tap / a.kw, kx = tap - ky * a.kw;
       const int iy = iy0 + ky, ix = ix0 + kx;
-      if (mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-        ra = *reinterpret_cast<const f32x4v*>(xb + ((int64_t)iy * a.W + ix) * a.Cin + c0);
-      else
-        ra = f32x4v{0.f, 0.f, 0.f, 0.f};
-      rb = *reinterpret_cast<const f32x4v*>(wrow + kt * 16 + kq);
+      const bool ok = mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const float* src = xb + ((int64_t)iy * a.W + ix) * a.Cin + c0;
+#pragma unroll
+      for (int v = 0; v < VPT / 4; ++v) {
+        ra[v] = ok ? *reinterpret_cast<const f32x4v*>(src + 4 * v) : f32x4v{0.f, 0.f, 0.f, 0.f};
+        rb[v] = *reinterpret_cast<const f32x4v*>(wrow + kt * BK + kq + 4 * v);
+      }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = kt * 16 + kq + j;
+      for (int j = 0; j < VPT; ++j) {
+        const int k = kt * BK + kq + j;
         float va = 0.f, vb = 0.f;
         if (k < K) {
           const int tap = k / a.Cin, c = k - tap * a.Cin;
@@ -91,16 +96,16 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
           if (mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) va = xb[((int64_t)iy * a.W + ix) * a.Cin + c];
           vb = wrow[k];
         }
-        ra[j] = va;
-        rb[j] = vb;
+        ra[j / 4][j % 4] = va;
+        rb[j / 4][j % 4] = vb;
       }
     }
   };
   auto stash = [&]() {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      sA[kq + j][lr] = ra[j];
-      sB[kq + j][lr] = rb[j];
+    for (int j = 0; j < VPT; ++j) {
+      sA[kq + j][lr] = ra[j / 4][j % 4];
+      sB[kq + j][lr] = rb[j / 4][j % 4];
     }
   };
 
@@ -117,7 +122,7 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + 1 < nk) load(kt + 1);
 #pragma unroll
-    for (int k4 = 0; k4 < 4; ++k4) {
+    for (int k4 = 0; k4 < BK / 4; ++k4) {
       const int kk = k4 * 4 + lk;
       float fa[2], fb[2];
 #pragma unroll
@@ -409,10 +414,14 @@ int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w,
   const int64_t M = (int64_t)N * a.Ho * a.Wo;
   if (M > (int64_t)1 << 30 || (int64_t)Cout * kh * kw * Cin > (int64_t)1 << 30) return MMT_E_ARG;
   const dim3 grid(blocks_for(M, 64), Cout / 64);
-  if (Cin % 16 == 0)
-    hipLaunchKernelGGL(conv_f32_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  // 32-deep K-tiles (half the barriers per MFMA) where a tile stays inside one tap; 16 for Cin = 48 / 16
+  static const int bk = getenv("MMT_CONV_BK") ? atoi(getenv("MMT_CONV_BK")) : 32;
+  if (Cin % 32 == 0 && bk == 32)
+    hipLaunchKernelGGL((conv_f32_kernel<true, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  else if (Cin % 16 == 0)
+    hipLaunchKernelGGL((conv_f32_kernel<true, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(conv_f32_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((conv_f32_kernel<false, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);
   return last_err();
 }
 
