@@ -31,7 +31,6 @@ for _p in (REPO, os.path.join(REPO, "multi-modal-trakcing-bechmark_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)

@@ -20,7 +20,6 @@ the reference run with the same seed.
 """
 from __future__ import annotations
 
-import ctypes
 import math
 
 import numpy as np
@@ -164,7 +163,7 @@ class DiMP:
         br = posl + szl // 2 + 1
         geom = [df, int(os_[0]), int(os_[1]), int(tl[0]), int(tl[1]), int(szl[0]), int(szl[1])]
         patch = sample_patch_device(frame, geom, output_sz.long().tolist())
-        return patch.permute(0, 1, 2, 3), df * torch.cat((tl, br)).view(1, 4)
+        return patch, df * torch.cat((tl, br)).view(1, 4)
 
     # ------------------------------------------------------------------ reference API
     def initialize(self, image, info: dict) -> dict:
@@ -525,4 +524,4 @@ class PipelinedBatch:
         return outs
 
 
-__all__ = ["DiMP", "parameters", "TrackerParams", "track_batch", "PipelinedBatch", "ctypes"]
+__all__ = ["DiMP", "parameters", "TrackerParams", "track_batch", "PipelinedBatch"]

@@ -21,7 +21,6 @@ from __future__ import annotations
 import ctypes
 import math
 
-import numpy as np
 import torch
 
 from . import _lib
@@ -273,4 +272,4 @@ def prroi_pool(feat_nchw, rois_xyxy, spatial_scale, ph, pw):
     return out
 
 
-__all__ = ["DiMPNet", "sample_patch_device", "patch_transform_device", "conv2d", "prroi_pool", "np"]
+__all__ = ["DiMPNet", "sample_patch_device", "patch_transform_device", "conv2d", "prroi_pool"]
