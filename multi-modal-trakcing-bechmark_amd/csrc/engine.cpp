@@ -81,8 +81,10 @@ struct mmt_engine {
   mmt_config cfg{};
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;       // second half of a split launch
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  static constexpr int kMaxParts = 4;
+  hipStream_t xstream[kMaxParts - 1] = {};   // parts 1.. of a split launch (part 0 runs on `stream`)
+  hipEvent_t fork_ev = nullptr, join_ev[kMaxParts - 1] = {};
+  int nparts = 2;                      // parts of a split launch (MMT_NPARTS, 2..4)
   int overlap_min = 64;                // split launches of >= this many sequences over two streams (0: never)
   std::string err;
   std::map<std::string, std::vector<int64_t>> expected;
@@ -129,7 +131,7 @@ struct mmt_engine {
         *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
   int *gidx0 = nullptr, *gidx1 = nullptr, *slot2pos = nullptr, *gather = nullptr, *removed = nullptr;
-  float* splitk_ws = nullptr;   // [2 stream halves][kSplitKWsElems] fp32 split-K partials (few-tile GEMMs)
+  float* splitk_ws = nullptr;   // [kMaxParts launch parts][kSplitKWsElems] fp32 split-K partials (few-tile GEMMs)
   uint8_t* dbg_patch = nullptr;
   CropParam* params_dev = nullptr;
   SeqState* state_dev = nullptr;      // [max_batch] tracker state per slot (device-resident)
@@ -558,7 +560,7 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->state_dev, (size_t)B * sizeof(SeqState)}, {(void**)&e->out_dev, (size_t)B * sizeof(TrackOut)},
   };
   reqs.push_back({(void**)&e->zero, 256});
-  reqs.push_back({(void**)&e->splitk_ws, (size_t)2 * kSplitKWsElems * 4});
+  reqs.push_back({(void**)&e->splitk_ws, (size_t)mmt_engine::kMaxParts * kSplitKWsElems * 4});
   if (e->split) {
     const std::vector<Req> lo = {
         {(void**)&e->A_rgb_l, (size_t)B * L * C * 2},   {(void**)&e->A_aux_l, (size_t)B * L * C * 2},
@@ -702,13 +704,13 @@ inline T* off(T* p, size_t o) {
   return p ? p + o : nullptr;
 }
 
-void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s) {
+void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int part) {
   const auto& c = e->cfg;
   const int Lz = e->Lz, Lx = e->Lx, L = e->L;
   // per-launch activation views: this launch covers launch-relative sequences [r0, r0 + n)
   // split-K workspace per stream half; parity mode only (in bf16 a different summation order can flip a
   // bf16 rounding and, through CE, a box: that mode keeps batch-size-independent results instead)
-  float* const q_ws = e->split ? e->splitk_ws + (r0 > 0 ? (size_t)kSplitKWsElems : 0) : nullptr;
+  float* const q_ws = e->split ? e->splitk_ws + (size_t)part * kSplitKWsElems : nullptr;
   auto* const q_X = off(e->X, (size_t)r0 * (size_t)L * C);
   auto* const q_X2 = off(e->X2, (size_t)r0 * (size_t)L * C);
   auto* const q_tok_rgb = off(e->tok_rgb, (size_t)r0 * (size_t)L * C);
@@ -1037,16 +1039,20 @@ int stage_frame(mmt_engine* e, int slot, int ring, const uint8_t* frame, int Hh,
 // half's GEMM tails leave idle.  Each half owns disjoint activation rows, results are unchanged.
 void enqueue_split(mmt_engine* e, int b0, int n) {
   if (e->overlap_min <= 0 || n < e->overlap_min || e->probe) {
-    enqueue_forward(e, b0, 0, n, e->stream);
+    enqueue_forward(e, b0, 0, n, e->stream, 0);
     return;
   }
-  const int n1 = n / 2;
+  const int P = std::min(e->nparts, n);
   hipEventRecord(e->fork_ev, e->stream);
-  hipStreamWaitEvent(e->stream2, e->fork_ev, 0);
-  enqueue_forward(e, b0, 0, n1, e->stream);
-  enqueue_forward(e, b0 + n1, n1, n - n1, e->stream2);
-  hipEventRecord(e->join_ev, e->stream2);
-  hipStreamWaitEvent(e->stream, e->join_ev, 0);
+  for (int p = 1; p < P; ++p) hipStreamWaitEvent(e->xstream[p - 1], e->fork_ev, 0);
+  for (int p = 0; p < P; ++p) {
+    const int r0 = n * p / P, r1 = n * (p + 1) / P;
+    enqueue_forward(e, b0 + r0, r0, r1 - r0, p ? e->xstream[p - 1] : e->stream, p);
+  }
+  for (int p = 1; p < P; ++p) {
+    hipEventRecord(e->join_ev[p - 1], e->xstream[p - 1]);
+    hipStreamWaitEvent(e->stream, e->join_ev[p - 1], 0);
+  }
 }
 
 int launch(mmt_engine* e, int b0, int n, const GraphEntry** replayed) {
@@ -1150,18 +1156,21 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   }
   if (hipSetDevice(device) != hipSuccess) return MMT_E_HIP;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
-  if (hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
+  for (auto& xs : e->xstream)
+    if (hipStreamCreateWithFlags(&xs, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
   if (hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
   for (auto& ev : e->copy_ev)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
   if (hipEventCreateWithFlags(&e->frame_ev, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
-  if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->join_ev, hipEventDisableTiming) != hipSuccess)
+  for (auto& je : e->join_ev)
+    if (hipEventCreateWithFlags(&je, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
+  if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess)
     return MMT_E_HIP;
   // f16x3 GEMMs are 3x longer, so halves of 16 sequences still fill the chip and the two streams fill each
   // other's tile-quantisation tails (+8 % at 32 sequences; plain bf16 lost 4 % there)
   if (e->split) e->overlap_min = 32;
   if (const char* ov = std::getenv("MMT_OVERLAP_MIN")) e->overlap_min = std::atoi(ov);
+  if (const char* np = std::getenv("MMT_NPARTS")) e->nparts = std::min(std::max(std::atoi(np), 2), mmt_engine::kMaxParts);
   build_expected(e.get());
   e->frame_dev.assign((size_t)c.max_batch * kRing, nullptr);
   e->frame_cap.assign((size_t)c.max_batch * kRing, 0);
@@ -1197,7 +1206,8 @@ void mmt_destroy(mmt_engine* e) {
   for (auto& t : e->ring)
     if (t.done) hipEventDestroy(t.done);
   if (e->stream) hipStreamDestroy(e->stream);
-  if (e->stream2) hipStreamDestroy(e->stream2);
+  for (auto& xs : e->xstream)
+    if (xs) hipStreamDestroy(xs);
   if (e->cstream) {
     hipStreamSynchronize(e->cstream);
     hipStreamDestroy(e->cstream);
@@ -1206,7 +1216,8 @@ void mmt_destroy(mmt_engine* e) {
     if (ev) hipEventDestroy(ev);
   if (e->frame_ev) hipEventDestroy(e->frame_ev);
   if (e->fork_ev) hipEventDestroy(e->fork_ev);
-  if (e->join_ev) hipEventDestroy(e->join_ev);
+  for (auto& je : e->join_ev)
+    if (je) hipEventDestroy(je);
   delete e;
 }
 

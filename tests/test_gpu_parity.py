@@ -310,3 +310,29 @@ def test_pipelined_frames_equal_blocking(use_graphs):
     for a, b in zip(res["sync"], res["pipe"]):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(res["pipe"][2], res["pipe"][0][-1])
+
+
+@pytest.mark.parametrize("nparts", ["2", "4"])
+def test_split_launch_equals_single(nparts, monkeypatch):
+    """A launch of >= 32 sequences runs as parts on separate HIP streams (engine.cpp enqueue_split, captured
+    into one graph); every sequence's boxes equal that sequence tracked alone (to fp32 rounding: the parts'
+    few-tile GEMMs may split K differently from a one-sequence launch)."""
+    monkeypatch.setenv("MMT_NPARTS", nparts)
+    n = 32
+    cfg = EngineConfig(max_batch=n, use_graphs=True, precision="fp32")
+    sd = synth.make_state_dict(0, **SHAPES["deep_rgbt"])
+    eng = Engine(cfg, sd)
+    seqs = [synth.make_frames(300 + i, 3, 360, 480, 6, box=(120.0 + 9 * i, 100.0 + 3 * i, 40.0, 32.0))
+            for i in range(n)]
+    for i, (fr, gt) in enumerate(seqs):
+        eng.initialize(i, fr[0], list(gt[0]))
+    outs = [eng.track_batch(0, [seqs[i][0][t] for i in range(n)])[0] for t in (1, 2)]
+    eng.close()
+    single = Engine(EngineConfig(max_batch=1, use_graphs=True, precision="fp32"), sd)
+    for i in (0, n // 2 - 1, n // 2, n - 1):
+        fr, gt = seqs[i]
+        single.initialize(0, fr[0], list(gt[0]))
+        for t in (1, 2):
+            box, _ = single.track(0, fr[t])
+            np.testing.assert_allclose(outs[t - 1][i], box, rtol=1e-5, atol=1e-3)
+    single.close()
