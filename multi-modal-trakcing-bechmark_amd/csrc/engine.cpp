@@ -1578,6 +1578,10 @@ int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const fl
   static float* ws = nullptr;
   if (!zero && hipMalloc(&zero, 256) == hipSuccess) hipMemset(zero, 0, 256);
   if (!ws && hipMalloc(&ws, kSplitKWsElems * 4) != hipSuccess) ws = nullptr;
+  if (ws) {   // the split-K tickets at the workspace's end start at zero
+    static bool zeroed = hipMemset(ws, 0, kSplitKWsElems * 4) == hipSuccess;
+    if (!zeroed) return MMT_E_HIP;
+  }
   GemmArgs a{};
   a.g[0] = GemmGroup{(const bf16_t*)A, nullptr, lda, (const bf16_t*)W, nullptr, ldw, bias, Cp, nullptr, ldc, R, ldr};
   a.groups = 1;

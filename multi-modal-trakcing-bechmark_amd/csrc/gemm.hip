@@ -72,6 +72,7 @@ __device__ unsigned long long* g_gemm_stamps = nullptr;
   } while (0)
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
   // raw buffer: stride 0, num_records = bytes (loads past it return 0), gfx9 dword3
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)min(bytes, (int64_t)0x7fffffff),
@@ -198,6 +199,35 @@ struct LdsTile {
     }
   }
 };
+
+// the last slice of a split-K tile sums the ksplit fp32 slabs of the tile in slice order and applies
+// the epilogue (the arithmetic of splitk_reduce_kernel)
+template <int EPI, bool SPLIT, int BM, int BN, int NT>
+__device__ __forceinline__ void sk_combine(const GemmArgs& args, const GemmGroup& g, int m0, int n0) {
+  const int64_t MN = (int64_t)args.M * args.N;
+  const float* base = args.ws + (int64_t)blockIdx.z * args.ksplit * MN;
+  const rsrc_t rs = make_rsrc(base, args.ksplit * MN * 4);
+  constexpr int NCH = BN / 4;
+#pragma unroll
+  for (int k = 0; k < BM * NCH / NT; ++k) {
+    const int idx = threadIdx.x + k * NT;
+    const int r = idx / NCH, c = idx - r * NCH;
+    const int m = m0 + r, n = n0 + c * 4;
+    if (m >= args.M) continue;
+    f32x4 acc;
+    if (args.sk_sc1) {   // every load of a write-through slab is an sc1 load (no acquire was taken)
+      const int o = (m * args.N + n) * 4;
+      acc = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
+      for (int s = 1; s < args.ksplit; ++s)
+        acc += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + (int)(s * MN * 4), 0, 16));
+    } else {
+      const float* p = base + (int64_t)m * args.N + n;
+      acc = *reinterpret_cast<const f32x4*>(p);
+      for (int s = 1; s < args.ksplit; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * MN);
+    }
+    store4<EPI, SPLIT>(g, args, m, n, acc);
+  }
+}
 
 template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int STAGES, int BK = 64>
 __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args) {
@@ -395,7 +425,59 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
         LT::put(lds, wm * T::WM + i * 16 + (lane & 15), col, v);
       }
     __syncthreads();
-    LT::template drain<BM, T::NT>(lds, gp, args, m0, n0, M);
+    if (args.sk_cnt && args.sk_sc1) {   // write-through slab stores straight from the LDS tile
+      const int rows = min(BM, M - m0);
+      const rsrc_t rs = make_rsrc(static_cast<float*>(gp.C) + (int64_t)m0 * args.N, (int64_t)rows * args.N * 4);
+#pragma unroll
+      for (int k = 0; k < BM * LT::NCH / T::NT; ++k) {
+        const int idx = tid + k * T::NT;
+        const int r = idx / LT::NCH, c = idx - r * LT::NCH;
+        if (r >= rows) continue;
+        const u32x4 d = *reinterpret_cast<const u32x4*>(lds + r * BN * 4 + ((c ^ (r & LT::MASK)) << 4));
+        __builtin_amdgcn_raw_buffer_store_b128(d, rs, (r * args.N + n0 + c * 4) * 4, 0, 16);
+      }
+    } else {
+      LT::template drain<BM, T::NT>(lds, gp, args, m0, n0, M);
+    }
+    if (args.sk_cnt) {
+      // in-launch combine (cdna_hip_programming.md, split-K seam): every wave retires its slab stores,
+      // one lane publishes them with an agent-scope release and draws a ticket; the slice that draws
+      // ksplit - 1 resets the ticket, acquires, and reduces the slabs in slice order 0, 1, .. -- the
+      // order and arithmetic of splitk_reduce_kernel, so either path gives the same bits
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        unsigned* cnt = args.sk_cnt + blockIdx.z * ntiles + id;
+        if (!args.sk_sc1) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == (unsigned)(args.ksplit - 1);
+        if (last) {
+          __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!args.sk_sc1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        }
+        flag[0] = last;
+      }
+      __syncthreads();
+      if (flag[0]) {
+        switch (args.sk_epi) {
+          case EPI_BF16: sk_combine<EPI_BF16, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
+          case EPI_GELU_BF16: sk_combine<EPI_GELU_BF16, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
+          case EPI_RESID_F32: sk_combine<EPI_RESID_F32, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
+          case EPI_RELU_BF16: sk_combine<EPI_RELU_BF16, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
+          case EPI_F32: sk_combine<EPI_F32, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
+          case EPI_RELU_F32: sk_combine<EPI_RELU_F32, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
+          case EPI_POS_F32: sk_combine<EPI_POS_F32, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
+          default: break;
+        }
+      }
+    }
   } else if constexpr (LDS_EPI) {
     char* lds = reinterpret_cast<char*>(smem);
 #pragma unroll
@@ -600,7 +682,6 @@ __device__ __forceinline__ void vm_wait_rt(int n) {   // n wave-uniform; scalar 
   }
 }
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int BM, int BN, int WMW, int WNW, int EPI, int NS, int BK>
 __global__ __launch_bounds__(WMW* WNW * 64) void gemm_ring_kernel(const GemmArgs args) {
@@ -1290,8 +1371,19 @@ static void launch_splitk(const GemmArgs& a0, int epi, int ks, hipStream_t s) {
   a.ksplit = ks;
   const int tiles_m = (a.M + BM - 1) / BM;
   a.gm = tiles_m < 8 ? tiles_m : 8;
+  // MMT_SK_INLAUNCH (tuning): the tile's last slice combines in-launch -- 1: write-through slabs, 2: plain
+  // slabs behind agent-scope release / acquire.  Both give the separate reduce's bits and both measured slower
+  // at one sequence (825 -> 749 / 673 frames/s, tests/sk_ab.sh): ~60 reducing workgroups read their slabs
+  // serially at the tail, where the reduce launch spreads the same bytes over every CU
+  static const int inlaunch = getenv("MMT_SK_INLAUNCH") ? atoi(getenv("MMT_SK_INLAUNCH")) : 0;
+  if (inlaunch > 0 && tiles_m * (a.N / BN) * a.groups <= kSkCounters) {
+    a.sk_cnt = reinterpret_cast<unsigned*>(a.ws + a.ws_elems - kSkCounters);
+    a.sk_epi = epi;
+    a.sk_sc1 = inlaunch == 1 ? 1 : 0;
+  }
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI_PARTIAL, AM, SPLIT, ST>), dim3(tiles_m * (a.N / BN), ks, a.groups),
                      dim3(WMW * WNW * 64), 0, s, a);
+  if (a.sk_cnt) return;
   const dim3 rg((unsigned)(((int64_t)a.M * a.N / 4 + 255) / 256), 1, a.groups);
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_BF16, SPLIT>), rg, dim3(256), 0, s, a); break;
@@ -1407,6 +1499,12 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // (not for one sequence's few rows: fc1 at M = 320 keeps 240 64 x 64 workgroups instead of 72)
     if (!old_rule && (a.amode == A_DENSE || !conv_old) && a.N % 128 == 0 && t128n >= t128_min && t128 >= 8) {
       // the head's implicit 3x3 conv (A_CONV3, K = 6912) gathers 64-channel K-tiles
+      static const int n768 = getenv("MMT_SPLIT_N768") ? atoi(getenv("MMT_SPLIT_N768")) : 0;   // tuning
+      if (n768 && a.amode == A_DENSE && a.N % 256 == 0) {
+        if (n768 == 1) return launch_cfg<256, 128, 4, 2, true, 3, 32>(a, epi, s);
+        if (n768 == 2) return launch_cfg<256, 128, 4, 2, true, 2, 32>(a, epi, s);
+        if (n768 == 3) return launch_cfg<128, 256, 2, 4, true, 2, 32>(a, epi, s);
+      }
       if (a.K <= 1024 && a.amode == A_DENSE) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
       return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);
     }
@@ -1422,11 +1520,11 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     static const int sk_target = getenv("MMT_SPLITK_TARGET") ? atoi(getenv("MMT_SPLITK_TARGET")) : 256;
     static const int sk_minkt = getenv("MMT_SPLITK_MINKT") ? atoi(getenv("MMT_SPLITK_MINKT")) : 4;
     static const int sk_max = getenv("MMT_SPLITK_MAX") ? atoi(getenv("MMT_SPLITK_MAX")) : 8;
-    if (a.ws && tiles < sk_tiles && nk >= 2 * sk_minkt) {
+    if (a.ws && a.ws_elems > kSkCounters && tiles < sk_tiles && nk >= 2 * sk_minkt) {
       int ks = (sk_target + tiles - 1) / tiles;
       ks = ks < nk / sk_minkt ? ks : nk / sk_minkt;
       ks = ks < sk_max ? ks : sk_max;
-      while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems) --ks;
+      while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems - kSkCounters) --ks;   // tickets at the end
       if (ks > 1) {
         // f16x3: a 3-deep ring (96 KB of LDS) beat 4-deep at one sequence (tests/sweep_ring_b1.sh)
         constexpr int SKST = SPLIT ? 3 : 4;

@@ -46,7 +46,13 @@ struct GemmArgs {
   float* ws;        // split-K workspace ([groups][ksplit][M][N] fp32) or null: never split
   int64_t ws_elems; // its capacity in floats
   const bf16_t* zero;   // unused by the buffer-load kernels (kept for ABI stability of the struct)
+  // (set by the launcher) in-launch split-K combine: per-tile arrival tickets (the workspace's last
+  // kSkCounters words, zero between launches) and the final epilogue the last arriving slice applies
+  unsigned* sk_cnt;
+  int sk_epi;
+  int sk_sc1;       // 1: the slabs move write-through (sc1 stores and loads), no release / acquire fences
 };
+constexpr int kSkCounters = 1024;
 
 void gemm(const GemmArgs& a, int epi, hipStream_t s);
 void gemm_force_config(int cfg);   // tuning override, -1 = heuristic

@@ -58,6 +58,30 @@ def test_gemm_dense(lib, M, N, K, epi):
         torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-3)
 
 
+def test_splitk_combine_bitwise(tmp_path):
+    """The in-launch split-K combines (the tile's last-arriving slice reduces the slabs, gemm.hip sk_combine;
+    MMT_SK_INLAUNCH=1 write-through, =2 release / acquire) and the default separate reduce launch give the same
+    bits: op-level GEMMs and a parity-mode sequence whose few-tile GEMMs split K (tests/sk_dump.py, one child
+    process each)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = {}
+    for mode, extra in (("separate", {}), ("sc1", {"MMT_SK_INLAUNCH": "1"}), ("fenced", {"MMT_SK_INLAUNCH": "2"})):
+        env = {k: v for k, v in os.environ.items() if k != "MMT_SK_INLAUNCH"}
+        env.update(extra)
+        path = str(tmp_path / f"{mode}.npz")
+        r = subprocess.run([sys.executable, os.path.join(here, "sk_dump.py"), path], env=env, capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        res[mode] = np.load(path)
+    for mode in ("sc1", "fenced"):
+        assert sorted(res[mode].files) == sorted(res["separate"].files)
+        for k in res[mode].files:
+            np.testing.assert_array_equal(res[mode][k], res["separate"][k], err_msg=f"{mode} {k}")
+
+
 @pytest.mark.parametrize("M,N,K", [(4896, 3072, 768), (10240, 2304, 768), (300, 256, 128), (7808, 768, 3072),
                                    (256, 512, 64)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
