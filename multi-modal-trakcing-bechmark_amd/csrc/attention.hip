@@ -36,22 +36,29 @@ constexpr int CE_MAX = 1024;   // max tokens for the exported CE row
 // byte offset of 16-B chunk c of row r in a [64][64] bf16 tile (128-B rows, chunk XOR row)
 __device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 
-template <int WAVES, bool SPLIT, int RB = 1>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVES < 4 ? 1 : (SPLIT ? ATTN_WPE_SPLIT : ATTN_WPE)))) void attn_kernel(const AttnArgs a) {
+// KSPLIT: the WAVES waves of a workgroup share ONE 16-query row block and split its keys (wave w takes key
+// tiles w, w + WAVES, ...; each stages its own tiles), then merge their (max, sum, O) in wave order -- for
+// few (sequence, head) pairs (one sequence: 12), where a lone wave per row block would load every K / V tile
+// by itself
+template <int WAVES, bool SPLIT, int RB = 1, bool KSPLIT = false>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVES < 4 || KSPLIT ? 1 : (SPLIT ? ATTN_WPE_SPLIT : ATTN_WPE)))) void attn_kernel(const AttnArgs a) {
   // SPLIT (fp32-faithful f16x3, common.h): every operand is an (hi, lo) fp16 pair of a range-scaled
   // value and each product is hi*hi + lo*hi + hi*lo; the LDS images of K and V^T hold both halves.
   // RB: 16-query row blocks per wave, multiplied together against each K / V fragment (fragment
   // reads shared, RB independent softmax chains interleaved).
   static_assert(RB == 1 || !SPLIT, "split mode uses one row block per wave");
+  static_assert(RB == 1 || !KSPLIT, "key split: one row block");
   constexpr int NH = SPLIT ? 2 : 1;
   constexpr int QW = 16 * RB;   // queries per wave
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[NH][KB * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[NH][KB * 64];
+  constexpr int QWAVES = KSPLIT ? 1 : WAVES;   // waves with distinct queries
+  constexpr int KW = KSPLIT ? WAVES : 1;       // K / V staging slots
+  __shared__ __attribute__((aligned(16))) bf16_t KsAll[KW][NH][KB * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t VsAll[KW][NH][KB * 64];
   __shared__ float ce_row[CE_MAX];
 
   // XCD-aware order: logical id = (b * heads + h) * nqt + qt; blocks bid, bid + 8, ... (one XCD) take a
   // contiguous logical range, so the query tiles of one (b, h) share an L2
-  const int nqt = (a.N + QW * WAVES - 1) / (QW * WAVES);
+  const int nqt = (a.N + QW * QWAVES - 1) / (QW * QWAVES);
   const int nblk = nqt * a.heads * a.B;
   const int bid = blockIdx.x, xcd = bid & 7, jx = bid >> 3;
   const int q8 = nblk >> 3, r8 = nblk & 7;
@@ -59,9 +66,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
   const int qt = lid % nqt, bh = lid / nqt;
   const int b = bh / a.heads, h = bh - b * a.heads;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  bf16_t(&Ks)[NH][KB * 64] = KsAll[KSPLIT ? wave : 0];
+  bf16_t(&Vs)[NH][KB * 64] = VsAll[KSPLIT ? wave : 0];
   const int N = a.N, Cd = 64 * a.heads, C3 = 3 * Cd;
   const bf16_t* base = a.qkv + (int64_t)b * N * C3;
-  const int q0 = qt * (QW * WAVES) + wave * QW;
+  const int q0 = qt * (QW * QWAVES) + (KSPLIT ? 0 : wave * QW);
   const int g = lane >> 4;
 
   const bf16_t* base_lo = SPLIT ? a.qkv_lo + (int64_t)b * N * C3 : nullptr;
@@ -106,13 +115,20 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
   // K/V staging, software-pipelined: the next tile's 16-B chunks are loaded into registers while the
   // current tile is multiplied, then copied to LDS
   constexpr int NCHUNK = NH * KB * 8;                               // 16-B chunks of K (and of V) per tile
-  constexpr int NCHT = (NCHUNK + WAVES * 64 - 1) / (WAVES * 64);    // per thread
-  constexpr bool CH_EXACT = NCHUNK % (WAVES * 64) == 0;
+  constexpr int LT = KSPLIT ? 64 : WAVES * 64;                      // threads staging one tile
+  constexpr int NCHT = (NCHUNK + LT - 1) / LT;                      // per thread
+  constexpr bool CH_EXACT = NCHUNK % LT == 0;
+  const int ltid = KSPLIT ? lane : tid;
+  // a key-split wave syncs only with itself: its LDS operations complete in order
+  auto tile_sync = [&]() {
+    if constexpr (KSPLIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else __syncthreads();
+  };
   uint4 kreg[NCHT], vreg[NCHT];
   auto fetch = [&](int kb) {
 #pragma unroll
     for (int i = 0; i < NCHT; ++i) {
-      const int q = tid + i * WAVES * 64;
+      const int q = ltid + i * LT;
       if (!CH_EXACT && q >= NCHUNK) break;
       const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
       const int r = qq >> 3, c = qq & 7, key = kb + r;
@@ -125,20 +141,22 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
       }
     }
   };
-  fetch(0);
-  for (int kb = 0; kb < N; kb += KB) {
-    __syncthreads();
+  const int kb0 = KSPLIT ? wave * KB : 0;
+  constexpr int KSTEP = KSPLIT ? WAVES * KB : KB;
+  if (kb0 < N) fetch(kb0);
+  for (int kb = kb0; kb < N; kb += KSTEP) {
+    tile_sync();
 #pragma unroll
     for (int i = 0; i < NCHT; ++i) {
-      const int q = tid + i * WAVES * 64;
+      const int q = ltid + i * LT;
       if (!CH_EXACT && q >= NCHUNK) break;
       const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
       const int r = qq >> 3, c = qq & 7;
       *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Ks[hl]) + tile_off(r, c)) = kreg[i];
       *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Vs[hl]) + tile_off(r, c)) = vreg[i];
     }
-    __syncthreads();
-    if (kb + KB < N) fetch(kb + KB);
+    tile_sync();
+    if (kb + KSTEP < N) fetch(kb + KSTEP);
 
     f32x4 sc[RB][4];
 #pragma unroll
@@ -254,6 +272,47 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
     }
   }
 
+  if constexpr (KSPLIT) {
+    // merge the waves' partial softmax states in wave order: m = max m_w, l = sum l_w e^(m_w - m),
+    // O = sum O_w e^(m_w - m); the K / V slots are free once every wave is past its last tile
+    __syncthreads();
+    float* st = reinterpret_cast<float*>(&KsAll[0][0][0]);   // [WAVES][18][64]
+    if (wave > 0) {
+      float* my = st + wave * 18 * 64 + lane;
+      my[0] = m[0];
+      my[64] = l[0];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) my[(2 + 4 * dt + r) * 64] = o[0][dt][r];
+    }
+    __syncthreads();
+    if (wave > 0) return;
+    float mw[WAVES];
+    mw[0] = m[0];
+    float mm = m[0];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) {
+      mw[w] = st[w * 18 * 64 + lane];
+      mm = fmaxf(mm, mw[w]);
+    }
+    const float f0 = __expf(mw[0] - mm);
+    float ll = l[0] * f0;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[0][dt] *= f0;
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) {
+      const float* ow = st + w * 18 * 64 + lane;
+      const float f = __expf(mw[w] - mm);
+      ll += ow[64] * f;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[0][dt][r] += ow[(2 + 4 * dt + r) * 64] * f;
+    }
+    m[0] = mm;
+    l[0] = ll;
+  }
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int qi = q0 + 16 * rb + (lane & 15);
@@ -278,7 +337,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
       }
     }
   }
-  __syncthreads();
+  if constexpr (!KSPLIT) __syncthreads();   // (key split: every wave's ce_row logits landed before the merge)
   if (ce_wave) {
     const int src = (a.ce_query - q0) & 15;
     float cm = m[0], cl = l[0];
@@ -303,6 +362,7 @@ static void attention_t(const AttnArgs& a, hipStream_t s) {
   // K/V staging shared by 128 queries, half the L2 re-reads of 4 waves (-24 % kernel time, +2.5 %
   // end to end; at the ViPT lengths N <= 320 it measured level in isolation and -0.4 % end to end)
   static const int w8 = getenv("MMT_ATTN_W") ? atoi(getenv("MMT_ATTN_W")) : 0;
+  static const bool ks4 = getenv("MMT_ATTN_NOKS") == nullptr;   // tuning: one wave per row block instead
   if (!SPLIT && bh >= 128 && (w8 == 8 || (w8 == 0 && a.N > 320))) {
     hipLaunchKernelGGL((attn_kernel<8, false>), dim3((a.N + 127) / 128 * bh), dim3(512), 0, s, a);
     return;
@@ -317,6 +377,12 @@ static void attention_t(const AttnArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((attn_kernel<4, SPLIT>), dim3((a.N + 63) / 64 * bh), dim3(256), 0, s, a);
   } else if (per4 * 2 >= 240) {
     hipLaunchKernelGGL((attn_kernel<2, SPLIT>), dim3((a.N + 31) / 32 * bh), dim3(128), 0, s, a);
+  } else if (SPLIT && ks4) {
+    // few (sequence, head) pairs: 4 waves split the keys of each 16-query block (one sequence, N = 320:
+    // 240 workgroups whose K / V tiles load 4 waves at a time instead of one).  f16x3 only: the merge
+    // changes the fp32 rounding with the batch size, which the bf16 mode keeps bit-exact (its kernel
+    // choice does not change a query's arithmetic; test_batch_equals_single)
+    hipLaunchKernelGGL((attn_kernel<4, SPLIT, 1, true>), dim3((a.N + 15) / 16 * bh), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL((attn_kernel<1, SPLIT>), dim3((a.N + 15) / 16 * bh), dim3(64), 0, s, a);
   }

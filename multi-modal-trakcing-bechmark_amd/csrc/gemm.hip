@@ -1520,14 +1520,26 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     static const int sk_target = getenv("MMT_SPLITK_TARGET") ? atoi(getenv("MMT_SPLITK_TARGET")) : 256;
     static const int sk_minkt = getenv("MMT_SPLITK_MINKT") ? atoi(getenv("MMT_SPLITK_MINKT")) : 4;
     static const int sk_max = getenv("MMT_SPLITK_MAX") ? atoi(getenv("MMT_SPLITK_MAX")) : 8;
+    // slices per tile rounded DOWN, so the slices of every tile run in one round of workgroups (fc2 at one
+    // sequence: 60 tiles x 4 = 240 workgroups of 768-deep slices beat 300 of 614 that take two rounds on 44
+    // CUs; 823 -> 906 frames/s, tests/sk_round_ab.sh); MMT_SPLITK_CEIL: round up (tuning)
+    static const bool sk_ceil = getenv("MMT_SPLITK_CEIL") != nullptr;
+    // 64 x 64 few-tile GEMMs with 8 waves (16 x 32 each): twice the waves issuing each K-tile's LDS-DMA
+    // loads -- at one sequence these GEMMs are bound by what a CU can take in (one tile per CU, ~400 KB of
+    // hi + lo operands at ~45 GB/s), 906 -> 929 frames/s (tests/few_w8_ab.sh); MMT_FEW_W4: 4 waves (tuning)
+    static const bool few_w8 = getenv("MMT_FEW_W4") == nullptr;
     if (a.ws && a.ws_elems > kSkCounters && tiles < sk_tiles && nk >= 2 * sk_minkt) {
-      int ks = (sk_target + tiles - 1) / tiles;
+      int ks = sk_ceil ? (sk_target + tiles - 1) / tiles : sk_target / tiles;
       ks = ks < nk / sk_minkt ? ks : nk / sk_minkt;
       ks = ks < sk_max ? ks : sk_max;
       while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems - kSkCounters) --ks;   // tickets at the end
       if (ks > 1) {
         // f16x3: a 3-deep ring (96 KB of LDS) beat 4-deep at one sequence (tests/sweep_ring_b1.sh)
         constexpr int SKST = SPLIT ? 3 : 4;
+        if (few_w8) {
+          if (a.amode == A_CONV3) return launch_splitk<64, 64, 4, 2, A_CONV3, SPLIT, SKST>(a, epi, ks, s);
+          return launch_splitk<64, 64, 4, 2, A_DENSE, SPLIT, SKST>(a, epi, ks, s);
+        }
         if (a.amode == A_CONV3) return launch_splitk<64, 64, 2, 2, A_CONV3, SPLIT, SKST>(a, epi, ks, s);
         return launch_splitk<64, 64, 2, 2, A_DENSE, SPLIT, SKST>(a, epi, ks, s);
       }
@@ -1535,6 +1547,7 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // few tiles (small batches): each workgroup walks the whole K serially, so keep K-tiles in flight
     // (bf16: 4-deep LDS ring, an 8-deep one measured no better at M = 320; f16x3: 3-deep, qkv 17.3 ->
     // 15.4 us and fc1 16.8 -> 16.5 us at one sequence, tests/sweep_ring_b1.sh)
+    if (few_w8 && a.K >= 6 * 64) return launch_cfg<64, 64, 4, 2, SPLIT, SPLIT ? 3 : 4>(a, epi, s);
     if (a.K >= 6 * 64) return launch_cfg<64, 64, 2, 2, SPLIT, SPLIT ? 3 : 4>(a, epi, s);
     return launch_cfg<64, 64, 2, 2, SPLIT>(a, epi, s);
   }
