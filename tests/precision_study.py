@@ -60,43 +60,58 @@ def oracle_pairs(name, n, seed0):
     return sd, cfg, pairs
 
 
-def run_mode(name, sd, cfg, pairs, precision, forced):
-    eng = Engine(EngineConfig(**{**cfg.__dict__, "precision": precision}), sd)
+def run_mode(name, sd, cfg, pairs, precision, forced, batch=1):
+    """batch > 1: the pairs go B at a time through one track_batch launch (the bench path's kernels: 8-wave
+    attention, 256 x 256 / 128 x 128 f16x3 tiles, two-stream halves from 32 sequences)."""
+    eng = Engine(EngineConfig(**{**cfg.__dict__, "precision": precision, "max_batch": max(batch, 1)}), sd)
     rows = []
-    for p in pairs:
-        f0, f1, box = identity_frames(p["zp"], p["xp"], cfg.search_factor)
-        if forced and p["keys"] is not None:
-            eng.force_ce(0, p["keys"])
-        eng.initialize(0, f0, box)
-        eng.track(0, f1)
+    for c0 in range(0, len(pairs), batch):
+        chunk = pairs[c0:c0 + batch]
+        f1s = []
+        for i, p in enumerate(chunk):
+            f0, f1, box = identity_frames(p["zp"], p["xp"], cfg.search_factor)
+            if forced and p["keys"] is not None:
+                eng.force_ce(i, p["keys"])
+            eng.initialize(i, f0, box)
+            f1s.append(f1)
+        if batch == 1:
+            eng.track(0, f1s[0])
+        else:
+            eng.track_batch(0, f1s)
         if forced:
-            eng.force_ce(0, None)
-        res = eng.debug("result")
-        maps = eng.debug("maps")
-        removed = eng.debug("removed")
-        r = {"argmax": int(res[5]) == p["argmax"], "iou": float(iou(to_xywh(res[:4]), to_xywh(p["box"]))),
-             "dscore": float(np.abs(maps[0] - p["score"]).max()), "top2": p["top2"]}
-        ce_ok, off = [], 0
-        Lx = cfg.search_size ** 2 // 256
-        for st, keep in enumerate(p["keep"]):
-            n_rm = (Lx if st == 0 else len(p["keep"][st - 1])) - len(keep)
-            got_rm = set(removed[off:off + n_rm].tolist())
-            prev = set(range(Lx)) if st == 0 else set(p["keep"][st - 1].tolist())
-            ce_ok.append(got_rm == prev - set(keep.tolist()))
-            off += n_rm
-        r["ce_ok"] = all(ce_ok)
-        r["ce_stage_ok"] = ce_ok
-        r["min_margin"] = min(p["margins"]) if p["margins"] else None
-        if p["keys"] is not None and not forced:
-            ek = eng.debug("ce_keys")
-            rel = []
-            for st in range(len(p["keep"])):
-                m = p["keys"][st] > 0
-                rel.append(float(np.max(np.abs(ek[st][m] - p["keys"][st][m]) / p["keys"][st][m])))
-            r["key_rel_err"] = max(rel)
-        rows.append(r)
+            for i in range(len(chunk)):
+                eng.force_ce(i, None)
+        for i, p in enumerate(chunk):
+            rows.append(check_pair(eng, cfg, p, i, forced))
     eng.close()
     return rows
+
+
+def check_pair(eng, cfg, p, bi, forced):
+    res = eng.debug("result", bi)
+    maps = eng.debug("maps", bi)
+    removed = eng.debug("removed", bi)
+    r = {"argmax": int(res[5]) == p["argmax"], "iou": float(iou(to_xywh(res[:4]), to_xywh(p["box"]))),
+         "dscore": float(np.abs(maps[0] - p["score"]).max()), "top2": p["top2"]}
+    ce_ok, off = [], 0
+    Lx = cfg.search_size ** 2 // 256
+    for st, keep in enumerate(p["keep"]):
+        n_rm = (Lx if st == 0 else len(p["keep"][st - 1])) - len(keep)
+        got_rm = set(removed[off:off + n_rm].tolist())
+        prev = set(range(Lx)) if st == 0 else set(p["keep"][st - 1].tolist())
+        ce_ok.append(got_rm == prev - set(keep.tolist()))
+        off += n_rm
+    r["ce_ok"] = all(ce_ok)
+    r["ce_stage_ok"] = ce_ok
+    r["min_margin"] = min(p["margins"]) if p["margins"] else None
+    if p["keys"] is not None and not forced:
+        ek = eng.debug("ce_keys", bi)
+        rel = []
+        for st in range(len(p["keep"])):
+            m = p["keys"][st] > 0
+            rel.append(float(np.max(np.abs(ek[st][m] - p["keys"][st][m]) / p["keys"][st][m])))
+        r["key_rel_err"] = max(rel)
+    return r
 
 
 def summarize(label, rows):
@@ -127,19 +142,20 @@ def main():
     ap.add_argument("--seed0", type=int, default=700)
     ap.add_argument("--modes", default="bf16,fp32")
     ap.add_argument("--forced", default="bf16,fp32", help="modes also run with teacher-forced CE")
+    ap.add_argument("--batch", type=int, default=1, help="pairs per track_batch launch (32: the bench path)")
     args = ap.parse_args()
     torch.set_num_threads(16)
     sd, cfg, pairs = oracle_pairs(args.net, args.n, args.seed0)
-    print(f"# {args.net}: {args.n} pairs; reference CE margins min {min(min(p['margins']) for p in pairs):.2e}, "
+    print(f"# {args.net}: {args.n} pairs, {args.batch} per launch; reference CE margins min {min(min(p['margins']) for p in pairs):.2e}, "
           f"top-2 score gap min {min(p['top2'] for p in pairs):.2e}", flush=True)
     out = []
     for m in args.modes.split(","):
         precision = MODES[m]
-        s = summarize(m, run_mode(args.net, sd, cfg, pairs, precision, False))
+        s = summarize(m, run_mode(args.net, sd, cfg, pairs, precision, False, args.batch))
         print(json.dumps(s), flush=True)
         out.append(s)
         if m in args.forced.split(","):
-            s = summarize(m + "+forcedCE", run_mode(args.net, sd, cfg, pairs, precision, True))
+            s = summarize(m + "+forcedCE", run_mode(args.net, sd, cfg, pairs, precision, True, args.batch))
             print(json.dumps(s), flush=True)
             out.append(s)
     print("SUMMARY " + json.dumps(out))
