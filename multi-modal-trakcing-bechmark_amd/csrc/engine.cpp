@@ -138,6 +138,12 @@ struct mmt_engine {
   TrackOut* out_dev = nullptr;        // [max_batch] per-launch results
   CropParam* params_host = nullptr;   // pinned [kRing][max_batch]
   TrackOut* outs_host = nullptr;      // pinned [kRing][max_batch]
+  // ring hand-off: the geometry kernel reads a launch's frame parameters straight from params_host and
+  // the decode kernel writes its results straight into outs_host (device-visible pinned memory), so a
+  // step carries no copy launches; ring_ctr counts launches on the device (== the host's tickets)
+  bool ring_handoff = true;
+  RingArgs hring{};
+  int64_t launches = 0;
 
   // pipelined frames (mmt_track_batch_submit / _fetch): ticket t uses ring entry t % kRing
   struct Ticket {
@@ -560,6 +566,7 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->state_dev, (size_t)B * sizeof(SeqState)}, {(void**)&e->out_dev, (size_t)B * sizeof(TrackOut)},
   };
   reqs.push_back({(void**)&e->zero, 256});
+  reqs.push_back({(void**)&e->hring.ctr, 256});   // ctr, cur
   reqs.push_back({(void**)&e->splitk_ws, (size_t)mmt_engine::kMaxParts * kSplitKWsElems * 4});
   if (e->split) {
     const std::vector<Req> lo = {
@@ -589,6 +596,12 @@ int alloc_acts(mmt_engine* e) {
   }
   HIPCHECK(e, hipHostMalloc((void**)&e->params_host, (size_t)kRing * B * sizeof(CropParam), hipHostMallocDefault));
   HIPCHECK(e, hipHostMalloc((void**)&e->outs_host, (size_t)kRing * B * sizeof(TrackOut), hipHostMallocDefault));
+  e->hring.cur = e->hring.ctr + 1;
+  e->hring.kring = kRing;
+  e->hring.pitch = B;
+  e->ring_handoff = getenv("MMT_RING_COPY") == nullptr;   // tuning / A-B: copy launches instead
+  HIPCHECK(e, hipHostGetDevicePointer((void**)&e->hring.params, e->params_host, 0));
+  HIPCHECK(e, hipHostGetDevicePointer((void**)&e->hring.outs, e->outs_host, 0));
   for (auto& t : e->ring) HIPCHECK(e, hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
   return MMT_OK;
 }
@@ -753,8 +766,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
   bf16_t* A_rgb_l = off(e->A_rgb_l, (size_t)b0 * L * C);
   bf16_t* A_aux_l = off(e->A_aux_l, (size_t)b0 * L * C);
 
-  // 1. crop geometry from each sequence's device-resident state, then crop + normalise + patchify
-  crop_geometry(e->params_dev + r0, e->state_dev + b0, n, c.search_factor, c.search_size, s);
+  // 1. (crop geometry: enqueue_split, once per launch) crop + normalise + patchify
   CropArgs ca{};
   ca.params = e->params_dev + r0;
   ca.B = n;
@@ -991,6 +1003,12 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
   da.params = e->params_dev + r0;
   da.out = e->out_dev + r0;
   da.search_size = c.search_size;
+  if (e->ring_handoff) {
+    da.ring_outs = e->hring.outs;
+    da.ring_cur = e->hring.cur;
+    da.ring_pitch = e->hring.pitch;
+    da.row0 = r0;
+  }
   decode(da, s);
 }
 
@@ -1038,6 +1056,10 @@ int stage_frame(mmt_engine* e, int slot, int ring, const uint8_t* frame, int Hh,
 // half's latency-bound kernels (LayerNorm, prompt, CE select, head tails) fill the CUs the other
 // half's GEMM tails leave idle.  Each half owns disjoint activation rows, results are unchanged.
 void enqueue_split(mmt_engine* e, int b0, int n) {
+  // crop geometry of all n sequences from their device-resident state (and, ring hand-off, their frame
+  // parameters from the host ring), once per launch before any part starts
+  crop_geometry(e->params_dev, e->state_dev + b0, n, e->cfg.search_factor, e->cfg.search_size,
+                e->ring_handoff ? &e->hring : nullptr, e->stream);
   if (e->overlap_min <= 0 || n < e->overlap_min || e->probe) {
     enqueue_forward(e, b0, 0, n, e->stream, 0);
     return;
@@ -1356,11 +1378,18 @@ int mmt_track_batch_submit(mmt_engine* e, int first_slot, int n, const uint8_t* 
     HIPCHECK(e, hipEventRecord(ce, e->cstream));
     HIPCHECK(e, hipStreamWaitEvent(e->stream, ce, 0));
   }
-  HIPCHECK(e, hipMemcpyAsync(e->params_dev, ph, n * sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
+  if (e->ring_handoff) {   // the device's launch counter picks ring entry next_ticket % kRing
+    if (e->launches != e->next_ticket) return e->fail(MMT_E_STATE, "ring hand-off out of step");
+  } else {
+    HIPCHECK(e, hipMemcpyAsync(e->params_dev, ph, n * sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
+  }
   const GraphEntry* replayed = nullptr;
   TRY(launch(e, first_slot, n, &replayed));
-  TrackOut* oh = e->outs_host + (size_t)(e->next_ticket % kRing) * e->cfg.max_batch;
-  HIPCHECK(e, hipMemcpyAsync(oh, e->out_dev, (size_t)n * sizeof(TrackOut), hipMemcpyDeviceToHost, e->stream));
+  ++e->launches;
+  if (!e->ring_handoff) {
+    TrackOut* oh = e->outs_host + (size_t)(e->next_ticket % kRing) * e->cfg.max_batch;
+    HIPCHECK(e, hipMemcpyAsync(oh, e->out_dev, (size_t)n * sizeof(TrackOut), hipMemcpyDeviceToHost, e->stream));
+  }
   HIPCHECK(e, hipEventRecord(t.done, e->stream));
   t.id = e->next_ticket++;
   t.first = first_slot;

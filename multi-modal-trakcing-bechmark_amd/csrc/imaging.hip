@@ -69,10 +69,8 @@ __device__ __forceinline__ double dmin(double a, double b) { return b < a ? b : 
 
 // processing_utils.py:32-41: crop_sz = ceil(sqrt(w h) factor) ('Too small bounding box.' if < 1),
 // x1 = round(x + w/2 - crop_sz/2) with python's round (half to even)
-__global__ void geometry_kernel(CropParam* params, SeqState* state, int n, double factor, int out_sz) {
+__device__ void geometry_one(CropParam* params, SeqState* state, int i, double factor, int out_sz) {
 #pragma clang fp contract(off)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
   SeqState& st = state[i];
   const double x = st.box[0], y = st.box[1], w = st.box[2], h = st.box[3];
   const double cs = ceil(sqrt(w * h) * factor);
@@ -93,8 +91,36 @@ __global__ void geometry_kernel(CropParam* params, SeqState* state, int n, doubl
   st.err = err;
 }
 
-void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, hipStream_t s) {
-  hipLaunchKernelGGL(geometry_kernel, dim3((n + 63) / 64), dim3(64), 0, s, params, state, n, factor, out_sz);
+// one workgroup: every thread reads the launch counter before thread 0 advances it
+__global__ __launch_bounds__(256) void geometry_kernel(CropParam* params, SeqState* state, int n, double factor,
+                                                       int out_sz, RingArgs ring, int use_ring) {
+  int e = 0;
+  if (use_ring) e = *ring.ctr % ring.kring;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    if (use_ring) {
+      const CropParam h = ring.params[(int64_t)e * ring.pitch + i];
+      CropParam& p = params[i];
+      p.frame = h.frame;
+      p.stride = h.stride;
+      p.H = h.H;
+      p.W = h.W;
+      p.C = h.C;
+    }
+    geometry_one(params, state, i, factor, out_sz);
+  }
+  if (use_ring) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      *ring.cur = e;
+      *ring.ctr = *ring.ctr + 1;
+    }
+  }
+}
+
+void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, const RingArgs* ring,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(geometry_kernel, dim3(1), dim3(256), 0, s, params, state, n, factor, out_sz,
+                     ring ? *ring : RingArgs{}, ring ? 1 : 0);
 }
 
 // vipt.py:84-88 (pred_box * S / resize_factor in float32 tensors, then python floats) + map_box_back
@@ -130,6 +156,10 @@ __device__ void update_state(const DecodeArgs& a, int b, const float* r) {
   st.box[2] = bw;
   st.box[3] = bh;
   for (int k = 0; k < 4; ++k) o.box[k] = st.box[k];
+}
+
+__device__ void ring_out(const DecodeArgs& a, int b) {   // the launch's result row into the host ring entry
+  if (a.ring_outs) a.ring_outs[(int64_t)(*a.ring_cur) * a.ring_pitch + a.row0 + b] = a.out[b];
 }
 
 __global__ __launch_bounds__(256) void decode_kernel(const DecodeArgs a) {
@@ -196,7 +226,10 @@ __global__ __launch_bounds__(256) void decode_kernel(const DecodeArgs a) {
     r[5] = (float)p;
     r[6] = 0.f;
     r[7] = 0.f;
-    if (a.state) update_state(a, b, r);
+    if (a.state) {
+      update_state(a, b, r);
+      ring_out(a, b);
+    }
   }
 }
 

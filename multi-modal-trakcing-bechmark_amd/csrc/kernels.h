@@ -153,6 +153,12 @@ void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, c
                         hipStream_t s);
 
 // ---------------------------------------------------------------- crop + normalise + patchify
+struct TrackOut {                  // one per sequence of a launch (read back by the host)
+  double box[4];                   // 'target_bbox' after this frame (unchanged state on error)
+  float score;                     // 'best_score'
+  int err;                         // 0, or the geometry error of this frame
+  int pad_[2];
+};
 struct CropParam {                 // one per sequence (device memory, rewritten every frame)
   const uint8_t* frame;            // H x W x C uint8, row stride in bytes
   int64_t stride;
@@ -184,15 +190,20 @@ struct SeqState {                  // one per slot
   int err;                         // MMT_E_BOX / MMT_E_ARG of this frame's geometry, else 0
   int pad_;
 };
-struct TrackOut {                  // one per sequence of a launch (read back by the host)
-  double box[4];                   // 'target_bbox' after this frame (unchanged state on error)
-  float score;                     // 'best_score'
-  int err;                         // 0, or the geometry error of this frame
-  int pad_[2];
-};
 // processing_utils.py:32-41 for the search crop of sequences [0, n): params[i] <- x1, y1, crop_sz of
-// state[i].box (factor, out_sz), state[i].rf <- out_sz / crop_sz, state[i].err <- geometry error
-void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, hipStream_t s);
+// state[i].box (factor, out_sz), state[i].rf <- out_sz / crop_sz, state[i].err <- geometry error.
+// Ring hand-off (ring non-null): the frame fields of params[i] are first read from the host's pinned
+// ring entry ring->params[(ctr % kring) * pitch + i] (no copy launch), then *cur <- that entry and
+// ctr advances -- one per launch, in the same order as the host's tickets.
+struct RingArgs {
+  const CropParam* params;   // device-visible pinned [kring][pitch]
+  TrackOut* outs;            // device-visible pinned [kring][pitch] (decode writes the launch's results)
+  int* ctr;                  // launches so far (device)
+  int* cur;                  // ring entry of the launch in flight (device)
+  int kring, pitch;
+};
+void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, const RingArgs* ring,
+                   hipStream_t s);
 
 struct DecodeArgs {
   int B, fs;                       // feature map fs x fs
@@ -207,6 +218,9 @@ struct DecodeArgs {
   const CropParam* params;         // [B] frame H / W of this frame
   TrackOut* out;                   // [B]
   int search_size;
+  TrackOut* ring_outs;             // ring hand-off (or null): out rows also go to ring_outs[*ring_cur * pitch + row0 + b]
+  const int* ring_cur;
+  int ring_pitch, row0;
 };
 void decode(const DecodeArgs& a, hipStream_t s);
 
