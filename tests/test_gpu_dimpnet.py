@@ -29,7 +29,9 @@ def close(got, ref, rel=1e-3):
 @pytest.mark.parametrize("N,C,H,W,Co,k,s,p", [(2, 3, 37, 41, 64, 7, 2, 3), (1, 64, 18, 18, 256, 1, 1, 0),
                                              (3, 128, 19, 17, 128, 3, 1, 1), (2, 128, 36, 36, 128, 3, 2, 1),
                                              (2, 256, 35, 33, 512, 1, 2, 0), (1, 1024, 18, 18, 512, 3, 1, 1),
-                                             (1, 48, 9, 9, 64, 3, 1, 1)])
+                                             (1, 48, 9, 9, 64, 3, 1, 1),
+                                             # wide layers with a ragged M
+                                             (4, 256, 37, 35, 1024, 1, 1, 0), (16, 128, 48, 48, 512, 3, 2, 1)])
 def test_conv2d_vs_torch(N, C, H, W, Co, k, s, p):
     from mmtrack_amd import dimpnet
     g = torch.Generator().manual_seed(N * 100 + C + k)
