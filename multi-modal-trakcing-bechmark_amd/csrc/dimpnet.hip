@@ -45,14 +45,17 @@ struct ConvArgs {
 // ends with 4 consecutive output channels of one pixel: 16-B NHWC stores with bias / residual / ReLU /
 // running-max epilogues.  FAST: a K-tile is BK channels of one tap (float4 loads);
 // otherwise (the 3-channel stem) each k is decoded separately.
-template <bool FAST, int BK>
+// W4 (the 3-channel stem, MMT_CONV_W4): weights padded to 4 channels per tap, a K-tile is 4 taps and a
+// thread loads one tap (3 pixel values + 0, one float4 of weights) -- no per-element index decode
+template <bool FAST, int BK, bool W4 = false>
 __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
+  static_assert(!W4 || (!FAST && BK == 16), "W4: BK 16");
   constexpr int VPT = BK / 4;   // K values per thread per K-tile (A and W each)
   __shared__ float sA[BK][68];
   __shared__ float sB[BK][68];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  const int M = a.N * a.Ho * a.Wo, K = a.kh * a.kw * a.Cin;
+  const int M = a.N * a.Ho * a.Wo, K = a.kh * a.kw * (W4 ? 4 : a.Cin);
   const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
   // this thread's load slot: row (pixel / channel) t >> 2, K offset (t & 3) * VPT
   const int lr = t >> 2, kq = (t & 3) * VPT;
@@ -84,6 +87,15 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
         ra[v] = ok ? *reinterpret_cast<const f32x4v*>(src + 4 * v) : f32x4v{0.f, 0.f, 0.f, 0.f};
         rb[v] = *reinterpret_cast<const f32x4v*>(wrow + kt * BK + kq + 4 * v);
       }
+    } else if constexpr (W4) {
+      const int tap = kt * 4 + (t & 3);
+      const bool tv = tap < a.kh * a.kw;
+      const int ky = tap / a.kw, kx = tap - ky * a.kw;
+      const int iy = iy0 + ky, ix = ix0 + kx;
+      const bool ok = tv && mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const float* src = xb + ((int64_t)iy * a.W + ix) * 3;
+      ra[0] = ok ? f32x4v{src[0], src[1], src[2], 0.f} : f32x4v{0.f, 0.f, 0.f, 0.f};
+      rb[0] = tv ? *reinterpret_cast<const f32x4v*>(wrow + tap * 4) : f32x4v{0.f, 0.f, 0.f, 0.f};
     } else {
 #pragma unroll
       for (int j = 0; j < VPT; ++j) {
@@ -405,7 +417,8 @@ extern "C" {
 int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w, const float* bias, int Cout, int kh,
                    int kw, int stride, int pad, const float* resid, float* y, int flags, void* stream) {
   if (!x || !w || !y || N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || Cout % 64 || kh <= 0 || kw <= 0 ||
-      stride <= 0 || pad < 0 || (flags & ~(MMT_CONV_RELU | MMT_CONV_MAX)))
+      stride <= 0 || pad < 0 || (flags & ~(MMT_CONV_RELU | MMT_CONV_MAX | MMT_CONV_W4)) ||
+      ((flags & MMT_CONV_W4) && Cin != 3))
     return MMT_E_ARG;
   ConvArgs a{x, w, bias, resid, y, N, H, W, Cin, Cout, kh, kw, stride, pad, 0, 0, flags};
   a.Ho = (H + 2 * pad - kh) / stride + 1;
@@ -416,7 +429,9 @@ int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w,
   const dim3 grid(blocks_for(M, 64), Cout / 64);
   // 32-deep K-tiles (half the barriers per MFMA) where a tile stays inside one tap; 16 for Cin = 48 / 16
   static const int bk = getenv("MMT_CONV_BK") ? atoi(getenv("MMT_CONV_BK")) : 32;
-  if (Cin % 32 == 0 && bk == 32)
+  if (flags & MMT_CONV_W4)
+    hipLaunchKernelGGL((conv_f32_kernel<false, 16, true>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  else if (Cin % 32 == 0 && bk == 32)
     hipLaunchKernelGGL((conv_f32_kernel<true, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
   else if (Cin % 16 == 0)
     hipLaunchKernelGGL((conv_f32_kernel<true, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);

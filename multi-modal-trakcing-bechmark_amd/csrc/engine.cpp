@@ -140,7 +140,8 @@ struct mmt_engine {
   TrackOut* outs_host = nullptr;      // pinned [kRing][max_batch]
   // ring hand-off: the geometry kernel reads a launch's frame parameters straight from params_host and
   // the decode kernel writes its results straight into outs_host (device-visible pinned memory), so a
-  // step carries no copy launches; ring_ctr counts launches on the device (== the host's tickets)
+  // step carries no copy launches; the device counts executed launches (hring.ctr) exactly as `launches`
+  // does on the host, and a ticket keeps the ring entry (launches % kRing) its launch used
   bool ring_handoff = true;
   RingArgs hring{};
   int64_t launches = 0;
@@ -152,6 +153,7 @@ struct mmt_engine {
     bool open = false;
     hipEvent_t done = nullptr;
     const GraphEntry* replayed = nullptr;
+    int entry = 0;   // params / results ring entry of its launch
   };
   Ticket ring[kRing];
   int64_t next_ticket = 0;
@@ -1083,6 +1085,7 @@ int launch(mmt_engine* e, int b0, int n, const GraphEntry** replayed) {
   // identical launch sequence eagerly, bracketing the probed kernel class with stream events
   if (!e->cfg.use_graphs || e->probe) {
     enqueue_split(e, b0, n);
+    ++e->launches;
     HIPCHECK(e, hipGetLastError());
     return MMT_OK;
   }
@@ -1098,6 +1101,7 @@ int launch(mmt_engine* e, int b0, int n, const GraphEntry** replayed) {
       p->pending_work.clear();
     }
     enqueue_split(e, b0, n);
+    ++e->launches;
     HIPCHECK(e, hipGetLastError());
     GraphEntry entry;
     if (p) p->capture = &entry;
@@ -1115,6 +1119,7 @@ int launch(mmt_engine* e, int b0, int n, const GraphEntry** replayed) {
     return MMT_OK;
   }
   HIPCHECK(e, hipGraphLaunch(it->second.exec, e->stream));
+  ++e->launches;
   *replayed = &it->second;
   return MMT_OK;
 }
@@ -1356,7 +1361,8 @@ int mmt_track_batch_submit(mmt_engine* e, int first_slot, int n, const uint8_t* 
   auto& t = e->ring[e->next_ticket % kRing];
   if (t.open) return e->fail(MMT_E_STATE, "too many unfetched frames (fetch before submitting more)");
   if (e->probe && e->unfetched > 0) return e->fail(MMT_E_STATE, "the timing probe needs fetch before the next submit");
-  CropParam* ph = e->params_host + (size_t)(e->next_ticket % kRing) * e->cfg.max_batch;
+  const int entry = (int)(e->launches % kRing);   // the ring entry this launch's geometry / decode use
+  CropParam* ph = e->params_host + (size_t)entry * e->cfg.max_batch;
   for (int i = 0; i < n; ++i) {
     const int slot = first_slot + i;
     if (!e->active[slot]) return e->fail(MMT_E_STATE, "track() before initialize() on slot " + std::to_string(slot));
@@ -1378,16 +1384,12 @@ int mmt_track_batch_submit(mmt_engine* e, int first_slot, int n, const uint8_t* 
     HIPCHECK(e, hipEventRecord(ce, e->cstream));
     HIPCHECK(e, hipStreamWaitEvent(e->stream, ce, 0));
   }
-  if (e->ring_handoff) {   // the device's launch counter picks ring entry next_ticket % kRing
-    if (e->launches != e->next_ticket) return e->fail(MMT_E_STATE, "ring hand-off out of step");
-  } else {
+  if (!e->ring_handoff)
     HIPCHECK(e, hipMemcpyAsync(e->params_dev, ph, n * sizeof(CropParam), hipMemcpyHostToDevice, e->stream));
-  }
   const GraphEntry* replayed = nullptr;
   TRY(launch(e, first_slot, n, &replayed));
-  ++e->launches;
   if (!e->ring_handoff) {
-    TrackOut* oh = e->outs_host + (size_t)(e->next_ticket % kRing) * e->cfg.max_batch;
+    TrackOut* oh = e->outs_host + (size_t)entry * e->cfg.max_batch;
     HIPCHECK(e, hipMemcpyAsync(oh, e->out_dev, (size_t)n * sizeof(TrackOut), hipMemcpyDeviceToHost, e->stream));
   }
   HIPCHECK(e, hipEventRecord(t.done, e->stream));
@@ -1396,6 +1398,7 @@ int mmt_track_batch_submit(mmt_engine* e, int first_slot, int n, const uint8_t* 
   t.n = n;
   t.open = true;
   t.replayed = replayed;
+  t.entry = entry;
   ++e->unfetched;
   *ticket = t.id;
   e->last_batch = n;
@@ -1415,7 +1418,7 @@ int mmt_track_batch_fetch(mmt_engine* e, int64_t ticket, double* out_xywh, float
     probe_collect_graph(e, *t.replayed);
   else
     probe_collect(e);
-  const TrackOut* oh = e->outs_host + (size_t)(ticket % kRing) * e->cfg.max_batch;
+  const TrackOut* oh = e->outs_host + (size_t)t.entry * e->cfg.max_batch;
   int rc = MMT_OK;
   for (int i = 0; i < t.n; ++i) {
     const int slot = t.first + i;

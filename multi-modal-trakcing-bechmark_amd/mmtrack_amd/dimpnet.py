@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -44,7 +45,7 @@ def _p(t):
 class _Conv:
     """One conv (+ folded BN): weight [Cout][kh][kw][Cin] and bias [Cout] fp32 on the device."""
 
-    def __init__(self, w, bn=None, bias=None, stride=1, pad=0, dev=None):
+    def __init__(self, w, bn=None, bias=None, stride=1, pad=0, dev=None, w4=True):
         w = w.detach().double()
         co = w.shape[0]
         b = bias.detach().double() if bias is not None else torch.zeros(co, dtype=torch.float64)
@@ -53,7 +54,12 @@ class _Conv:
             s = g / torch.sqrt(var + 1e-5)
             w = w * s.view(-1, 1, 1, 1)
             b = (b - mean) * s + beta
-        self.w = w.permute(0, 2, 3, 1).contiguous().float().to(dev)
+        wk = w.permute(0, 2, 3, 1)
+        # the 3-channel stem: weights padded to 4 channels per tap (MMT_CONV_W4, one float4 per tap)
+        self.w4 = w4 and w.shape[1] == 3 and not os.environ.get("MMT_CONV_NOW4")   # (env: tuning A/B)
+        if self.w4:
+            wk = torch.nn.functional.pad(wk, (0, 1))
+        self.w = wk.contiguous().float().to(dev)
         self.b = b.float().to(dev) if (bn is not None or bias is not None) else None
         self.cout, self.cin, self.kh, self.kw = co, w.shape[1], w.shape[2], w.shape[3]
         self.stride, self.pad = stride, pad
@@ -62,7 +68,7 @@ class _Conv:
         return (H + 2 * self.pad - self.kh) // self.stride + 1, (W + 2 * self.pad - self.kw) // self.stride + 1
 
     def __call__(self, lib, x, N, H, W, out, stream, relu=False, resid=None, merge_max=False):
-        flags = (1 if relu else 0) | (2 if merge_max else 0)
+        flags = (1 if relu else 0) | (2 if merge_max else 0) | (4 if self.w4 else 0)
         _rc(lib.mmt_conv2d_f32(_p(x), N, H, W, self.cin, _p(self.w), _p(self.b), self.cout, self.kh, self.kw,
                                self.stride, self.pad, _p(resid), _p(out), flags, stream), "mmt_conv2d_f32")
         return out
@@ -247,10 +253,10 @@ def patch_transform_device(img, tf, out_hw):
     return out
 
 
-def conv2d(x_nchw, w, bias=None, stride=1, pad=0, resid=None, relu=False):
+def conv2d(x_nchw, w, bias=None, stride=1, pad=0, resid=None, relu=False, w4=True):
     """Test / tool helper: torch NCHW conv through mmt_conv2d_f32 (weights nn.Conv2d layout)."""
     lib = _lib.load()
-    conv = _Conv(w, bias=bias, stride=stride, pad=pad, dev=x_nchw.device)
+    conv = _Conv(w, bias=bias, stride=stride, pad=pad, dev=x_nchw.device, w4=w4)
     N, C, H, W = x_nchw.shape
     Ho, Wo = conv.out_hw(H, W)
     x = x_nchw.permute(0, 2, 3, 1).contiguous()

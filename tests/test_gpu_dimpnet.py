@@ -46,6 +46,22 @@ def test_conv2d_vs_torch(N, C, H, W, Co, k, s, p):
     close(got, F.relu(ref + r), 1e-4)
 
 
+def test_conv2d_stem_w4():
+    """The 3-channel stem through MMT_CONV_W4 (weights padded to 4 channels per tap) and through the generic
+    per-element path agree with torch and each other (summation orders differ: fp32 rounding)."""
+    from mmtrack_amd import dimpnet
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(3, 3, 75, 61, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) / math.sqrt(147)
+    b = torch.randn(64, generator=g) * 0.1
+    ref = F.conv2d(x, w, b, stride=2, padding=3)
+    got4 = dimpnet.conv2d(x.cuda(), w, bias=b, stride=2, pad=3, relu=False, w4=True).cpu()
+    gotg = dimpnet.conv2d(x.cuda(), w, bias=b, stride=2, pad=3, relu=False, w4=False).cpu()
+    close(got4, ref, 1e-5)
+    close(gotg, ref, 1e-5)
+    close(got4, gotg, 1e-5)
+
+
 def test_conv2d_max_merge_and_errors():
     import ctypes
 
