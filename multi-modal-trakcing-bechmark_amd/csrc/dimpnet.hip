@@ -51,8 +51,12 @@ template <bool FAST, int BK, bool W4 = false>
 __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
   static_assert(!W4 || (!FAST && BK == 16), "W4: BK 16");
   constexpr int VPT = BK / 4;   // K values per thread per K-tile (A and W each)
-  __shared__ float sA[BK][68];
-  __shared__ float sB[BK][68];
+  // KV (FAST or W4): the tile is stored row-major with K contiguous and lane group lk of the MFMA owns
+  // K-range [VPT lk, VPT lk + VPT) -- step k4 multiplies k = VPT lk + k4 -- so a lane's fragments come in
+  // 16-B reads and the stash is 16-B writes (k-major tiles took a 4-B LDS op per value): +5 % mfDiMP
+  constexpr bool KV = FAST || W4;
+  __shared__ float sA[KV ? 64 : BK][KV ? BK + 4 : 68];
+  __shared__ float sB[KV ? 64 : BK][KV ? BK + 4 : 68];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int M = a.N * a.Ho * a.Wo, K = a.kh * a.kw * (W4 ? 4 : a.Cin);
@@ -114,10 +118,18 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
     }
   };
   auto stash = [&]() {
+    if constexpr (KV) {
 #pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      sA[kq + j][lr] = ra[j / 4][j % 4];
-      sB[kq + j][lr] = rb[j / 4][j % 4];
+      for (int v = 0; v < VPT / 4; ++v) {
+        *reinterpret_cast<f32x4v*>(&sA[lr][kq + 4 * v]) = ra[v];
+        *reinterpret_cast<f32x4v*>(&sB[lr][kq + 4 * v]) = rb[v];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        sA[kq + j][lr] = ra[j / 4][j % 4];
+        sB[kq + j][lr] = rb[j / 4][j % 4];
+      }
     }
   };
 
@@ -133,6 +145,27 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
   const int li = lane & 15, lk = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + 1 < nk) load(kt + 1);
+    if constexpr (KV) {
+      f32x4v av[2][VPT / 4], bv[2][VPT / 4];
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int h = 0; h < VPT / 4; ++h)
+          av[p][h] = *reinterpret_cast<const f32x4v*>(&sA[wr * 32 + p * 16 + li][lk * VPT + 4 * h]);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int h = 0; h < VPT / 4; ++h)
+          bv[c][h] = *reinterpret_cast<const f32x4v*>(&sB[wc * 32 + c * 16 + li][lk * VPT + 4 * h]);
+#pragma unroll
+      for (int k4 = 0; k4 < VPT; ++k4)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[c][k4 / 4][k4 % 4], av[p][k4 / 4][k4 % 4], acc[p][c], 0,
+                                                             0, 0);
+    } else
 #pragma unroll
     for (int k4 = 0; k4 < BK / 4; ++k4) {
       const int kk = k4 * 4 + lk;
