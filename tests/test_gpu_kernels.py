@@ -62,21 +62,24 @@ def test_splitk_combine_bitwise(tmp_path):
     """The in-launch split-K combines (the tile's last-arriving slice reduces the slabs, gemm.hip sk_combine;
     MMT_SK_INLAUNCH=1 write-through, =2 release / acquire) and the default separate reduce launch give the same
     bits: op-level GEMMs and a parity-mode sequence whose few-tile GEMMs split K (tests/sk_dump.py, one child
-    process each)."""
+    process each).  So does the engine with copy launches for the frame parameters and results
+    (MMT_RING_COPY=1) instead of the ring hand-off."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    for mode, extra in (("separate", {}), ("sc1", {"MMT_SK_INLAUNCH": "1"}), ("fenced", {"MMT_SK_INLAUNCH": "2"})):
-        env = {k: v for k, v in os.environ.items() if k != "MMT_SK_INLAUNCH"}
+    modes = (("separate", {}), ("sc1", {"MMT_SK_INLAUNCH": "1"}), ("fenced", {"MMT_SK_INLAUNCH": "2"}),
+             ("ringcopy", {"MMT_RING_COPY": "1"}))
+    for mode, extra in modes:
+        env = {k: v for k, v in os.environ.items() if k not in ("MMT_SK_INLAUNCH", "MMT_RING_COPY")}
         env.update(extra)
         path = str(tmp_path / f"{mode}.npz")
         r = subprocess.run([sys.executable, os.path.join(here, "sk_dump.py"), path], env=env, capture_output=True,
                            text=True, timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr
         res[mode] = np.load(path)
-    for mode in ("sc1", "fenced"):
+    for mode in ("sc1", "fenced", "ringcopy"):
         assert sorted(res[mode].files) == sorted(res["separate"].files)
         for k in res[mode].files:
             np.testing.assert_array_equal(res[mode][k], res["separate"][k], err_msg=f"{mode} {k}")
