@@ -1182,17 +1182,9 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
     e->keep_at.push_back(Ls);
   }
   if (hipSetDevice(device) != hipSuccess) return MMT_E_HIP;
-  // stream parts at different HIP priorities: the extra parts high, the main stream (part 0, which also
-  // carries the geometry before the fork and the join) normal -- +0.6 % at 32 sequences, one-box A/B
-  // (profiles/r02_ab_part_priority.txt).  MMT_PART_PRIO (tuning): 0 equal, 1 main stream high, 2 (default)
-  static const int part_prio = getenv("MMT_PART_PRIO") ? atoi(getenv("MMT_PART_PRIO")) : 2;
-  int prio_lo = 0, prio_hi = 0;
-  hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, part_prio == 1 ? prio_hi : prio_lo) != hipSuccess)
-    return MMT_E_HIP;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
   for (auto& xs : e->xstream)
-    if (hipStreamCreateWithPriority(&xs, hipStreamNonBlocking, part_prio == 2 ? prio_hi : prio_lo) != hipSuccess)
-      return MMT_E_HIP;
+    if (hipStreamCreateWithFlags(&xs, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
   if (hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
   for (auto& ev : e->copy_ev)
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
