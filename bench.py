@@ -154,7 +154,10 @@ def spawn_ranks(n):
 
 
 def aggregate_throughput(batch, steps, elapsed):
-    """(whole-job frames/s, max-over-ranks elapsed, world): every rank tracked batch x steps frames."""
+    """(whole-job frames/s, max-over-ranks elapsed, world): every rank tracked batch x steps frames.
+
+    `value` is this whole-job rate, as the driver's bench contract defines it (it derives the scaling
+    efficiency from the per-N values itself); the per-GPU rate the metric's name quotes is `per_gpu_fps`."""
     from mmtrack_amd.sharding import max_over_ranks, rank_world
     _, world = rank_world()
     elapsed = max_over_ranks(elapsed)
@@ -205,6 +208,9 @@ def roofline_from(classes, precision, workload, batch):
             "peak_note": ("f16x3 split products (Wh*Ah + Wl*Ah + Wh*Al, fp16 MFMA at the bf16 rate): dense 2500 TF/s / 3; achieved counts "
                           "algorithmic 2MNK flops, the MFMA pipe issues 3x that") if split else "dense bf16",
             "mfma_pipe_frac": round(c["achieved_tflops"] * (3 if split else 1) / PEAK_BF16_TFLOPS, 4),
+            "probe_config": ("eager launches of the timed steps' kernels with the two-stream halves off (HIP cannot "
+                             "time kernels inside a captured graph, and the halves would overlap the classes): "
+                             "each class's own duration, not its share of the overlapped step"),
             "classes": classes}
 
 
@@ -335,6 +341,10 @@ def main():
             "host_frames_fps_rank0": round(host_fps, 2) if host_fps else None,
             "model_tflops": round(value * gf / 1e3, 1),
             "roofline": roof,
+            # the whole timed step (graph replays, halves on) against the same dense peak: algorithmic
+            # FLOPs of every kernel of the step / ms_per_step, per GPU
+            "step_frac_of_peak": round(value / world * gf / 1e3 / (PEAK_BF16_TFLOPS / (3 if args.precision == "fp32"
+                                                                                         else 1)), 4),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -458,6 +468,7 @@ def dry_main(args, rank, world, dist):
         print(json.dumps({"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": w,
                           "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / args.steps * 1e3, 4), "dry": True,
+                          "per_gpu_fps": round(value / w, 2),
                           "config": {"sequences_per_gpu": args.batch, "global_batch": args.batch * w}}), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -258,6 +258,16 @@ int mmt_op_attention(const void* qkv, void* out, int B, int N, int heads, int ce
                      float* ce_prob, void* hip_stream);
 int mmt_op_layernorm(const float* x, const float* w, const float* b, void* out_bf16, float* out_f32, int rows,
                      void* hip_stream);
+/* parity-mode ("f16x3") operators, the kernels the engine launches at precision = 1: every operand v is
+ * carried as the fp16 pair hi = f16(v s), lo = f16(v s - hi) of its power-of-two range scale s
+ * (uint16 storage).  GEMM: acc = sum Wh*Ah + Wl*Ah + Wh*Al, y = acc * inv + bias (inv = 1 / (s_A s_W));
+ * 16-bit epilogues (0, 1, 3) write the pair of y * out_scale to C / C_lo, fp32 ones (2, 4, 5, 6) write y
+ * (+ R).  Attention: qkv halves of qkv * s_qkv -> out halves of O * s_qkv (softmax scale 64^-0.5).      */
+int mmt_op_gemm_f16x3(const void* A_hi, const void* A_lo, int64_t lda, const void* W_hi, const void* W_lo, int64_t ldw,
+                      const float* bias, void* C, void* C_lo, int64_t ldc, const float* R, int64_t ldr, int M, int N, int K,
+                      int epi, float inv, float out_scale, int conv_hw, int conv_cin, void* hip_stream);
+int mmt_op_attention_f16x3(const void* qkv_hi, const void* qkv_lo, void* out_hi, void* out_lo, int B, int N, int heads,
+                           int ce_query, int ce_lens_t, float* ce_prob, float s_qkv, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,8 @@
 The reference's mfDiMP source is an empty submodule (RGBT/models/end2end_rgbt_tracking/); the in-tree
 multi-modal DiMP is DeT's DiMP-50 (two ResNet-50 backbones, 'max' feature merge, DiMP classifier), which
 this build runs as HIP kernels (mmtrack_amd.dimpnet / dimp / dimp_tracker).  This driver tracks seeded
-synthetic RGB-T sequences -- or a LasHeR / RGBT234 / GTOT folder with --seq_home -- one sequence per
+synthetic RGB-T sequences -- or a LasHeR / RGBT234 / GTOT folder with --seq_home and a checkpoint
+(--net_path; --synthetic_weights runs the seeded network there, into a separately named result folder) -- one sequence per
 tracker, several sequences per GPU per launch (dimp_tracker.track_batch), sequences sharded over ranks
 (torchrun: sequence i on rank i % world, no collective), and writes one result file per sequence in the
 RGB-T workspace format (np.savetxt, test_rgbt_mgpus.py:116).
@@ -37,7 +38,15 @@ def main(argv=None):
     ap.add_argument("--dataset_name", default="LasHeR")
     ap.add_argument("--batch", type=int, default=8, help="sequences tracked per launch")
     ap.add_argument("--out_root", default=".")
+    ap.add_argument("--net_path", default="", help="DiMPnet_DeT checkpoint (a state_dict, or pytracking's "
+                    "{'net': state_dict}), loaded with torch.load(weights_only=True)")
+    ap.add_argument("--synthetic_weights", action="store_true",
+                    help="seeded synthetic weights on a --seq_home dataset (results land in mfDiMP_synthetic_weights)")
     args = ap.parse_args(argv)
+    if not args.synthetic and not args.net_path and not args.synthetic_weights:
+        # random weights would produce result files that look like real benchmark outputs
+        raise SystemExit("--seq_home needs real weights (--net_path); pass --synthetic_weights to run the "
+                         "seeded synthetic network on it anyway")
     rank, world = rank_world()
     if torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
@@ -53,8 +62,14 @@ def main(argv=None):
             rgb, aux, gt = gen_config(os.path.join(args.seq_home, name), args.dataset_name)
             seqs.append((name, len(rgb), frame_getter(rgb, aux, 'rgbrgb'), gt))
     mine = [seqs[i] for i in shard_indices(len(seqs), rank, world)]
-    net = DiMPNet(synth.make_dimp_state_dict(0))
-    out_dir = os.path.join(args.out_root, "RGBT_workspace", "results", args.dataset_name, "mfDiMP")
+    if args.net_path:
+        ck = torch.load(args.net_path, map_location="cpu", weights_only=True)
+        net = DiMPNet(ck["net"] if isinstance(ck, dict) and "net" in ck else ck)
+        tag = "mfDiMP"
+    else:
+        net = DiMPNet(synth.make_dimp_state_dict(0))
+        tag = "mfDiMP" if args.synthetic else "mfDiMP_synthetic_weights"
+    out_dir = os.path.join(args.out_root, "RGBT_workspace", "results", args.dataset_name, tag)
     os.makedirs(out_dir, exist_ok=True)
     t0, tracked = time.perf_counter(), 0
     for b0 in range(0, len(mine), args.batch):

@@ -596,8 +596,11 @@ int alloc_acts(mmt_engine* e) {
     *r.p = static_cast<char*>(e->aarena) + off;
     off += (r.bytes + 255) & ~size_t(255);
   }
-  HIPCHECK(e, hipHostMalloc((void**)&e->params_host, (size_t)kRing * B * sizeof(CropParam), hipHostMallocDefault));
-  HIPCHECK(e, hipHostMalloc((void**)&e->outs_host, (size_t)kRing * B * sizeof(TrackOut), hipHostMallocDefault));
+  // the ring is read / written by kernels in place: fine-grained coherent pinned memory, so no GPU cache
+  // holds a stale copy of an entry between the launches that reuse it (frame pointer / size may change)
+  constexpr unsigned kRingFlags = hipHostMallocMapped | hipHostMallocCoherent;
+  HIPCHECK(e, hipHostMalloc((void**)&e->params_host, (size_t)kRing * B * sizeof(CropParam), kRingFlags));
+  HIPCHECK(e, hipHostMalloc((void**)&e->outs_host, (size_t)kRing * B * sizeof(TrackOut), kRingFlags));
   e->hring.cur = e->hring.ctr + 1;
   e->hring.kring = kRing;
   e->hring.pitch = B;
@@ -1628,6 +1631,68 @@ int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const fl
   a.conv_cin = conv_cin;
   a.pos_rows = pos_rows > 0 ? pos_rows : 1;
   gemm(a, epi, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+// the engine's split-K workspace for the operator entry points (tickets at its end start at zero)
+static float* op_workspace() {
+  static float* ws = nullptr;
+  if (!ws && hipMalloc(&ws, kSplitKWsElems * 4) == hipSuccess && hipMemset(ws, 0, kSplitKWsElems * 4) != hipSuccess) {
+    hipFree(ws);
+    ws = nullptr;
+  }
+  return ws;
+}
+
+int mmt_op_gemm_f16x3(const void* A_hi, const void* A_lo, int64_t lda, const void* W_hi, const void* W_lo, int64_t ldw,
+                      const float* bias, void* C, void* C_lo, int64_t ldc, const float* R, int64_t ldr, int M, int N, int K,
+                      int epi, float inv, float out_scale, int conv_hw, int conv_cin, void* stream) {
+  if (!A_hi || !A_lo || !W_hi || !W_lo || !C || M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 32 || epi < 0 || epi > 6)
+    return MMT_E_ARG;
+  const bool out16 = epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RELU_BF16;
+  if (out16 && !C_lo) return MMT_E_ARG;
+  if ((epi == EPI_RESID_F32 || epi == EPI_POS_F32) && !R) return MMT_E_ARG;
+  if (conv_hw > 0 && (conv_cin % 64 || K != 9 * conv_cin || (epi != EPI_RELU_BF16 && epi != EPI_RELU_F32)))
+    return MMT_E_ARG;
+  float* ws = op_workspace();
+  GemmArgs a{};
+  a.g[0] = GemmGroup{(const bf16_t*)A_hi, (const bf16_t*)A_lo, lda, (const bf16_t*)W_hi, (const bf16_t*)W_lo, ldw,
+                     bias, C, out16 ? C_lo : nullptr, ldc, R, ldr, inv, out_scale};
+  a.groups = 1;
+  a.split = 1;
+  a.ws = ws;
+  a.ws_elems = ws ? kSplitKWsElems : 0;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.amode = conv_hw > 0 ? A_CONV3 : A_DENSE;
+  a.conv_hw = conv_hw;
+  a.conv_cin = conv_cin;
+  a.pos_rows = 1;
+  gemm(a, epi, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_op_attention_f16x3(const void* qkv_hi, const void* qkv_lo, void* out_hi, void* out_lo, int B, int N, int heads,
+                           int ce_query, int ce_lens_t, float* ce_prob, float s_qkv, void* stream) {
+  if (!qkv_hi || !qkv_lo || !out_hi || !out_lo || B <= 0 || N <= 0 || N > 1024 || heads <= 0 || !(s_qkv > 0))
+    return MMT_E_ARG;
+  if (ce_query >= 0 && (!ce_prob || ce_lens_t < 0 || ce_lens_t >= N || ce_query >= N)) return MMT_E_ARG;
+  AttnArgs a{};
+  a.qkv = (const bf16_t*)qkv_hi;
+  a.qkv_lo = (const bf16_t*)qkv_lo;
+  a.out = (bf16_t*)out_hi;
+  a.out_lo = (bf16_t*)out_lo;
+  a.B = B;
+  a.N = N;
+  a.heads = heads;
+  a.ce_query = ce_query;
+  a.ce_lens_t = ce_lens_t;
+  a.ce_prob = ce_prob;
+  a.qk_inv = 0.125f / (s_qkv * s_qkv);   // the engine's arguments (enqueue_forward), head dim 64
+  a.pv_inv = 1.0f / (16384.0f * s_qkv);
+  a.out_scale = s_qkv;
+  attention(a, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 

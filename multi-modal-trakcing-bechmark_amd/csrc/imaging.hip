@@ -95,7 +95,7 @@ __device__ void geometry_one(CropParam* params, SeqState* state, int i, double f
 __global__ __launch_bounds__(256) void geometry_kernel(CropParam* params, SeqState* state, int n, double factor,
                                                        int out_sz, RingArgs ring, int use_ring) {
   int e = 0;
-  if (use_ring) e = *ring.ctr % ring.kring;
+  if (use_ring) e = *ring.ctr;   // kept in [0, kring): launches mod kring, as the host's tickets count them
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     if (use_ring) {
       const CropParam h = ring.params[(int64_t)e * ring.pitch + i];
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void geometry_kernel(CropParam* params, SeqSta
     __syncthreads();
     if (threadIdx.x == 0) {
       *ring.cur = e;
-      *ring.ctr = *ring.ctr + 1;
+      *ring.ctr = e + 1 == ring.kring ? 0 : e + 1;   // never overflows however long the engine runs
     }
   }
 }

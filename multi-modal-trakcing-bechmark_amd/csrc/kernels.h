@@ -198,7 +198,7 @@ struct SeqState {                  // one per slot
 struct RingArgs {
   const CropParam* params;   // device-visible pinned [kring][pitch]
   TrackOut* outs;            // device-visible pinned [kring][pitch] (decode writes the launch's results)
-  int* ctr;                  // launches so far (device)
+  int* ctr;                  // launches so far mod kring (device; the ring entry of the next launch)
   int* cur;                  // ring entry of the launch in flight (device)
   int kring, pitch;
 };

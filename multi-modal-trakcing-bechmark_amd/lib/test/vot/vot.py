@@ -45,6 +45,7 @@ class VOT(object):
     """Base class for Python VOT integration (vot.py:22-111)."""
 
     def __init__(self, region_format, channels=None, source=None):
+        self._source = None   # set first: a failed construction must still quit() cleanly from __del__
         if channels not in _CHANNELS:
             raise Exception('Illegal configuration {}.'.format(channels))
         self.channels = _CHANNELS[channels]
@@ -78,7 +79,7 @@ class VOT(object):
         return self._source.frame()
 
     def quit(self):
-        q = getattr(self._source, 'quit', None)
+        q = getattr(getattr(self, '_source', None), 'quit', None)
         if q is not None:
             q()
 

@@ -118,6 +118,9 @@ SIGNATURES = {
     "mmt_gemm_force_config": (_I, [_I]),
     "mmt_op_attention": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "mmt_op_layernorm": (_I, [_P, _P, _P, _P, _P, _I, _P]),
+    "mmt_op_gemm_f16x3": (_I, [_P, _P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _I64, _I, _I, _I, _I, _F, _F, _I, _I,
+                               _P]),
+    "mmt_op_attention_f16x3": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _F, _P]),
 }
 
 _lib = None

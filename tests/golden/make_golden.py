@@ -294,6 +294,54 @@ def tracker_fixture(name, yaml_name, sd, n_frames, seq_seed, H, W, C, init_box):
     print("wrote tracker", name, np.round(np.array(boxes), 1).tolist(), "gt", np.round(gts, 1).tolist())
 
 
+def ostrack_tracker_fixture(sd, n_frames, seq_seed, H, W, init_box):
+    """OSTrack-384 (C4) through the reference ViPTTrack state machine at its search factor 5.0.
+
+    The reference's own OSTrack tracker does not run as shipped (lib/test/tracker/ostrack.py:56, 79 call
+    methods its network does not have), so the reference build_ostrack network
+    (ostrack.py:95-144) is driven by ViPTTrack's initialize / track (vipt.py:41-110) with the RGB
+    Preprocessor (data_utils.py:4-13) and the hann window of the 24 x 24 score map."""
+    import lib.test.tracker.vipt as tv
+    from lib.models.vipt import build_ostrack
+    from lib.test.tracker.basetracker import BaseTracker
+    from lib.test.tracker.data_utils import Preprocessor
+    from lib.test.utils.hann import hann2d
+    from lib.test.utils.params import TrackerParams
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    nn.Module.cuda = lambda self, *a, **k: self
+    cfg = ostrack_cfg()
+    params = TrackerParams()
+    params.cfg = cfg
+    params.template_factor = cfg.TEST.TEMPLATE_FACTOR
+    params.template_size = cfg.TEST.TEMPLATE_SIZE
+    params.search_factor = cfg.TEST.SEARCH_FACTOR
+    params.search_size = cfg.TEST.SEARCH_SIZE
+    params.save_all_boxes = False
+    params.debug = 0
+    tracker = object.__new__(tv.ViPTTrack)
+    BaseTracker.__init__(tracker, params)
+    net = build_ostrack(cfg, training=False)
+    net.load_state_dict(sd, strict=True)
+    tracker.network = net.eval()
+    tracker.cfg = cfg
+    tracker.preprocessor = Preprocessor()
+    tracker.state = None
+    tracker.feat_sz = cfg.TEST.SEARCH_SIZE // cfg.MODEL.BACKBONE.STRIDE
+    tracker.output_window = hann2d(torch.tensor([tracker.feat_sz, tracker.feat_sz]).long(), centered=True)
+    tracker.use_visdom, tracker.debug, tracker.frame_id, tracker.save_all_boxes = False, 0, 0, False
+    frames, gts = synth.make_frames(seq_seed, n_frames, H, W, 3, box=init_box)
+    boxes, scores = [list(init_box)], [1.0]
+    tracker.initialize(frames[0], {"init_bbox": list(init_box)})
+    for t in range(1, n_frames):
+        o = tracker.track(frames[t])
+        boxes.append([float(v) for v in o["target_bbox"]])
+        scores.append(float(o["best_score"]))
+    np.savez_compressed(os.path.join(HERE, "tracker_ostrack384.npz"), boxes=np.array(boxes), scores=np.array(scores),
+                        meta=np.array([seq_seed, n_frames, H, W, 3]), init_box=np.array(init_box, dtype=np.float64),
+                        search_factor=np.array([params.search_factor]))
+    print("wrote tracker ostrack384", np.round(np.array(boxes), 1).tolist(), "gt", np.round(gts, 1).tolist())
+
+
 def crop_fixture():
     """sample_target geometry from the reference (processing_utils.py) on edge boxes."""
     from lib.train.data.processing_utils import sample_target
@@ -344,6 +392,10 @@ def main():
     torch.set_num_threads(8)
     from lib.models.vipt import build_viptrack, build_ostrack
     install_ce_recorder()
+    if "--only-ostrack-tracker" in sys.argv:   # round 3: the C4 tracker sequence alone (the rest is unchanged)
+        ostrack_tracker_fixture(synth.make_state_dict(0, kind="ostrack", search_size=384, template_size=192), 12, 53,
+                                480, 640, (300.0, 220.0, 14.0, 12.0))
+        return
 
     mani = {}
     # --- ViPT deep / shaw, RGB-T and RGB-D yamls (C2, C3): 8 crop pairs each (the first ones are the
@@ -373,6 +425,8 @@ def main():
     tracker_fixture("deep_rgbt", "deep_rgbt", sd, 10, 31, 480, 640, 6, (300.0, 200.0, 40.0, 30.0))
     # a second, longer sequence at DepthTrack's frame shape (C3) with a different target
     tracker_fixture("deep_rgbd", "deep_rgbd", sd, 20, 47, 360, 640, 6, (220.0, 140.0, 52.0, 44.0))
+    ostrack_tracker_fixture(synth.make_state_dict(0, kind="ostrack", search_size=384, template_size=192), 12, 53,
+                            480, 640, (300.0, 220.0, 14.0, 12.0))
     crop_fixture()
     dimp_fixture()
 

@@ -10,4 +10,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -
   python bench.py --steps $STEPS --warmup 0 --no-cpu-baseline --probe none ${ARGS:-} > $OUT/bench.log 2>&1
 STATS=$(find $OUT -name '*kernel_stats.csv' | head -n 1)
 cp $STATS $OUT/kernel_stats.csv
-python tests/prof_summary.py $OUT/kernel_stats.csv $STEPS 30 > $OUT/summary.txt
+python tests/prof_summary.py $OUT/kernel_stats.csv auto 30 > $OUT/summary.txt

@@ -336,3 +336,29 @@ def test_split_launch_equals_single(nparts, monkeypatch):
             box, _ = single.track(0, fr[t])
             np.testing.assert_allclose(outs[t - 1][i], box, rtol=1e-5, atol=1e-3)
     single.close()
+
+
+def test_ostrack384_tracker_sequence_matches_reference():
+    """C4 at its bench search factor 5.0: the reference build_ostrack network driven by the reference ViPTTrack
+    state machine (tracker_ostrack384.npz, make_golden.py ostrack_tracker_fixture; the reference's own OSTrack
+    tracker does not run as shipped) against the engine's OSTrack-384 path, 12 frames of 640 x 480 RGB: boxes
+    IoU >= 0.999 on every frame, best scores within 1e-3."""
+    g = np.load(os.path.join(GOLDEN, "tracker_ostrack384.npz"))
+    seed, n, H, W, C = [int(v) for v in g["meta"]]
+    assert float(g["search_factor"][0]) == 5.0
+    frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
+    cfg = EngineConfig(model="ostrack", prompt_type="none", in_chans=3, template_size=192, search_size=384,
+                       search_factor=5.0)
+    eng = Engine(cfg, synth.make_state_dict(0, **SHAPES["ostrack384"]))
+    try:
+        eng.initialize(0, frames[0], list(g["init_box"]))
+        ious, dsc = [], []
+        for t in range(1, n):
+            box, score = eng.track(0, frames[t])
+            ious.append(iou(box, g["boxes"][t]))
+            dsc.append(abs(score - g["scores"][t]))
+        print("OSTrack-384 per-frame IoU vs reference:", np.round(ious, 5), "max|dscore|", max(dsc))
+        assert min(ious) >= 0.999
+        assert max(dsc) < 1e-3
+    finally:
+        eng.close()

@@ -102,6 +102,9 @@ def test_bench_spawns_ranks_for_gpus_flag():
     line = lines[0]
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 16
     assert line["value"] == pytest.approx(2 * 8 * 20 / (line["ms_per_step"] * 20 / 1e3), rel=1e-3)
+    # value is the whole-job rate (the driver's contract); the metric's per-GPU rate sits beside it
+    assert line["n_gpus"] == 2
+    assert line["per_gpu_fps"] == pytest.approx(line["value"] / 2, rel=1e-3)
     env1 = dict(env, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry"], capture_output=True,
                        text=True, env=env1, timeout=120)

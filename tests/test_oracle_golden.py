@@ -77,6 +77,21 @@ def test_oracle_tracker_matches_reference(name):
     np.testing.assert_allclose(scores, g["scores"], rtol=1e-3, atol=1e-5)
 
 
+def test_oracle_ostrack384_tracker_matches_reference():
+    """C4 at search factor 5.0: the oracle tracker (the ViPTTrack state machine, oracle/tracker.py) with the
+    OSTrack-384 network against the reference build_ostrack network in the reference ViPTTrack
+    (tracker_ostrack384.npz, make_golden.py ostrack_tracker_fixture)."""
+    g = np.load(os.path.join(GOLDEN, "tracker_ostrack384.npz"))
+    seed, n, H, W, C = [int(v) for v in g["meta"]]
+    frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
+    sd = synth.make_state_dict(0, kind="ostrack", search_size=384, template_size=192)
+    cfg = ov.NetCfg(kind="ostrack", search_size=384, template_size=192)
+    tr = otracker.OracleTracker(sd, cfg, search_factor=float(g["search_factor"][0]))
+    boxes, scores = otracker.run_sequence(tr, frames, g["init_box"])
+    np.testing.assert_allclose(boxes, g["boxes"], rtol=1e-4, atol=2e-2)
+    np.testing.assert_allclose(scores, g["scores"], rtol=1e-3, atol=1e-5)
+
+
 def test_cv2_resize_restatement_properties():
     """Unpinned piece: self-consistency of the INTER_LINEAR restatement."""
     rng = np.random.Generator(np.random.PCG64(3))
