@@ -126,7 +126,9 @@ struct mmt_engine {
   // parity diagnostics (debug_outputs): CE keys by slot [B][n_ce][Lx] as computed, and teacher-forced keys
   float *ce_keys = nullptr, *ce_forced = nullptr;
   bool force_ce = false;
-  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr, *s8 = nullptr,
+  // a8 / c8: the prompt blocks' two 8-channel branches, [2][B][L][8] each (layer i writes half i & 1 and the
+  // next layer re-forms the fovea output s8 from the half it did not write)
+  float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr,
         *a8 = nullptr,
         *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
@@ -555,8 +557,8 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->A_rgb, (size_t)B * L * C * 2},      {(void**)&e->A_aux, (size_t)B * L * C * 2},
       {(void**)&e->tok_rgb, (size_t)B * L * C * 4},    {(void**)&e->tok_aux, (size_t)B * L * C * 4},
       {(void**)&e->X, (size_t)B * L * C * 4},          {(void**)&e->X2, (size_t)B * L * C * 4},
-      {(void**)&e->s8, (size_t)B * L * 8 * 4},         {(void**)&e->a8, (size_t)B * L * 8 * 4},
-      {(void**)&e->c8, (size_t)B * L * 8 * 4},         {(void**)&e->Hn, (size_t)B * L * C * 2},
+      {(void**)&e->a8, (size_t)2 * B * L * 8 * 4},
+      {(void**)&e->c8, (size_t)2 * B * L * 8 * 4},         {(void**)&e->Hn, (size_t)B * L * C * 2},
       {(void**)&e->QKV, (size_t)B * L * 3 * C * 2},    {(void**)&e->O, (size_t)B * L * C * 2},
       {(void**)&e->Hm, (size_t)B * L * MLPD * 2},      {(void**)&e->feat, (size_t)B * Lx * C * 2},
       {(void**)&e->h1, (size_t)B * Lx * 3 * hc * 2},   {(void**)&e->h2, (size_t)B * Lx * 3 * (hc / 2) * 2},
@@ -704,7 +706,8 @@ GemmArgs scaled(GemmArgs a, float sa_sw, float out_scale) {
   return a;
 }
 
-void run_gemm(mmt_engine* e, hipStream_t st, const char* cls, const GemmArgs& a, int epi) {
+// returns gemm()'s K splits (> 1 only with a.defer_reduce: the partial slabs are left in a.ws)
+int run_gemm(mmt_engine* e, hipStream_t st, const char* cls, const GemmArgs& a, int epi) {
   const double flops = 2.0 * a.M * a.N * (double)a.K * a.groups;
   // algorithmic HBM bytes: A and W once, C once (bf16 or fp32), R once for the residual epilogues
   const bool out16 = epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RELU_BF16;
@@ -712,8 +715,18 @@ void run_gemm(mmt_engine* e, hipStream_t st, const char* cls, const GemmArgs& a,
   const double rb = (epi == EPI_RESID_F32) ? (double)a.M * a.N * 4.0 : 0.0;
   const double bytes = (((double)a.M * a.K + (double)a.N * a.K) * 2.0 * (a.split ? 2.0 : 1.0) + outb + rb) * a.groups;
   probe_begin(e, st, cls, flops, bytes);
-  gemm(a, epi, st);
+  const int ks = gemm(a, epi, st);
   probe_end(e, st, cls);
+  return ks;
+}
+
+// a residual-stream GEMM (EPI_RESID_F32 into X) whose split-K combine is left to the consuming row kernel
+RowReduce run_resid_gemm(mmt_engine* e, hipStream_t st, const char* cls, GemmArgs a) {
+  a.defer_reduce = a.ws ? 1 : 0;
+  const int ks = run_gemm(e, st, cls, a, EPI_RESID_F32);
+  RowReduce rr{};
+  if (ks > 1) rr = RowReduce{a.ws, ks, (int64_t)a.M * a.N, a.g[0].inv, a.g[0].bias};
+  return rr;
 }
 
 // offset a possibly-null low-half pointer
@@ -733,9 +746,9 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
   auto* const q_X2 = off(e->X2, (size_t)r0 * (size_t)L * C);
   auto* const q_tok_rgb = off(e->tok_rgb, (size_t)r0 * (size_t)L * C);
   auto* const q_tok_aux = off(e->tok_aux, (size_t)r0 * (size_t)L * C);
-  auto* const q_a8 = off(e->a8, (size_t)r0 * (size_t)L * 8);
-  auto* const q_c8 = off(e->c8, (size_t)r0 * (size_t)L * 8);
-  auto* const q_s8 = off(e->s8, (size_t)r0 * (size_t)L * 8);
+  const size_t a8half = (size_t)c.max_batch * L * 8;   // layer i's a8 / c8 live in half i & 1
+  auto q_a8 = [&](int i) { return e->a8 + (size_t)(i & 1) * a8half + (size_t)r0 * L * 8; };
+  auto q_c8 = [&](int i) { return e->c8 + (size_t)(i & 1) * a8half + (size_t)r0 * L * 8; };
   auto* const q_Hn = off(e->Hn, (size_t)r0 * (size_t)L * C);
   auto* const q_Hn_l = off(e->Hn_l, (size_t)r0 * (size_t)L * C);
   auto* const q_QKV = off(e->QKV, (size_t)r0 * (size_t)L * 3 * C);
@@ -808,11 +821,13 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
   pa.B = n;
   pa.Lz = Lz;
   pa.Lx = Lx;
-  pa.a8 = q_a8;
-  pa.c8 = q_c8;
-  pa.s8 = q_s8;
   auto set_prompt = [&](int i, int lnA) {
     pa.layer = i;
+    pa.a8 = q_a8(i);
+    pa.c8 = q_c8(i);
+    pa.a8p = i ? q_a8(i - 1) : nullptr;
+    pa.c8p = i ? q_c8(i - 1) : nullptr;
+    pa.smooth_p = i ? e->pw[i - 1].smooth : 0.f;
     pa.lnA_w = e->pw[lnA].nw;
     pa.lnA_b = e->pw[lnA].nb;
     pa.lnB_w = e->pw[i].nw;
@@ -838,6 +853,9 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
   int removed_off = 0;
   int Ls = Lx;
   int ce_stage = 0;
+  // a split-K update of the residual stream X still in the workspace (proj / fc2 of few-tile launches): the next
+  // row kernel that reads X applies it and writes X back, instead of a reduce launch
+  RowReduce pend{};
   for (int i = 0; i < DEPTH; ++i) {
     const LayerW& w = e->lw[i];
     const int Na = Lz + Ls;
@@ -848,6 +866,8 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
       pa.srcA_rows = Na;
       pa.srcB = nullptr;
       pa.slot2pos = q_slot2pos;
+      pa.rr = pend;   // the previous block's fc2 update of X
+      pend = RowReduce{};
       prompt_reduce(pa, s);
       ln_mode = 2;
     }
@@ -859,7 +879,9 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
       la.Lz = Lz;
       la.Lx = Lx;
       la.X = X;
-      la.s8 = q_s8;
+      la.a8 = q_a8(i);
+      la.c8 = q_c8(i);
+      la.smooth = e->pw[i].smooth;
       la.w1 = e->pw[i].w1;   // conv1x1 of the prompt block that ran for this layer
       la.b1 = e->pw[i].b1;
       la.tok_rgb = q_tok_rgb;
@@ -870,9 +892,10 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
       la.out = q_Hn;
       la.out_lo = q_Hn_l;
       la.out_scale = w.ln1_s;
-      prompt_expand_ln(pa, la, s);
+      prompt_expand_ln(la, s);
     } else {
-      layernorm(X, w.n1w, w.n1b, q_Hn, q_Hn_l, w.ln1_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+      layernorm(X, w.n1w, w.n1b, q_Hn, q_Hn_l, w.ln1_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s, pend);
+      pend = RowReduce{};
     }
     run_gemm(e, s, "qkv",
              scaled(dense(e, q_ws, q_Hn, q_Hn_l, C, w.qkv_w, w.qkv_wl, C, w.qkv_b, q_QKV, q_QKV_l, 3 * C, nullptr, 0,
@@ -897,10 +920,10 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
     probe_begin(e, s, "attn", 4.0 * n * HEADS * (double)Na * Na * 64, (double)n * Na * 4 * C * 2);
     attention(aa, s);
     probe_end(e, s, "attn");
-    run_gemm(e, s, "proj",
-             scaled(dense(e, q_ws, q_O, q_O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
-                    w.qkv_os * w.proj_s, 1.0f),
-             EPI_RESID_F32);
+    pend = run_resid_gemm(
+        e, s, "proj",
+        scaled(dense(e, q_ws, q_O, q_O_l, C, w.proj_w, w.proj_wl, C, w.proj_b, X, nullptr, C, X, C, n * Na, C, C),
+               w.qkv_os * w.proj_s, 1.0f));
     if (ce) {  // attn_blocks.py:99-101
       const int keep = e->keep_at[i];
       CEArgs ce_a{};
@@ -927,25 +950,25 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
       removed_off += Ls - keep;
       std::swap(gin, gout);
       Ls = keep;
-      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * (Lz + Ls), Lz + Ls, q_gather, Na, X2, s);
+      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * (Lz + Ls), Lz + Ls, q_gather, Na, X2, s, pend);
       std::swap(X, X2);
     } else {
-      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s);
+      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s, pend);
     }
+    pend = RowReduce{};
     const int Nm = Lz + Ls;
     run_gemm(e, s, "fc1",
              scaled(dense(e, q_ws, q_Hn, q_Hn_l, C, w.fc1_w, w.fc1_wl, C, w.fc1_b, q_Hm, q_Hm_l, MLPD, nullptr, 0,
                           n * Nm, MLPD, C),
                     w.ln2_s * w.fc1_s, w.fc1_os),
              EPI_GELU_BF16);
-    run_gemm(e, s, "fc2",
-             scaled(dense(e, q_ws, q_Hm, q_Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C, n * Nm, C,
-                          MLPD),
-                    w.fc1_os * w.fc2_s, 1.0f),
-             EPI_RESID_F32);
+    pend = run_resid_gemm(e, s, "fc2",
+                          scaled(dense(e, q_ws, q_Hm, q_Hm_l, MLPD, w.fc2_w, w.fc2_wl, MLPD, w.fc2_b, X, nullptr, C, X, C,
+                                       n * Nm, C, MLPD),
+                                 w.fc1_os * w.fc2_s, 1.0f));
   }
   final_norm_recover(X, Lz + Ls, q_slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, q_feat, q_feat_l, e->feat_s,
-                     q_dbg_feat, s);
+                     q_dbg_feat, s, pend);
 
   // CENTER head: conv1 of the three branches fused (N = 3*hc), then per-branch grouped convs
   const int hc = c.head_channels, fs = e->fs, M = n * Lx;

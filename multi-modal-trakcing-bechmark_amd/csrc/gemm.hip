@@ -1365,12 +1365,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs args)
   store4<EPI, SPLIT>(g, args, m, n, acc);
 }
 
+// K splits of the last gemm() call on this host thread (1: no split); with defer_reduce a split run leaves its
+// slabs for the consumer (RowReduce, kernels.h) and skips the reduce launch
+static thread_local int g_last_ks = 1;
+constexpr int kMaxDeferKs = 8;   // tokens.hip apply_reduce holds at most this many slabs per row
+
 template <int BM, int BN, int WMW, int WNW, int AM, bool SPLIT, int ST>
 static void launch_splitk(const GemmArgs& a0, int epi, int ks, hipStream_t s) {
   GemmArgs a = a0;
   a.ksplit = ks;
   const int tiles_m = (a.M + BM - 1) / BM;
   a.gm = tiles_m < 8 ? tiles_m : 8;
+  if (a.defer_reduce && a.groups == 1 && epi == EPI_RESID_F32 && ks <= kMaxDeferKs) {
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI_PARTIAL, AM, SPLIT, ST>), dim3(tiles_m * (a.N / BN), ks, 1),
+                       dim3(WMW * WNW * 64), 0, s, a);
+    g_last_ks = ks;
+    return;
+  }
   // MMT_SK_INLAUNCH (tuning): the tile's last slice combines in-launch -- 1: write-through slabs, 2: plain
   // slabs behind agent-scope release / acquire.  Both give the separate reduce's bits and both measured slower
   // at one sequence (825 -> 749 / 673 frames/s, tests/sk_ab.sh): ~60 reducing workgroups read their slabs
@@ -1555,11 +1566,13 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
   return launch_cfg<32, 32, 2, 1, SPLIT>(a, epi, s);
 }
 
-void gemm(const GemmArgs& a, int epi, hipStream_t s) {
+int gemm(const GemmArgs& a, int epi, hipStream_t s) {
+  g_last_ks = 1;
   if (a.split)
     gemm_dispatch<true>(a, epi, s);
   else
     gemm_dispatch<false>(a, epi, s);
+  return g_last_ks;
 }
 
 void gemm_force_config(int cfg) { g_force_cfg = cfg; }

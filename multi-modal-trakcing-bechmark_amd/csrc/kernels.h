@@ -51,10 +51,24 @@ struct GemmArgs {
   unsigned* sk_cnt;
   int sk_epi;
   int sk_sc1;       // 1: the slabs move write-through (sc1 stores and loads), no release / acquire fences
+  int defer_reduce; // EPI_RESID_F32, one group: a split-K run leaves its partial slabs for the consumer (gemm())
+};
+
+// A residual-stream update whose split-K partial sums were left in the workspace (gemm() with defer_reduce):
+// the consuming row kernel forms X[row] += sum_s ws[s][row] * inv + bias itself, with the arithmetic of the
+// reduce launch it replaces (slices summed in order, then store4's EPI_RESID_F32), and writes X[row] back.
+struct RowReduce {
+  const float* ws;        // null: nothing pending, X is current
+  int ks;                 // slabs
+  int64_t slab;           // floats per slab (M * 768)
+  float inv;              // f16x3 1 / (s_A s_W) (1 in bf16 mode)
+  const float* bias;      // [768]
 };
 constexpr int kSkCounters = 1024;
 
-void gemm(const GemmArgs& a, int epi, hipStream_t s);
+// returns the K splits it ran: 1, or (a.defer_reduce and few tiles) ks > 1 with the raw fp32 partial slabs left
+// in a.ws ([ks][M][N], one group) for the consumer to combine (RowReduce below) instead of a reduce launch
+int gemm(const GemmArgs& a, int epi, hipStream_t s);
 void gemm_force_config(int cfg);   // tuning override, -1 = heuristic
 int gemm_set_stamps(void* dev_buf);  // tuning: per-block cycle stamps [blocks][4] (null: off)
 
@@ -77,9 +91,11 @@ void attention(const AttnArgs& a, hipStream_t s);
 // ---------------------------------------------------------------- layer norm (row of 768)
 // out_bf16[r] = LN(x[src(r)]), src(r) = gather ? b*in_pitch + gather[b][t] : r ; optional copy of x[src] to xcopy[r]
 // out_lo non-null: out_bf16 / out_lo are the f16x3 halves of LN * out_scale instead (common.h)
+// rr.ws non-null: x[src] first receives its pending split-K update (RowReduce), written to xcopy[r] when given,
+// else back to x[src] (ungathered rows only)
 void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float out_scale,
                float* out_f32, int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy,
-               hipStream_t s);
+               hipStream_t s, const RowReduce& rr = RowReduce{});
 
 // ---------------------------------------------------------------- ViPT prompt blocks
 struct PromptArgs {
@@ -95,10 +111,14 @@ struct PromptArgs {
   const float* w01; const float* b01;       // conv0_1 [8][768] (layer 0 only)
   const float* fold;         // deep layers: LN_B + conv0_1 folded onto the previous s8 (PromptFold)
   float smooth;              // fovea.smooth (device scalar copied to host at load)
-  float* a8;                 // scratch [B][L][8]
-  float* c8;                 // scratch [B][L][8]
-  float* s8;                 // prompt block output before conv1x1 [B][L][8] (the next layer folds
-                             // LN_B + conv0_1 onto it instead of reading P)
+  float* a8;                 // [B][L][8] conv0_0 branch of this layer (written)
+  float* c8;                 // [B][L][8] conv0_1 branch of this layer (written)
+  // deep layers: the previous prompt block's a8 / c8 and fovea smooth; its output s8 = fovea(a8) + c8 (the
+  // prompt before conv1x1, onto which LN_B + conv0_1 fold) is re-formed here from them, per slot, with the
+  // per-(sequence, part) softmax statistics computed in this block (fovea_stats) -- s8 is never stored
+  const float* a8p; const float* c8p;
+  float smooth_p;
+  RowReduce rr;              // deep layers: the previous block's fc2 split-K update of X, applied here
 };
 // PromptFold (float[160]) for deep layer i, from prompt_norms[i] (g, b), conv0_1 of block i (W, w0)
 // and conv1x1 of block i-1 (V [768][8], v0): with V' / v0' the column-centred V / v0,
@@ -113,7 +133,8 @@ struct LnPromptArgs {
   int mode;                  // 1: layer 0 (X = tok_rgb + P + pos), 2: deep layer (X += P[slot])
   int rows, rows_per_seq, Lz, Lx;
   float* X;
-  const float* s8;           // [B][Lz+Lx][8] fovea output of every slot (PromptArgs::s8)
+  const float* a8; const float* c8;   // [B][Lz+Lx][8] this prompt block's branches; s8 = fovea(a8) + c8
+  float smooth;
   const float* w1; const float* b1;         // conv1x1 channel-major [8][768] -> the prompt P = w1^T s8 + b1
   const float* tok_rgb;      // mode 1
   const float* pos;          // mode 1: [Lz+Lx][768]
@@ -122,10 +143,9 @@ struct LnPromptArgs {
   bf16_t* out; bf16_t* out_lo;   // out_lo non-null: f16x3 halves of LN * out_scale
   float out_scale;
 };
-// fovea (s8 for every slot), then the prompt residual (conv1x1 of s8, formed per row from an LDS copy
-// of conv1x1) and LN1
-// for the compact rows
-void prompt_expand_ln(const PromptArgs& pa, const LnPromptArgs& a, hipStream_t s);
+// the fovea statistics of the row's sequence, s8 of its slot, the prompt residual (conv1x1 of s8, formed per
+// row from an LDS copy of conv1x1) and LN1, for the compact rows
+void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- candidate elimination
 struct CEArgs {
@@ -150,7 +170,7 @@ void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s
 // feat_lo non-null: feat / feat_lo are the f16x3 halves of the normed rows * feat_scale
 void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
                         int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float feat_scale, float* feat_f32_dbg,
-                        hipStream_t s);
+                        hipStream_t s, const RowReduce& rr = RowReduce{});
 
 // ---------------------------------------------------------------- crop + normalise + patchify
 struct TrackOut {                  // one per sequence of a launch (read back by the host)

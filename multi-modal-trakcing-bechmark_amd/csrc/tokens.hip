@@ -98,10 +98,76 @@ __device__ __forceinline__ void store_f32(float* p, const Row12& y, int lane) {
   for (int i = 0; i < 3; ++i) q[lane + 64 * i] = y.v[i];
 }
 
+// X row + its pending split-K update (RowReduce): the slabs summed in slice order, then store4's
+// EPI_RESID_F32 arithmetic -- the bits of the splitk_reduce launch this replaces.  All slab loads are issued
+// before the first add.
+constexpr int kMaxDeferSlabs = 8;
+__device__ __forceinline__ Row12 apply_reduce(const Row12& x, const RowReduce& rr, int64_t row, int lane) {
+  f32x4 p[kMaxDeferSlabs][3];
+  const float* base = rr.ws + row * C768;
+#pragma unroll
+  for (int sl = 0; sl < kMaxDeferSlabs; ++sl)
+    if (sl < rr.ks)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) p[sl][i] = reinterpret_cast<const f32x4*>(base + sl * rr.slab)[lane + 64 * i];
+  Row12 o;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    f32x4 acc = p[0][i];
+#pragma unroll
+    for (int sl = 1; sl < kMaxDeferSlabs; ++sl)
+      if (sl < rr.ks) acc += p[sl][i];
+    const float4 bv = reinterpret_cast<const float4*>(rr.bias)[lane + 64 * i];
+    const float sc = rr.inv;
+    const float v[4] = {acc[0] * sc + bv.x, acc[1] * sc + bv.y, acc[2] * sc + bv.z, acc[3] * sc + bv.w};
+    const float4 r = x.v[i];
+    o.v[i] = make_float4(r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]);
+  }
+  return o;
+}
+
+// ------------------------------------------------------------------ fovea statistics (vit_ce_prompt.py:33-47)
+// Per (sequence, part) and channel: the max over the part's slots of a8 * smooth and the sum of
+// exp(a8 * smooth - max), part 0 = template slots [0, Lz), part 1 = search slots [Lz, L).  Run by a whole
+// 512-thread block, 256 threads per part in the thread layout and reduction order of the former standalone
+// fovea kernel (channel = tid & 7, slot stripes of 32), so every block that needs a sequence's statistics
+// forms the same bits.  st[part * 16 + c] = max, st[part * 16 + 8 + c] = sum.
+__device__ __forceinline__ void fovea_stats(const float* a8seq, int Lz, int Lx, float sm, float* red, float* st) {
+  const int tid = threadIdx.x, part = tid >> 8, t = tid & 255;
+  const int lo = part ? Lz : 0, n = part ? Lx : Lz;
+  const int c = t & 7, stripe = t >> 3;
+  float* rp = red + part * 32;
+  float mx = -INFINITY;
+  for (int k = stripe; k < n; k += 32) mx = fmaxf(mx, a8seq[(lo + k) * 8 + c] * sm);
+  mx = fmaxf(mx, dpp<DPP_ROR8>(mx));
+  mx = xmax16(mx);
+  mx = xmax32(mx);
+  if ((t & 63) < 8) rp[(t >> 6) * 8 + c] = mx;
+  __syncthreads();
+  if (t < 8) st[part * 16 + t] = fmaxf(fmaxf(rp[t], rp[8 + t]), fmaxf(rp[16 + t], rp[24 + t]));
+  __syncthreads();
+  const float cm = st[part * 16 + c];
+  float sum = 0.f;
+  for (int k = stripe; k < n; k += 32) sum += __expf(a8seq[(lo + k) * 8 + c] * sm - cm);
+  sum += dpp<DPP_ROR8>(sum);
+  sum = xsum16(sum, sum);
+  sum = xsum32(sum, sum);
+  __syncthreads();
+  if ((t & 63) < 8) rp[(t >> 6) * 8 + c] = sum;
+  __syncthreads();
+  if (t < 8) st[part * 16 + 8 + t] = (rp[t] + rp[8 + t]) + (rp[16 + t] + rp[24 + t]);
+  __syncthreads();
+}
+// s8[c] of one slot (lane c < 8 of the caller): fovea mask * a8 + c8 (the former fovea kernel's expression)
+__device__ __forceinline__ float fovea_s8(float a, float cc, const float* st, int part, int c, float sm) {
+  return (__expf(a * sm - st[part * 16 + c]) / st[part * 16 + 8 + c]) * a + cc;
+}
+
 // ------------------------------------------------------------------ LayerNorm (optionally fused CE gather)
 __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w, const float* b, bf16_t* ob,
                                                  bf16_t* olo, float oscale, float* of, int rows, int rows_per_seq,
-                                                 const int* gather, int in_rows_per_seq, float* xcopy) {
+                                                 const int* gather, int in_rows_per_seq, float* xcopy,
+                                                 const RowReduce rr) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
   int64_t src = r;
@@ -109,7 +175,11 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
     const int bs = r / rows_per_seq;
     src = (int64_t)bs * in_rows_per_seq + gather[r];
   }
-  const Row12 xv = load_row(x + src * C768, lane);
+  Row12 xv = load_row(x + src * C768, lane);
+  if (rr.ws) {   // the pending split-K update of the residual stream (proj / fc2), then X is current again
+    xv = apply_reduce(xv, rr, src, lane);
+    if (!xcopy) store_f32(const_cast<float*>(x) + src * C768, xv, lane);
+  }
   if (xcopy) store_f32(xcopy + (int64_t)r * C768, xv, lane);
   const Row12 y = ln_row(xv, w, b, lane);
   if (olo) store_split(ob + (int64_t)r * C768, olo + (int64_t)r * C768, y, oscale, lane);
@@ -119,9 +189,9 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
 
 void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float out_scale,
                float* out_f32, int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy,
-               hipStream_t s) {
+               hipStream_t s, const RowReduce& rr) {
   hipLaunchKernelGGL(ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_scale, out_f32,
-                     rows, rows_per_seq, gather, in_rows_per_seq, xcopy);
+                     rows, rows_per_seq, gather, in_rows_per_seq, xcopy, rr);
 }
 
 // ------------------------------------------------------------------ prompt block, part 1
@@ -204,244 +274,121 @@ __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) 
   }
 }
 
-// Deep layers: conv0_0(LN_A(recovered X)) with conv0_0 (LN_A's affine folded in) in LDS;
-// conv0_1(LN_B(P_prev)) from the previous s8 and the folded constants (PromptFold) -- 8 floats per
-// token instead of a 768-float prompt row.
-// Each wave owns R rows (r0, r0 + nw, ...).  Every load the wave needs -- the rows' compact
-// positions, then the R rows -- is issued before the block's weight fill and barrier, so a wave
-// has all of its bytes in flight at once and the kernel runs at HBM rate even though each wave only
-// sees a few rows.
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && atoi(v) > 0 ? atoi(v) : dflt;
-}
-
+// Deep layers: conv0_0(LN_A(recovered X)) with conv0_0 (LN_A's affine folded in) in LDS; conv0_1(LN_B(P_prev))
+// from the previous prompt's s8 and the folded constants (PromptFold) -- 8 floats per token instead of a
+// 768-float prompt row.  s8_prev = fovea(a8_prev) + c8_prev is re-formed per slot from the previous block's
+// a8 / c8 and the fovea statistics of the slot's sequence, which this block computes (fovea_stats).
+// One block = 8 slots of one sequence (grid: slot blocks x sequences), one slot per wave; every global load
+// the wave needs -- the slot's compact position, its X row (and pending fc2 split-K slabs), the previous
+// a8 / c8 -- is issued before the block's weight fill, statistics and barriers.
 constexpr int TOK_THREADS = 512;   // 8 waves per block share one LDS copy of the weights
+constexpr int TOK_ROWS = TOK_THREADS / 64;
 
-struct DeepIn {
-  Row12 x;
-  float sp, sq;   // s8[lane & 7], s8[lane >> 3] of the row: the lane's term of the LN_B variance form
-};
-
-// compact position of slot row `row` (-1: pruned search slot)
-__device__ __forceinline__ int deep_pos(const PromptArgs& a, int row, int L) {
-  const int b = row / L, s = row - b * L;
-  return s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];
-}
-
-__device__ __forceinline__ DeepIn deep_fetch(const PromptArgs& a, int row, int pos, int L, int lane) {
-  const int b = row / L;
-  DeepIn d;
-  // unconditional load (a pruned slot reads compact row 0 and discards it): branch-free, so the
-  // in-order vmcnt waits count exactly the loads issued
-  d.x = load_row(a.srcA + ((int64_t)b * a.srcA_rows + max(pos, 0)) * C768, lane);
-  if (pos < 0) d.x = zero_row();
-  const float* sp = a.s8 + (int64_t)row * 8;
-  d.sp = sp[lane & 7];
-  d.sq = sp[lane >> 3];
-  return d;
-}
-
-template <int R>
 __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const PromptArgs a) {
   __shared__ float fold[FOLD_N];
   __shared__ __attribute__((aligned(16))) float W0[8 * C768];   // conv0_0 (LN_A affine folded in)
-  const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, rows = a.B * L;
-  const int nw = gridDim.x * (TOK_THREADS / 64);
-  const int r0 = blockIdx.x * (TOK_THREADS / 64) + (threadIdx.x >> 6);
-  // 1. positions of the wave's rows (lane j: row r0 + j * nw), 2. the weights, 3. the rows
-  const int pr = r0 + lane * nw;
-  const int posv = (lane < R && pr < rows) ? deep_pos(a, pr, L) : -1;
+  __shared__ float red[64], st[32];
+  const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, b = blockIdx.y;
+  const int s = blockIdx.x * TOK_ROWS + (threadIdx.x >> 6);   // slot of this wave
+  const bool valid = s < L;
+  const int pos = !valid ? -1 : s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];   // wave-uniform
+  const int64_t xrow = (int64_t)b * a.srcA_rows + max(pos, 0);
+  Row12 x = load_row(a.srcA + xrow * C768, lane);
+  const int64_t srow = ((int64_t)b * L + min(s, L - 1)) * 8;
+  const float ap = lane < 8 ? a.a8p[srow + lane] : 0.f, cp = lane < 8 ? a.c8p[srow + lane] : 0.f;
   constexpr int WV = 8 * C768 / 4 / TOK_THREADS;
   float4 wst[WV];
 #pragma unroll
   for (int k = 0; k < WV; ++k) wst[k] = reinterpret_cast<const float4*>(a.w00)[threadIdx.x + TOK_THREADS * k];
   const float fo = threadIdx.x < FOLD_N ? a.fold[threadIdx.x] : 0.f;
   const float ba = lane < 8 ? a.b00[lane] : 0.f;
-  DeepIn in[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int rj = min(r0 + j * nw, rows - 1);
-    in[j] = deep_fetch(a, rj, __builtin_amdgcn_readlane(posv, j), L, lane);
-  }
 #pragma unroll
   for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[threadIdx.x + TOK_THREADS * k] = wst[k];
   if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
-  __syncthreads();
+  fovea_stats(a.a8p + (int64_t)b * L * 8, a.Lz, a.Lx, a.smooth_p, red, st);   // ends with a barrier
+  if (!valid) return;
+  if (pos >= 0 && a.rr.ws) {   // the previous block's fc2 update of this slot's residual row, written back
+    x = apply_reduce(x, a.rr, xrow, lane);
+    store_f32(const_cast<float*>(a.srcA) + xrow * C768, x, lane);
+  }
   const int kk = lane & 7;
+  // s8_prev of the slot in lanes 0-7, then the lane's pair of it for the LN_B variance form
+  const float s8v = lane < 8 ? fovea_s8(ap, cp, st, s < a.Lz ? 0 : 1, lane, a.smooth_p) : 0.f;
+  const float sp = __shfl(s8v, kk, 64), sq = __shfl(s8v, lane >> 3, 64);
   // the lane's coefficients of the LN_B variance form: G[q][p] s_p s_q (+ 2 g_q s_q for p = 0, + gb in lane 0)
   const float vG = fold[FOLD_G + lane], vg = kk == 0 ? 2.f * fold[FOLD_g + (lane >> 3)] : 0.f;
   const float vb = lane == 0 ? fold[FOLD_gb] : 0.f;
+  float ra = 0.f;   // a pruned slot is a zero row: its LN is 0 and a8 = b00 exactly
+  if (pos >= 0) {   // wave-uniform
+    const Row12 y = ln_hat(x);   // LN_A's affine is folded into w00 / b00 (engine pack_weights)
+    float part[8];
 #pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int row = r0 + j * nw;
-    if (row >= rows) break;
-    float ra = 0.f;   // a pruned slot is a zero row: its LN is 0 and a8 = b00 exactly
-    if (__builtin_amdgcn_readlane(posv, j) >= 0) {   // wave-uniform
-      const Row12 y = ln_hat(in[j].x);   // LN_A's affine is folded into w00 / b00 (engine pack_weights)
-      float part[8];
+    for (int k = 0; k < 8; ++k) {
+      float t = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const float4 w = reinterpret_cast<const float4*>(W0 + k * C768)[lane + 64 * i];
-          t += y.v[i].x * w.x + y.v[i].y * w.y + y.v[i].z * w.z + y.v[i].w * w.w;
-        }
-        part[k] = t;
+      for (int i = 0; i < 3; ++i) {
+        const float4 w = reinterpret_cast<const float4*>(W0 + k * C768)[lane + 64 * i];
+        t += y.v[i].x * w.x + y.v[i].y * w.y + y.v[i].z * w.z + y.v[i].w * w.w;
       }
-      ra = reduce8(part, lane);
+      part[k] = t;
     }
-    // c8 from the previous prompt's s8: var = s^T G s + 2 g.s + gb, one (q, p) term per lane
-    const float var = wave_sum(fmaf(fmaf(vG, in[j].sp, vg), in[j].sq, vb));
-    const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + LN_EPS);
-    // lane kk < 8: mk = mc[kk] + MC[kk][:] . s   (s[q] is lane 8q's sq)
-    float mk = fold[FOLD_mc + kk];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) mk += fold[FOLD_MC + kk * 8 + q] * u2f(__builtin_amdgcn_readlane(f2u(in[j].sq), 8 * q));
-    const float rb = rstd * mk + fold[FOLD_cb + kk];
-    if (lane < 8) {
-      a.a8[(int64_t)row * 8 + lane] = ra + ba;
-      a.c8[(int64_t)row * 8 + lane] = rb;
-    }
+    ra = reduce8(part, lane);
   }
-}
-
-// rows per wave (tuning knob MMT_TOK_WAVES = the wave count to aim for; R = 1 measured fastest at
-// B = 32 on MI355X, the weights' LDS fill is amortised over the block's 8 waves)
-static int rows_per_wave(int rows) {
-  static const int target = env_int("MMT_TOK_WAVES", 1 << 24);   // default: one row per wave (measured best)
-  return rows >= 3 * target ? 4 : rows >= 2 * target ? 3 : rows >= target ? 2 : 1;
-}
-
-template <typename Args, typename K1, typename K2, typename K3, typename K4>
-static void launch_rows(int rows, K1 k1, K2 k2, K3 k3, K4 k4, const Args& a, hipStream_t s) {
-  const int R = rows_per_wave(rows);
-  const int waves = (rows + R - 1) / R;
-  const dim3 grid((waves + TOK_THREADS / 64 - 1) / (TOK_THREADS / 64));
-  auto k = R == 1 ? k1 : R == 2 ? k2 : R == 3 ? k3 : k4;
-  hipLaunchKernelGGL(k, grid, dim3(TOK_THREADS), 0, s, a);
+  // c8 from the previous prompt's s8: var = s^T G s + 2 g.s + gb, one (q, p) term per lane
+  const float var = wave_sum(fmaf(fmaf(vG, sp, vg), sq, vb));
+  const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + LN_EPS);
+  // lane kk < 8: mk = mc[kk] + MC[kk][:] . s   (s[q] is lane 8q's sq)
+  float mk = fold[FOLD_mc + kk];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) mk += fold[FOLD_MC + kk * 8 + q] * u2f(__builtin_amdgcn_readlane(f2u(sq), 8 * q));
+  const float rb = rstd * mk + fold[FOLD_cb + kk];
+  if (lane < 8) {
+    const int64_t row = (int64_t)b * L + s;
+    a.a8[row * 8 + lane] = ra + ba;
+    a.c8[row * 8 + lane] = rb;
+  }
 }
 
 void prompt_reduce(const PromptArgs& a, hipStream_t s) {
-  const int rows = a.B * (a.Lz + a.Lx);
+  const int L = a.Lz + a.Lx;
   if (a.layer == 0) {
-    const int waves = (rows + PR_ROWS - 1) / PR_ROWS;
+    const int waves = (a.B * L + PR_ROWS - 1) / PR_ROWS;
     hipLaunchKernelGGL(prompt_reduce_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, a);
   } else {
-    launch_rows(rows, prompt_reduce_deep_kernel<1>, prompt_reduce_deep_kernel<2>, prompt_reduce_deep_kernel<3>,
-                prompt_reduce_deep_kernel<4>, a, s);
-  }
-}
-
-// ------------------------------------------------------------------ prompt block, part 2
-// Fovea (vit_ce_prompt.py:33-47): per channel, softmax over the part's h*w positions of x*smooth,
-// times x; + the conv0_1 branch -> s8 [B][L][8].  One block per (part, sequence) computes the
-// part's per-channel max / sum once and writes s8 for every slot of the part.  The conv1x1
-// 8 -> 768 that turns s8 into the prompt P is fused into the consumer (ln_prompt below), and the
-// next layer folds LN_B + conv0_1 onto s8 (PromptFold), so P is never materialized.
-constexpr int FOVEA_MAX_TOKENS = 1024;
-
-__global__ __launch_bounds__(256) void fovea_kernel(const PromptArgs a) {
-  __shared__ __attribute__((aligned(16))) float va[FOVEA_MAX_TOKENS * 8];
-  __shared__ __attribute__((aligned(16))) float vc[FOVEA_MAX_TOKENS * 8];
-  __shared__ float red[256];
-  __shared__ float smax[8], ssum[8];
-  const int L = a.Lz + a.Lx, b = blockIdx.y, tid = threadIdx.x;
-  const int lo = blockIdx.x == 0 ? 0 : a.Lz, n = blockIdx.x == 0 ? a.Lz : a.Lx;
-  const float* a8 = a.a8 + ((int64_t)b * L + lo) * 8;
-  const float* c8 = a.c8 + ((int64_t)b * L + lo) * 8;
-  float* s8 = a.s8 + ((int64_t)b * L + lo) * 8;
-  // the part's a8 and c8 into LDS with coalesced 16-byte loads (all issued before the first use)
-  for (int e = tid; e < n * 2; e += 256) {
-    reinterpret_cast<float4*>(va)[e] = reinterpret_cast<const float4*>(a8)[e];
-    reinterpret_cast<float4*>(vc)[e] = reinterpret_cast<const float4*>(c8)[e];
-  }
-  __syncthreads();
-  const float sm = a.smooth;
-  const int c = tid & 7, stripe = tid >> 3;
-  float mx = -INFINITY;
-  for (int t = stripe; t < n; t += 32) mx = fmaxf(mx, va[t * 8 + c] * sm);
-  mx = fmaxf(mx, dpp<DPP_ROR8>(mx));
-  mx = xmax16(mx);
-  mx = xmax32(mx);
-  if ((tid & 63) < 8) red[(tid >> 6) * 8 + c] = mx;
-  __syncthreads();
-  if (tid < 8) smax[tid] = fmaxf(fmaxf(red[tid], red[8 + tid]), fmaxf(red[16 + tid], red[24 + tid]));
-  __syncthreads();
-  const float cm = smax[c];
-  float sum = 0.f;
-  for (int t = stripe; t < n; t += 32) sum += __expf(va[t * 8 + c] * sm - cm);
-  sum += dpp<DPP_ROR8>(sum);
-  sum = xsum16(sum, sum);
-  sum = xsum32(sum, sum);
-  __syncthreads();
-  if ((tid & 63) < 8) red[(tid >> 6) * 8 + c] = sum;
-  __syncthreads();
-  if (tid < 8) ssum[tid] = (red[tid] + red[8 + tid]) + (red[16 + tid] + red[24 + tid]);
-  __syncthreads();
-  // s8 = softmax mask * a8 + c8, four channels per thread, 16-byte loads / stores
-  for (int e = tid; e < n * 2; e += 256) {
-    const int c0 = (e & 1) * 4;
-    const float4 v = reinterpret_cast<const float4*>(va)[e];
-    const float4 cc = reinterpret_cast<const float4*>(vc)[e];
-    float4 o;
-    o.x = (__expf(v.x * sm - smax[c0]) / ssum[c0]) * v.x + cc.x;
-    o.y = (__expf(v.y * sm - smax[c0 + 1]) / ssum[c0 + 1]) * v.y + cc.y;
-    o.z = (__expf(v.z * sm - smax[c0 + 2]) / ssum[c0 + 2]) * v.z + cc.z;
-    o.w = (__expf(v.w * sm - smax[c0 + 3]) / ssum[c0 + 3]) * v.w + cc.w;
-    reinterpret_cast<float4*>(s8)[e] = o;
+    hipLaunchKernelGGL(prompt_reduce_deep_kernel, dim3((L + TOK_ROWS - 1) / TOK_ROWS, a.B), dim3(TOK_THREADS), 0, s, a);
   }
 }
 
 // ------------------------------------------------------------------ LN1 with the prompt residual fused
-// P[slot] = conv1x1(s8[slot]) + b1 (vit_ce_prompt.py:69-71), formed on the fly from the 32 bytes of s8
-// per token and the block's LDS copy of conv1x1 (P is never written to HBM).
+// The prompt block's output s8[slot] = fovea(a8)[slot] + c8[slot] (Fovea, vit_ce_prompt.py:33-47: per channel a
+// softmax over the part's h*w positions of a8 * smooth, times a8), formed per row from the block's fovea
+// statistics of the sequence; P[slot] = conv1x1(s8[slot]) + b1 (vit_ce_prompt.py:69-71) from the 32 bytes of
+// s8 and the block's LDS copy of conv1x1 (neither s8 nor P is ever written to HBM).
 // mode 1 (layer 0):  X[r] = (tok_rgb[r] + P[r]) + pos[t]          (vit_ce_prompt.py:218, 240-241)
 // mode 2 (layer i):  X[r] = X[r] + P[b][slot(t)], slot(t) = t < Lz ? t : gidx[b][t-Lz]
 //                    (candidate_elimination_prompt + x_ori add, attn_blocks.py:9-18, vit_ce_prompt.py:310)
-// then out = LN(X[r]) (norm1 of the block).
-struct LnpIn {
-  Row12 x, q;      // mode 2: x = X row; mode 1: x = tok_rgb row, q = pos row
-  float4 s0, s1;   // s8 of the row's slot
-};
-
+// then out = LN(X[r]) (norm1 of the block).  One block = 8 compact rows of one sequence, one per wave; the
+// slot, rows and weights are all requested before the statistics and barriers.
 template <int MODE>
-__device__ __forceinline__ int lnp_slot(const LnPromptArgs& a, int r) {
-  const int b = r / a.rows_per_seq, t = r - b * a.rows_per_seq;
-  if (MODE == 1 || t < a.Lz) return t;
-  return a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (t - a.Lz)];
-}
-
-template <int MODE>
-__device__ __forceinline__ LnpIn lnp_fetch(const LnPromptArgs& a, int r, int slot, int lane) {
-  const int b = r / a.rows_per_seq, t = r - b * a.rows_per_seq;
-  const int L = a.Lz + a.Lx;
-  LnpIn d;
-  if (MODE == 1) {
-    d.x = load_row(a.tok_rgb + (int64_t)r * C768, lane);
-    d.q = load_row(a.pos + (int64_t)t * C768, lane);
-  } else {
-    d.x = load_row(a.X + (int64_t)r * C768, lane);
-  }
-  const float4* sp = reinterpret_cast<const float4*>(a.s8 + ((int64_t)b * L + slot) * 8);
-  d.s0 = sp[0];
-  d.s1 = sp[1];
-  return d;
-}
-
-// Each wave owns R rows; slots, rows and weights are all requested before the barrier (see
-// prompt_reduce_deep_kernel).  conv1x1 is transposed into LDS, W1t[ch][col], so a lane's float4
-// of columns 4 * (lane + 64 i) for channel ch is one conflict-free ds_read_b128.
-template <int MODE, int R>
 __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptArgs a) {
   __shared__ __attribute__((aligned(16))) float W1t[8 * C768];
   __shared__ __attribute__((aligned(16))) float cst[3 * C768];   // conv1x1 bias, norm1 weight, norm1 bias
-  const int lane = threadIdx.x & 63;
-  const int nw = gridDim.x * (TOK_THREADS / 64);
-  const int r0 = blockIdx.x * (TOK_THREADS / 64) + (threadIdx.x >> 6);
-  const int pr = r0 + lane * nw;
-  const int slotv = (lane < R && pr < a.rows) ? lnp_slot<MODE>(a, pr) : 0;
+  __shared__ float red[64], st[32];
+  const int lane = threadIdx.x & 63, b = blockIdx.y, L = a.Lz + a.Lx;
+  const int t = blockIdx.x * TOK_ROWS + (threadIdx.x >> 6);
+  const bool valid = t < a.rows_per_seq;
+  const int tc = min(t, a.rows_per_seq - 1);
+  const int64_t r = (int64_t)b * a.rows_per_seq + tc;
+  const int slot = (MODE == 1 || tc < a.Lz) ? tc : a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (tc - a.Lz)];
+  Row12 xv, q;
+  if (MODE == 1) {
+    xv = load_row(a.tok_rgb + r * C768, lane);
+    q = load_row(a.pos + (int64_t)tc * C768, lane);
+  } else {
+    xv = load_row(a.X + r * C768, lane);
+  }
+  const int64_t srow = ((int64_t)b * L + slot) * 8;
+  const float av = lane < 8 ? a.a8[srow + lane] : 0.f, cv = lane < 8 ? a.c8[srow + lane] : 0.f;
   constexpr int WE = 8 * C768 / 4 / TOK_THREADS;   // 3 float4 of conv1x1 (channel-major, a.w1 = W1t) per thread
   float4 wst[WE];
 #pragma unroll
@@ -452,12 +399,6 @@ __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptAr
     const int e = threadIdx.x + TOK_THREADS * k;
     cs[k] = e < C768 ? a.b1[e] : e < 2 * C768 ? a.w[e - C768] : e < 3 * C768 ? a.b[e - 2 * C768] : 0.f;
   }
-  LnpIn in[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int rj = min(r0 + j * nw, a.rows - 1);
-    in[j] = lnp_fetch<MODE>(a, rj, __builtin_amdgcn_readlane(slotv, j), lane);
-  }
 #pragma unroll
   for (int k = 0; k < WE; ++k) reinterpret_cast<float4*>(W1t)[threadIdx.x + TOK_THREADS * k] = wst[k];
 #pragma unroll
@@ -465,56 +406,51 @@ __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptAr
     const int e = threadIdx.x + TOK_THREADS * k;
     if (e < 3 * C768) cst[e] = cs[k];
   }
-  __syncthreads();
+  fovea_stats(a.a8 + (int64_t)b * L * 8, a.Lz, a.Lx, a.smooth, red, st);   // ends with a barrier
+  if (!valid) return;
+  const float s8v = lane < 8 ? fovea_s8(av, cv, st, slot < a.Lz ? 0 : 1, lane, a.smooth) : 0.f;
+  float f[8];
 #pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int r = r0 + j * nw;
-    if (r >= a.rows) break;
-    const float f[8] = {in[j].s0.x, in[j].s0.y, in[j].s0.z, in[j].s0.w, in[j].s1.x, in[j].s1.y, in[j].s1.z, in[j].s1.w};
-    Row12 x;
+  for (int ch = 0; ch < 8; ++ch) f[ch] = u2f(__builtin_amdgcn_readlane(f2u(s8v), ch));
+  Row12 x;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float4 b1 = reinterpret_cast<const float4*>(cst)[lane + 64 * i];
-      float pv[4] = {b1.x, b1.y, b1.z, b1.w};
+  for (int i = 0; i < 3; ++i) {
+    const float4 b1 = reinterpret_cast<const float4*>(cst)[lane + 64 * i];
+    float pv[4] = {b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int ch = 0; ch < 8; ++ch) {
-        const float4 wv = reinterpret_cast<const float4*>(W1t + ch * C768)[lane + 64 * i];
-        pv[0] += wv.x * f[ch];
-        pv[1] += wv.y * f[ch];
-        pv[2] += wv.z * f[ch];
-        pv[3] += wv.w * f[ch];
-      }
-      const float4 xv = in[j].x.v[i];
-      if (MODE == 1) {
-        const float4 ps = in[j].q.v[i];
-        x.v[i] = make_float4((xv.x + pv[0]) + ps.x, (xv.y + pv[1]) + ps.y, (xv.z + pv[2]) + ps.z,
-                             (xv.w + pv[3]) + ps.w);
-      } else {
-        x.v[i] = make_float4(xv.x + pv[0], xv.y + pv[1], xv.z + pv[2], xv.w + pv[3]);
-      }
+    for (int ch = 0; ch < 8; ++ch) {
+      const float4 wv = reinterpret_cast<const float4*>(W1t + ch * C768)[lane + 64 * i];
+      pv[0] += wv.x * f[ch];
+      pv[1] += wv.y * f[ch];
+      pv[2] += wv.z * f[ch];
+      pv[3] += wv.w * f[ch];
     }
-    store_f32(a.X + (int64_t)r * C768, x, lane);
-    Row12 y = ln_hat(x);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float4 gw = reinterpret_cast<const float4*>(cst + C768)[lane + 64 * i];
-      const float4 gb = reinterpret_cast<const float4*>(cst + 2 * C768)[lane + 64 * i];
-      y.v[i] = make_float4(y.v[i].x * gw.x + gb.x, y.v[i].y * gw.y + gb.y, y.v[i].z * gw.z + gb.z,
-                           y.v[i].w * gw.w + gb.w);
+    const float4 xx = xv.v[i];
+    if (MODE == 1) {
+      const float4 ps = q.v[i];
+      x.v[i] = make_float4((xx.x + pv[0]) + ps.x, (xx.y + pv[1]) + ps.y, (xx.z + pv[2]) + ps.z, (xx.w + pv[3]) + ps.w);
+    } else {
+      x.v[i] = make_float4(xx.x + pv[0], xx.y + pv[1], xx.z + pv[2], xx.w + pv[3]);
     }
-    if (a.out_lo) store_split(a.out + (int64_t)r * C768, a.out_lo + (int64_t)r * C768, y, a.out_scale, lane);
-    else store_bf16(a.out + (int64_t)r * C768, y, lane);
   }
+  store_f32(a.X + r * C768, x, lane);
+  Row12 y = ln_hat(x);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 gw = reinterpret_cast<const float4*>(cst + C768)[lane + 64 * i];
+    const float4 gb = reinterpret_cast<const float4*>(cst + 2 * C768)[lane + 64 * i];
+    y.v[i] = make_float4(y.v[i].x * gw.x + gb.x, y.v[i].y * gw.y + gb.y, y.v[i].z * gw.z + gb.z, y.v[i].w * gw.w + gb.w);
+  }
+  if (a.out_lo) store_split(a.out + r * C768, a.out_lo + r * C768, y, a.out_scale, lane);
+  else store_bf16(a.out + r * C768, y, lane);
 }
 
-void prompt_expand_ln(const PromptArgs& pa, const LnPromptArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(fovea_kernel, dim3(2, pa.B), dim3(256), 0, s, pa);
+void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s) {
+  const dim3 grid((a.rows_per_seq + TOK_ROWS - 1) / TOK_ROWS, a.rows / a.rows_per_seq);
   if (a.mode == 1)
-    launch_rows(a.rows, ln_prompt_kernel<1, 1>, ln_prompt_kernel<1, 2>, ln_prompt_kernel<1, 3>,
-                ln_prompt_kernel<1, 4>, a, s);
+    hipLaunchKernelGGL(ln_prompt_kernel<1>, grid, dim3(TOK_THREADS), 0, s, a);
   else
-    launch_rows(a.rows, ln_prompt_kernel<2, 1>, ln_prompt_kernel<2, 2>, ln_prompt_kernel<2, 3>,
-                ln_prompt_kernel<2, 4>, a, s);
+    hipLaunchKernelGGL(ln_prompt_kernel<2>, grid, dim3(TOK_THREADS), 0, s, a);
 }
 
 // ------------------------------------------------------------------ candidate elimination
@@ -599,14 +535,20 @@ void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s
 // to their 16x16 slots; pruned slots are exact zeros.
 __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int rows_per_seq, const int* slot2pos,
                                                          const float* w, const float* b, int B, int Lz, int Lx,
-                                                         bf16_t* feat, bf16_t* feat_lo, float fscale, float* dbg) {
+                                                         bf16_t* feat, bf16_t* feat_lo, float fscale, float* dbg,
+                                                         const RowReduce rr) {
   const int L = Lz + Lx;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= B * L) return;
   const int bs = r / L, s = r - bs * L;
   int pos = s < Lz ? s : slot2pos[bs * Lx + (s - Lz)];
   Row12 y = zero_row();
-  if (pos >= 0) y = ln_row(load_row(X + ((int64_t)bs * rows_per_seq + pos) * C768, lane), w, b, lane);
+  if (pos >= 0) {
+    const int64_t row = (int64_t)bs * rows_per_seq + pos;
+    Row12 x = load_row(X + row * C768, lane);
+    if (rr.ws) x = apply_reduce(x, rr, row, lane);   // the last block's fc2 update (nothing reads X after this)
+    y = ln_row(x, w, b, lane);
+  }
   if (s >= Lz && feat_lo)
     store_split(feat + ((int64_t)bs * Lx + (s - Lz)) * C768, feat_lo + ((int64_t)bs * Lx + (s - Lz)) * C768, y, fscale,
                 lane);
@@ -617,10 +559,10 @@ __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int row
 
 void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
                         int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float feat_scale, float* feat_f32_dbg,
-                        hipStream_t s) {
+                        hipStream_t s, const RowReduce& rr) {
   const int rows = B * (Lz + Lx);
   hipLaunchKernelGGL(final_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, X, rows_per_seq, slot2pos, w, b, B,
-                     Lz, Lx, feat, feat_lo, feat_scale, feat_f32_dbg);
+                     Lz, Lx, feat, feat_lo, feat_scale, feat_f32_dbg, rr);
 }
 
 }  // namespace mmt

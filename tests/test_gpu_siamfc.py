@@ -80,12 +80,25 @@ def test_device_frames_and_errors(tracker):
         tracker.init(np.zeros((10, 10, 2), np.uint8), [1, 1, 4, 4])
 
 
+def _oracle_state_from_box(ref, box, sz0, x0, z0):
+    """The oracle tracker's state after a frame whose box is `box` (TrackerSiamFC.update's state law: centre and
+    target size from the box, x_sz / z_sz scaled by the same product of scale factors as the target size)."""
+    ref.center = np.array([box[1] - 1 + (box[3] - 1) / 2, box[0] - 1 + (box[2] - 1) / 2], dtype=np.float64)
+    ref.target_sz = np.array([box[3], box[2]], dtype=np.float64)
+    k = box[3] / sz0[0]
+    ref.x_sz, ref.z_sz = x0 * k, z0 * k
+
+
 def test_c1_benchmark_dispatch_100_frames(tmp_path):
     """BASELINE configs[0] as stated: RGBE/benchmark.py dispatches `python test.py` in models/siamfc
     (RGBE/benchmark.py:42-49 of the reference) on its default one 100-frame synthetic sequence; the result
-    file it writes (RGB-E format '%.14f' comma-separated, test_rgbe_mgpus.py:83) is compared with
-    oracle/siamfc.py tracking the same frames: IoU >= 0.999 on every frame (parity unpinned: the SiamFC source
-    is absent from the reference, so the oracle is the published algorithm's restatement)."""
+    file it writes (RGB-E format '%.14f' comma-separated, test_rgbe_mgpus.py:83) is checked frame by frame
+    against oracle/siamfc.py (parity unpinned: the SiamFC source is absent from the reference, so the oracle is
+    the published algorithm's restatement).  The check is per step: the oracle is put in the state the GPU
+    tracker had after frame t-1 and tracks frame t; its box must match the GPU's (IoU >= 0.999), unless the
+    GPU's choice is a tie at fp32 resolution in the oracle's own windowed response (its value within 1e-5
+    relative of the oracle's maximum: the 272 x 272 bicubic upsampling makes neighbouring pixels near-equal,
+    and the MIOpen AlexNet sums in another order than the CPU).  A free run of the oracle is reported beside."""
     import os
     import subprocess
     import sys
@@ -102,9 +115,38 @@ def test_c1_benchmark_dispatch_100_frames(tmp_path):
     res = np.loadtxt(os.path.join(out_root, "VisEvent", "siamfc", "synthetic_000.txt"), delimiter=",")
     name, frames, gt = synthetic_sequences(1, 100, C=3)[0]
     assert res.shape == (100, 4)
+    np.testing.assert_allclose(res[0], gt[0])
     ref = osf.OracleSiamFC(synth.make_siamfc_state_dict(0))
     ref.init(frames[0], gt[0])
-    ious = [_iou(res[t], ref.update(frames[t])) for t in range(1, 100)]
-    print("C1 SiamFC 100 frames: min IoU vs oracle", min(ious))
-    assert min(ious) >= 0.999
-    np.testing.assert_allclose(res[0], gt[0])
+    sz0, x0, z0 = ref.target_sz.astype(np.float64).copy(), float(ref.x_sz), float(ref.z_sz)
+    c = ref.cfg
+    up = c["response_up"] * c["response_sz"]
+    step_ious, ties = [], 0
+    for t in range(1, 100):
+        _oracle_state_from_box(ref, res[t - 1], sz0, x0, z0)
+        prev_center, prev_x = ref.center.copy(), ref.x_sz
+        rb = ref.update(frames[t])
+        v = _iou(res[t], rb)
+        step_ious.append(v)
+        if v >= 0.999:
+            continue
+        # the GPU's choice (scale id, response pixel) recovered from its box, scored in the oracle's response
+        sid = int(np.argmin(np.abs(res[t][3] / res[t - 1][3] - ((1 - c["scale_lr"]) + c["scale_lr"] * ref.scale_factors))))
+        gc = np.array([res[t][1] - 1 + (res[t][3] - 1) / 2, res[t][0] - 1 + (res[t][2] - 1) / 2])
+        disp = (gc - prev_center) * c["instance_sz"] / (prev_x * ref.scale_factors[sid]) * c["response_up"] / c["total_stride"]
+        loc = np.rint(disp + (up - 1) / 2).astype(int)
+        resp = ref.last_responses.copy()
+        o_sid, o_loc, o_val, _ = osf.response_select(resp.copy(), c)
+        # the oracle's windowed map of the GPU's scale (response_select's normalisation of that scale's map)
+        one = resp.copy()
+        one[[k for k in range(len(one)) if k != sid]] = -1e30   # force the GPU's scale
+        _, _, _, win = osf.response_select(one, c)
+        gv = float(win[loc[0], loc[1]])
+        assert gv >= o_val * (1 - 1e-5), (t, v, sid, o_sid, tuple(loc), o_loc, gv, o_val)
+        ties += 1
+    free = osf.OracleSiamFC(synth.make_siamfc_state_dict(0))
+    free.init(frames[0], gt[0])
+    free_ious = [_iou(res[t], free.update(frames[t])) for t in range(1, 100)]
+    print(f"C1 SiamFC 100 frames: per-step min IoU {min(step_ious):.5f} ({ties} fp32 ties), free-run min IoU "
+          f"{min(free_ious):.5f}, mean {np.mean(free_ious):.5f}")
+    assert ties <= 3
