@@ -180,6 +180,18 @@ int mmt_rgbx_merge(const uint8_t* rgb, int64_t rgb_stride, const uint8_t* aux, i
 /* nn.Conv2d (+ folded BN, + residual, ReLU): y [N*Ho*Wo][Cout] = conv(x [N][H][W][Cin]); Cout % 64 == 0 */
 int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w, const float* bias, int Cout, int kh,
                    int kw, int stride, int pad, const float* resid, float* y, int flags, void* hip_stream);
+/* the same convolution on the fp16 matrix cores at fp32-faithful precision ("f16x3", csrc/dimpconv.hip):
+ * w_hi / w_lo: fp16 halves of w * w_scale (w_scale a power of two with max|w| w_scale <= 2^14), layout
+ * [Cout][Kp], K = kh*kw*Cin (Cin = 3: kh*kw*4, each tap padded to 4 channels), zero-padded to Kp =
+ * ceil(K / 32) * 32; x_max: the input's max words (mmt_conv_max_words() floats: sharded max|x| that a
+ * producing conv accumulated into its y_max) or NULL with x_scale = the static power-of-two input scale;
+ * y_max: the output's max words (accumulated with agent-scope atomic max; zero them before the producer) or
+ * NULL.  Cin % 32 == 0 or Cin == 3; flags RELU / MAX.                                                  */
+size_t mmt_conv_max_words(void);
+int mmt_conv2d_f16x3(const float* x, int N, int H, int W, int Cin, const uint16_t* w_hi, const uint16_t* w_lo,
+                     float w_scale, int Kp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
+                     const float* resid, float* y, const float* x_max, float x_scale, float* y_max, int flags,
+                     void* hip_stream);
 /* nn.MaxPool2d(k, stride, pad) over NHWC                                                           */
 int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y,
                       void* hip_stream);

@@ -101,6 +101,8 @@ SIGNATURES = {
                                ctypes.c_size_t, _P]),
     "mmt_set_frame_stream": (_I, [_P, _P]),
     "mmt_conv2d_f32": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "mmt_conv_max_words": (ctypes.c_size_t, []),
+    "mmt_conv2d_f16x3": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _I, _P]),
     "mmt_maxpool2d_f32": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "mmt_image_normalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "mmt_instance_l2norm": (_I, [_P, _I, _I, _I, _I, _F, _F, _P, _P, _P]),

@@ -13,8 +13,12 @@ built by dimp50_DeT, :421-476) as the DiMP tracker uses it (pytracking/tracker/d
 
 Weights load from the reference state_dict keys (load_state_dict strict on the keys this path reads;
 IoU-Net ``bb_regressor.*``, ``layer4`` and ``fc`` keys are accepted and unused).  BatchNorm (eval) is
-folded into each conv in float64 on the host.  Everything runs in fp32 on the device (the convolutions on
-v_mfma_f32_16x16x4_f32); there is no CPU fallback: a missing libmmtrack.so raises ImportError.
+folded into each conv in float64 on the host.  Precision (``precision``): "f16x3" (default) runs every
+convolution on the fp16 matrix cores with fp32-faithful split products (mmt_conv2d_f16x3, csrc/dimpconv.hip:
+fp16 hi / lo halves of power-of-two range-scaled operands, Wh*Ah + Wl*Ah + Wh*Al with fp32 accumulation; the
+activation scales come from each producing conv's max|y|, kept on the device); "fp32" keeps the plain fp32
+MFMA kernel (mmt_conv2d_f32).  Everything else is fp32.  There is no CPU fallback: a missing libmmtrack.so
+raises ImportError.
 """
 from __future__ import annotations
 
@@ -42,10 +46,19 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-class _Conv:
-    """One conv (+ folded BN): weight [Cout][kh][kw][Cin] and bias [Cout] fp32 on the device."""
+def range_scale(m):
+    """engine.cpp range_scale: the power of two s with m * s <= 2^14 (m > 0)."""
+    return 2.0 ** (14 - math.ceil(math.log2(m))) if m > 0 else 1.0
 
-    def __init__(self, w, bn=None, bias=None, stride=1, pad=0, dev=None, w4=True):
+
+MAX_WORDS = 64 * 32   # sharded max|y| words per tensor (mmt_conv_max_words)
+
+
+class _Conv:
+    """One conv (+ folded BN): weight [Cout][kh][kw][Cin] and bias [Cout] fp32 on the device; with f16x3 the
+    weights also as the fp16 halves of w * s_w, [Cout][Kp] (the stem: 4 channels per tap, K padded to 32)."""
+
+    def __init__(self, w, bn=None, bias=None, stride=1, pad=0, dev=None, w4=True, f16x3=False):
         w = w.detach().double()
         co = w.shape[0]
         b = bias.detach().double() if bias is not None else torch.zeros(co, dtype=torch.float64)
@@ -63,11 +76,33 @@ class _Conv:
         self.b = b.float().to(dev) if (bn is not None or bias is not None) else None
         self.cout, self.cin, self.kh, self.kw = co, w.shape[1], w.shape[2], w.shape[3]
         self.stride, self.pad = stride, pad
+        self.f16x3 = f16x3
+        if f16x3:
+            wq = w.permute(0, 2, 3, 1)
+            if self.cin == 3:
+                wq = torch.nn.functional.pad(wq, (0, 1))
+            wq = wq.reshape(co, -1).float()
+            kp = (wq.shape[1] + 31) // 32 * 32
+            wq = torch.nn.functional.pad(wq, (0, kp - wq.shape[1]))
+            self.w_scale = range_scale(float(wq.abs().max()))
+            v = wq * self.w_scale
+            hi = v.half()
+            lo = (v - hi.float()).half()
+            self.wh, self.wl, self.kp = hi.contiguous().to(dev), lo.contiguous().to(dev), kp
 
     def out_hw(self, H, W):
         return (H + 2 * self.pad - self.kh) // self.stride + 1, (W + 2 * self.pad - self.kw) // self.stride + 1
 
-    def __call__(self, lib, x, N, H, W, out, stream, relu=False, resid=None, merge_max=False):
+    def __call__(self, lib, x, N, H, W, out, stream, relu=False, resid=None, merge_max=False, x_max=None,
+                 x_scale=0.0, y_max=None):
+        """f16x3: x_max = the input's sharded max words (or x_scale, a static power-of-two input scale), y_max =
+        the output's (accumulated by the epilogue; None: not tracked)."""
+        if self.f16x3:
+            flags = (1 if relu else 0) | (2 if merge_max else 0)
+            _rc(lib.mmt_conv2d_f16x3(_p(x), N, H, W, self.cin, _p(self.wh), _p(self.wl), self.w_scale, self.kp,
+                                     _p(self.b), self.cout, self.kh, self.kw, self.stride, self.pad, _p(resid),
+                                     _p(out), _p(x_max), float(x_scale), _p(y_max), flags, stream), "mmt_conv2d_f16x3")
+            return out
         flags = (1 if relu else 0) | (2 if merge_max else 0) | (4 if self.w4 else 0)
         _rc(lib.mmt_conv2d_f32(_p(x), N, H, W, self.cin, _p(self.w), _p(self.b), self.cout, self.kh, self.kw,
                                self.stride, self.pad, _p(resid), _p(out), flags, stream), "mmt_conv2d_f32")
@@ -75,7 +110,11 @@ class _Conv:
 
 
 class DiMPNet:
-    def __init__(self, state_dict, device=None, out_dim=512, filter_size=4, feat_stride=16):
+    def __init__(self, state_dict, device=None, out_dim=512, filter_size=4, feat_stride=16, precision="f16x3"):
+        if precision not in ("f16x3", "fp32"):
+            raise ValueError(f"precision must be 'f16x3' or 'fp32', got {precision!r}")
+        self.precision = precision
+        f16 = precision == "f16x3"
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise RuntimeError("DiMPNet needs an MI355X (HIP device); there is no CPU path")
@@ -98,22 +137,28 @@ class DiMPNet:
             return [sd[pre + s] for s in (".weight", ".bias", ".running_mean", ".running_var")]
         self.backbones = []
         for fe in ("feature_extractor", "feature_extractor_depth"):
-            stem = _Conv(sd[fe + ".conv1.weight"], bn(fe + ".bn1"), stride=2, pad=3, dev=self.dev)
+            stem = _Conv(sd[fe + ".conv1.weight"], bn(fe + ".bn1"), stride=2, pad=3, dev=self.dev, f16x3=f16)
             blocks = []
             for li, (planes, nb, stride) in enumerate(RESNET50_LAYERS):
                 for b in range(nb):
                     pre = f"{fe}.layer{li + 1}.{b}"
                     s = stride if b == 0 else 1
-                    c1 = _Conv(sd[pre + ".conv1.weight"], bn(pre + ".bn1"), dev=self.dev)
-                    c2 = _Conv(sd[pre + ".conv2.weight"], bn(pre + ".bn2"), stride=s, pad=1, dev=self.dev)
-                    c3 = _Conv(sd[pre + ".conv3.weight"], bn(pre + ".bn3"), dev=self.dev)
-                    ds = _Conv(sd[pre + ".downsample.0.weight"], bn(pre + ".downsample.1"), stride=s, dev=self.dev) \
-                        if b == 0 else None
+                    c1 = _Conv(sd[pre + ".conv1.weight"], bn(pre + ".bn1"), dev=self.dev, f16x3=f16)
+                    c2 = _Conv(sd[pre + ".conv2.weight"], bn(pre + ".bn2"), stride=s, pad=1, dev=self.dev, f16x3=f16)
+                    c3 = _Conv(sd[pre + ".conv3.weight"], bn(pre + ".bn3"), dev=self.dev, f16x3=f16)
+                    ds = _Conv(sd[pre + ".downsample.0.weight"], bn(pre + ".downsample.1"), stride=s, dev=self.dev,
+                               f16x3=f16) if b == 0 else None
                     blocks.append((c1, c2, c3, ds))
             self.backbones.append((stem, blocks))
-        self.clf = _Conv(sd["classifier.feature_extractor.0.weight"], pad=1, dev=self.dev)
+        self.clf = _Conv(sd["classifier.feature_extractor.0.weight"], pad=1, dev=self.dev, f16x3=f16)
         self.fconv = _Conv(sd["classifier.filter_initializer.filter_conv.weight"], pad=1,
-                           bias=sd["classifier.filter_initializer.filter_conv.bias"], dev=self.dev)
+                           bias=sd["classifier.filter_initializer.filter_conv.bias"], dev=self.dev, f16x3=f16)
+        # f16x3 activation range: sharded max|y| words per produced tensor, zeroed once per extract_backbone;
+        # the normalised image and the InstanceL2Norm output have static bounds
+        self._max_words = torch.zeros(128 * MAX_WORDS, dtype=torch.float32, device=self.dev) if f16 else None
+        self._nslot = 0
+        self.image_scale = range_scale(max((1 - m) / s for m, s in zip(MEAN, STD)))
+        self.l2_scale = lambda L: range_scale(self.norm_scale * math.sqrt(L))
         self._mean = (ctypes.c_float * 3)(*MEAN)
         self._std = (ctypes.c_float * 3)(*STD)
         self._bufs = {}
@@ -128,33 +173,50 @@ class DiMPNet:
             b = self._bufs[name] = torch.empty(n, dtype=torch.float32, device=self.dev)
         return b[:n]
 
-    def _resnet(self, bb, x, N, H, W, out, merge_max, s):
-        """One ResNet-50 to layer3 of NHWC x [N, H, W, 3]; writes (or max-merges into) out [N, H/16, W/16, 1024]."""
+    def _slot(self):
+        """The next tensor's sharded max words (f16x3), or None in fp32 mode."""
+        if self._max_words is None:
+            return None
+        k = self._nslot
+        self._nslot += 1
+        if (k + 1) * MAX_WORDS > self._max_words.numel():
+            raise RuntimeError("DiMPNet: out of max-word slots")
+        return self._max_words[k * MAX_WORDS:(k + 1) * MAX_WORDS]
+
+    def _resnet(self, bb, x, N, H, W, out, merge_max, s, out_max):
+        """One ResNet-50 to layer3 of NHWC x [N, H, W, 3]; writes (or max-merges into) out [N, H/16, W/16, 1024].
+        f16x3: every conv reads its input's max words and accumulates its output's (out_max for layer3, shared
+        by the two backbones so it bounds the merged map)."""
         lib = self.lib
         stem, blocks = bb
         h, w = stem.out_hw(H, W)
         t0 = self._buf("stem", N * h * w * 64)
-        stem(lib, x, N, H, W, t0, s, relu=True)
+        t0_max = self._slot()
+        stem(lib, x, N, H, W, t0, s, relu=True, x_scale=self.image_scale, y_max=t0_max)
         H2, W2 = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
         cur = self._buf("ping", N * H2 * W2 * 256)
         _rc(lib.mmt_maxpool2d_f32(_p(t0), N, h, w, 64, 3, 2, 1, _p(cur), s), "mmt_maxpool2d_f32")
+        cur_max = t0_max   # a max-pool never exceeds its input's maximum
         H, W, C = H2, W2, 64
         nxt_name = "pong"
         for i, (c1, c2, c3, ds) in enumerate(blocks):
             Ho, Wo = c2.out_hw(H, W)
             a = self._buf("a", N * H * W * c1.cout)
-            c1(lib, cur, N, H, W, a, s, relu=True)
+            a_max = self._slot()
+            c1(lib, cur, N, H, W, a, s, relu=True, x_max=cur_max, y_max=a_max)
             b = self._buf("b", N * Ho * Wo * c2.cout)
-            c2(lib, a, N, H, W, b, s, relu=True)
+            b_max = self._slot()
+            c2(lib, a, N, H, W, b, s, relu=True, x_max=a_max, y_max=b_max)
             if ds is not None:
                 res = self._buf("res", N * Ho * Wo * ds.cout)
-                ds(lib, cur, N, H, W, res, s)
+                ds(lib, cur, N, H, W, res, s, x_max=cur_max)   # only ever a residual operand: no max words
             else:
                 res = cur
             last = i == len(blocks) - 1
             o = out if last else self._buf(nxt_name, N * Ho * Wo * c3.cout)
-            c3(lib, b, N, Ho, Wo, o, s, relu=True, resid=res, merge_max=merge_max and last)
-            cur, nxt_name = o, ("ping" if nxt_name == "pong" else "pong")
+            o_max = out_max if last else self._slot()
+            c3(lib, b, N, Ho, Wo, o, s, relu=True, resid=res, merge_max=merge_max and last, x_max=b_max, y_max=o_max)
+            cur, cur_max, nxt_name = o, o_max, ("ping" if nxt_name == "pong" else "pong")
             H, W, C = Ho, Wo, c3.cout
         return H, W
 
@@ -190,10 +252,15 @@ class DiMPNet:
             "mmt_image_normalize")
         Hf, Wf = (H + 15) // 16, (W + 15) // 16
         out = torch.empty(N, Hf, Wf, 1024, dtype=torch.float32, device=self.dev)
+        if self._max_words is not None:
+            self._max_words.zero_()
+            self._nslot = 0
+        out_max = self._slot()
         # the aux backbone's last conv max-merges into the RGB backbone's layer3 (dimpnet.py:103)
-        h, w = self._resnet(self.backbones[0], xa, N, H, W, out, False, s)
-        self._resnet(self.backbones[1], xb, N, H, W, out, True, s)
+        h, w = self._resnet(self.backbones[0], xa, N, H, W, out, False, s, out_max)
+        self._resnet(self.backbones[1], xb, N, H, W, out, True, s, out_max)
         assert (h, w) == (Hf, Wf)
+        self._layer3_max = (out, out_max)
         return out
 
     def extract_classification_feat(self, layer3, nhwc=False):
@@ -201,7 +268,10 @@ class DiMPNet:
         N, h, w, _ = layer3.shape
         s = self._stream()
         t = self._buf("clf", N * h * w * self.out_dim)
-        self.clf(self.lib, layer3, N, h, w, t, s)
+        lm = getattr(self, "_layer3_max", None)
+        if self.precision == "f16x3" and (lm is None or lm[0] is not layer3):
+            raise ValueError("f16x3: extract_classification_feat takes the layer3 map of the last extract_backbone")
+        self.clf(self.lib, layer3, N, h, w, t, s, x_max=lm[1] if lm else None)
         out = torch.empty(N, self.out_dim, h, w, dtype=torch.float32, device=self.dev)
         out_nhwc = torch.empty(N, h, w, self.out_dim, dtype=torch.float32, device=self.dev) if nhwc else None
         _rc(self.lib.mmt_instance_l2norm(_p(t), N, h, w, self.out_dim, self.norm_scale, 1e-5, _p(out_nhwc), _p(out), s),
@@ -214,7 +284,8 @@ class DiMPNet:
         N, h, w, C = feat_nhwc.shape
         s = self._stream()
         f = self._buf("fconv", N * h * w * C)
-        self.fconv(self.lib, feat_nhwc, N, h, w, f, s)
+        # the InstanceL2Norm output: |y| <= norm_scale * sqrt(C h w) (normalization.py:6-21)
+        self.fconv(self.lib, feat_nhwc, N, h, w, f, s, x_scale=self.l2_scale(C * h * w))
         bb = torch.as_tensor(bb, dtype=torch.float32).reshape(-1, 4).clone()
         bb[:, 2:4] = bb[:, 0:2] + bb[:, 2:4]
         rois = bb.to(self.dev)
@@ -253,16 +324,23 @@ def patch_transform_device(img, tf, out_hw):
     return out
 
 
-def conv2d(x_nchw, w, bias=None, stride=1, pad=0, resid=None, relu=False, w4=True):
-    """Test / tool helper: torch NCHW conv through mmt_conv2d_f32 (weights nn.Conv2d layout)."""
+def conv2d(x_nchw, w, bias=None, stride=1, pad=0, resid=None, relu=False, w4=True, precision="fp32", x_max=None,
+           y_max=None):
+    """Test / tool helper: torch NCHW conv through mmt_conv2d_f32 or (precision "f16x3") mmt_conv2d_f16x3
+    (weights nn.Conv2d layout; f16x3 input range: x_max words, else the static scale of max|x|)."""
     lib = _lib.load()
-    conv = _Conv(w, bias=bias, stride=stride, pad=pad, dev=x_nchw.device, w4=w4)
+    f16 = precision == "f16x3"
+    conv = _Conv(w, bias=bias, stride=stride, pad=pad, dev=x_nchw.device, w4=w4, f16x3=f16)
     N, C, H, W = x_nchw.shape
     Ho, Wo = conv.out_hw(H, W)
     x = x_nchw.permute(0, 2, 3, 1).contiguous()
     out = torch.empty(N, Ho, Wo, conv.cout, dtype=torch.float32, device=x.device)
     r = resid.permute(0, 2, 3, 1).contiguous() if resid is not None else None
-    conv(lib, x, N, H, W, out, ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream), relu=relu, resid=r)
+    kw = {}
+    if f16:
+        kw = dict(x_max=x_max, x_scale=0.0 if x_max is not None else range_scale(float(x.abs().max())), y_max=y_max)
+    conv(lib, x, N, H, W, out, ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream), relu=relu, resid=r,
+         **kw)
     return out.permute(0, 3, 1, 2)
 
 

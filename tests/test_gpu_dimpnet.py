@@ -46,6 +46,36 @@ def test_conv2d_vs_torch(N, C, H, W, Co, k, s, p):
     close(got, F.relu(ref + r), 1e-4)
 
 
+@pytest.mark.parametrize("N,C,H,W,Co,k,s,p", [(2, 3, 37, 41, 64, 7, 2, 3), (1, 64, 18, 18, 256, 1, 1, 0),
+                                             (3, 128, 19, 17, 128, 3, 1, 1), (2, 128, 36, 36, 128, 3, 2, 1),
+                                             (2, 256, 35, 33, 512, 1, 2, 0), (1, 1024, 18, 18, 512, 3, 1, 1),
+                                             (1, 64, 9, 9, 64, 3, 1, 1), (4, 256, 37, 35, 1024, 1, 1, 0),
+                                             (16, 128, 48, 48, 512, 3, 2, 1), (5, 3, 288, 288, 64, 7, 2, 3)])
+def test_conv2d_f16x3_vs_fp64(N, C, H, W, Co, k, s, p):
+    """The parity-mode conv (mmt_conv2d_f16x3: fp16 hi / lo halves of range-scaled operands, three fp16 MFMAs,
+    fp32 accumulation) against float64 on the same fp32 operands: within 2e-6 of the output's scale (fp32's
+    own summation error at these K); the epilogue's sharded max|y| words hold exactly max|y| of its output,
+    and a consumer that reads them (x_max) gives the bits of one given the same scale statically."""
+    from mmtrack_amd import _lib, dimpnet
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(N * 100 + C + k + 1)
+    x = torch.randn(N, C, H, W, generator=g) * 3.0
+    w = torch.randn(Co, C, k, k, generator=g) / math.sqrt(C * k * k)
+    b = torch.randn(Co, generator=g) * 0.1
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=s, padding=p)
+    words = torch.zeros(lib.mmt_conv_max_words(), device="cuda")
+    got = dimpnet.conv2d(x.cuda(), w, bias=b, stride=s, pad=p, precision="f16x3", y_max=words).cpu()
+    close(got, ref, 2e-6)
+    assert float(words.max()) == float(got.abs().max())
+    r = torch.randn(ref.shape, generator=g)
+    got2 = dimpnet.conv2d(x.cuda(), w, bias=b, stride=s, pad=p, resid=r.cuda(), relu=True, precision="f16x3").cpu()
+    close(got2, F.relu(ref + r.double()), 2e-6)
+    # a consumer reading the producer's words: the words of max|x| (every shard) give the static scale's bits
+    xw = torch.full((lib.mmt_conv_max_words(),), float(x.abs().max()), device="cuda")
+    got3 = dimpnet.conv2d(x.cuda(), w, bias=b, stride=s, pad=p, precision="f16x3", x_max=xw).cpu()
+    assert torch.equal(got3, got)
+
+
 def test_conv2d_stem_w4():
     """The 3-channel stem through MMT_CONV_W4 (weights padded to 4 channels per tap) and through the generic
     per-element path agree with torch and each other (summation orders differ: fp32 rounding)."""
@@ -172,14 +202,19 @@ def test_patch_transforms_vs_reference_ops():
 
 
 @pytest.fixture(scope="module")
-def net():
+def nets():
     from mmtrack_amd import synth
     from mmtrack_amd.dimpnet import DiMPNet
-    return DiMPNet(synth.make_dimp_state_dict(0))
+    sd = synth.make_dimp_state_dict(0)
+    return {p: DiMPNet(sd, precision=p) for p in ("f16x3", "fp32")}
 
 
-def test_dimpnet_matches_reference_golden(net):
+@pytest.mark.parametrize("precision", ["f16x3", "fp32"])
+def test_dimpnet_matches_reference_golden(nets, precision):
+    """Both precisions against the reference DiMPnet_DeT outputs (layer3, clf features, initial filter, scores)
+    at 1e-3 of each map's scale."""
     from mmtrack_amd import synth
+    net = nets[precision]
     gd = np.load(os.path.join(GOLDEN, "dimpnet_det.npz"))
     ims = torch.stack([torch.from_numpy(synth.make_patch(int(s), 288, 6)).float().permute(2, 0, 1)
                        for s in gd["seeds"]]).cuda()
@@ -194,7 +229,8 @@ def test_dimpnet_matches_reference_golden(net):
     close(net.classify(filt, clf).cpu(), gd["scores"])
 
 
-def test_dimp_tracker_matches_reference_sequence():
+@pytest.mark.parametrize("precision", ["f16x3", "fp32"])
+def test_dimp_tracker_matches_reference_sequence(precision):
     """The reference DiMP tracker (DeT_DiMP50_Max parameters, use_iou_net False, torch.manual_seed before
     initialize) on a 24-frame synthetic RGB-D sequence: per-frame boxes IoU >= 0.999, identical
     localisation flags, confidences within 1 % (the 10-iteration Gauss-Newton init amplifies fp32
@@ -205,7 +241,8 @@ def test_dimp_tracker_matches_reference_sequence():
     gd = np.load(os.path.join(GOLDEN, "tracker_dimp.npz"))
     seed, n, H, W, C, tseed = [int(v) for v in gd["meta"]]
     frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(gd["init_box"]))
-    tr = DiMP(parameters(), state_dict=synth.make_dimp_state_dict(0))
+    from mmtrack_amd.dimpnet import DiMPNet
+    tr = DiMP(parameters(), net=DiMPNet(synth.make_dimp_state_dict(0), precision=precision))
     torch.manual_seed(tseed)
     tr.initialize(frames[0], {"init_bbox": list(gd["init_box"])})
     close(tr.target_filter.cpu(), gd["init_filter"], 1e-2)
