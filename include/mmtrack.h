@@ -254,6 +254,59 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
                       const float* bb, const float* sample_weight, const mmt_dimp_params* p, int num_iter,
                       void* workspace, size_t ws_bytes, float* losses, void* hip_stream);
 
+/* ---- DiMP tracker state machine on the device (csrc/dimptrack.hip), batched over sequences ----------------
+ * pytracking/tracker/dimp/dimp.py (DeT) per-frame step with the DeT_DiMP50_Max parameters, use_iou_net False:
+ * the per-sequence state (position, scale, sample memory weights / boxes) lives in device memory, so a frame
+ * of n sequences is: mmt_dimp_track_sample (patch geometry + sampling from the state) -> features ->
+ * mmt_dimp_apply_filter -> mmt_dimp_track_update (get_sample_location, localize_advanced, update_state, memory
+ * bookkeeping, the Gauss-Newton iteration choice; the frame's features into the chosen memory slot) -> the
+ * host reads the n results (boxes, scores, flags, iterations) and runs mmt_dimp_optimize_dev for the
+ * sequences that asked for steps.  Arrays of structs below are device memory.                          */
+#define MMT_DIMP_MEMORY 50
+typedef struct mmt_dimp_state {
+  float pos[2], target_sz[2], base_target_sz[2], image_sz[2];   /* (y, x) as the reference's tensors       */
+  float target_scale, min_scale_factor, max_scale_factor;
+  int frame_num, num_init, num_stored, prev_replace;            /* prev_replace -1: None                   */
+  float coords[4];                                              /* this frame's sample coords (tl, br) y,x */
+  float sample_weights[MMT_DIMP_MEMORY];
+  float target_boxes[MMT_DIMP_MEMORY][4];                       /* x, y, w, h in sample coordinates        */
+} mmt_dimp_state;
+typedef struct mmt_dimp_frame {   /* the sequence's current frame: H x W x C uint8, device                  */
+  const uint8_t* data;
+  int64_t stride;
+  int H, W, C, pad_;
+} mmt_dimp_frame;
+typedef struct mmt_dimp_track_params {
+  float img_sample_sz[2], feature_sz[2], kernel_size[2];
+  double target_not_found_threshold, uncertain_threshold, hard_sample_threshold;   /* -inf: unset        */
+  double distractor_threshold, hard_negative_threshold, target_neighborhood_scale, dispalcement_scale;
+  double target_inside_ratio, low_score_opt_threshold;                             /* NaN: unset         */
+  float learning_rate, hard_negative_learning_rate, init_samples_minimum_weight;
+  int sample_memory_size, train_sample_interval, train_skipping;
+  int net_opt_update_iter, net_opt_hn_iter, net_opt_low_iter, update_classifier;
+} mmt_dimp_track_params;
+typedef struct mmt_dimp_result {  /* per sequence, per frame                                                */
+  float box[4];                   /* 'target_bbox' x, y, w, h                                               */
+  float max_score;                /* 'confidence'                                                           */
+  int flag;                       /* 0 normal, 1 not_found, 2 uncertain, 3 hard_negative                    */
+  int num_iter;                   /* Gauss-Newton steps the filter takes now (0: none)                      */
+  int n_samples;                  /* memory samples they run over (min(num_stored, 50))                    */
+  int replace_ind;                /* memory slot written this frame (-1: none)                              */
+  float tv[2], sample_pos[2], sample_scale;   /* (internal: localisation intermediates)                    */
+  int aux[4];
+} mmt_dimp_result;
+size_t mmt_dimp_state_bytes(void);
+int mmt_dimp_track_sample(mmt_dimp_state* states, const mmt_dimp_frame* frames, int n, const mmt_dimp_track_params* p,
+                          int out_h, int out_w, float* patches, void* hip_stream);
+int mmt_dimp_track_update(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
+                          const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
+                          mmt_dimp_result* results, void* hip_stream);
+/* mmt_dimp_optimize with the boxes [I][S][4] and sample weights [I][S] (or NULL) in device memory: no host
+ * staging and no synchronisation (losses are not returned)                                                  */
+int mmt_dimp_optimize_dev(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
+                          const float* bb_dev, const float* sample_weight_dev, const mmt_dimp_params* p, int num_iter,
+                          void* workspace, size_t ws_bytes, void* hip_stream);
+
 /* ---- operator-level entry points (device pointers; used by the parity tests and by hosts that
  *      compose their own pipelines).  epi: 0 bias->bf16, 1 bias+GELU->bf16, 2 C(f32) = R + acc + bias,
  *      3 bias+ReLU->bf16, 4 bias->f32, 5 bias+ReLU->f32, 6 C(f32) = acc + bias + R[m % pos_rows].

@@ -38,6 +38,26 @@ struct DimpUpdate {
   float reg, alpha_eps, step;
 };
 
+// optimizer.py:108-125's per-sample constants, formed on the device: centers [IS][2] = ((y + h / 2) / stride - off0,
+// (x + w / 2) / stride - off1) of bb [IS][4] (x, y, w, h), sqrtsw [IS] = sqrt(sample_weight) (null: 1 / I)
+struct DimpPrep {
+  const float* bb; const float* sw;   // device
+  int IS, I;
+  float feat_stride, off0, off1;
+  float* centers; float* sqrtsw;
+};
+constexpr int kDimpPrepChunk = 160;   // samples per by-value launch (kernel arguments <= 4 KB)
+struct DimpPrepArgs {                 // the same from host values, by value
+  float bb[kDimpPrepChunk * 4];
+  float sw[kDimpPrepChunk];
+  int k0, n, I, has_sw;
+  float feat_stride, off0, off1;
+  float* centers; float* sqrtsw;
+};
+struct DimpParamArgs { float v[3 * 128]; float* dst; };   // label / mask / spatial predictor weights
+void dimp_prep(const DimpPrep& a, hipStream_t s);
+void dimp_prep_args(const DimpPrepArgs& a, hipStream_t s);
+void dimp_params(const DimpParamArgs& a, hipStream_t s);
 void dimp_maps(const DimpMaps& m, hipStream_t s);
 void dimp_filter(const DimpFilter& a, hipStream_t s);
 void dimp_transpose(const DimpTranspose& a, hipStream_t s);

@@ -201,6 +201,35 @@ __global__ __launch_bounds__(256) void dimp_loss_kernel(const float* rsq, int np
   if (threadIdx.x == 0) *loss = (ra + reg * red[0]) / (float)S;
 }
 
+__global__ __launch_bounds__(256) void dimp_prep_kernel(DimpPrep a) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= a.IS) return;
+  const float* b = a.bb + 4 * k;
+  a.centers[2 * k] = (b[1] + b[3] / 2) / a.feat_stride - a.off0;       // flip((1,)) -> (y, x)
+  a.centers[2 * k + 1] = (b[0] + b[2] / 2) / a.feat_stride - a.off1;
+  a.sqrtsw[k] = a.sw ? sqrtf(a.sw[k]) : (float)sqrt(1.0 / a.I);
+}
+__global__ __launch_bounds__(256) void dimp_prep_args_kernel(DimpPrepArgs a) {
+  const int j = threadIdx.x;
+  if (j >= a.n) return;
+  const int k = a.k0 + j;
+  const float* b = a.bb + 4 * j;
+  a.centers[2 * k] = (b[1] + b[3] / 2) / a.feat_stride - a.off0;
+  a.centers[2 * k + 1] = (b[0] + b[2] / 2) / a.feat_stride - a.off1;
+  a.sqrtsw[k] = a.has_sw ? sqrtf(a.sw[j]) : (float)sqrt(1.0 / a.I);
+}
+__global__ __launch_bounds__(384) void dimp_params_kernel(DimpParamArgs a) { a.dst[threadIdx.x] = a.v[threadIdx.x]; }
+
+void dimp_prep(const DimpPrep& a, hipStream_t s) {
+  hipLaunchKernelGGL(dimp_prep_kernel, dim3((a.IS + 255) / 256), dim3(256), 0, s, a);
+}
+void dimp_prep_args(const DimpPrepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(dimp_prep_args_kernel, dim3(1), dim3(256), 0, s, a);
+}
+void dimp_params(const DimpParamArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(dimp_params_kernel, dim3(1), dim3(384), 0, s, a);
+}
+
 void dimp_maps(const DimpMaps& m, hipStream_t s) {
   const int n = m.IS * m.Ho * m.Wo;
   hipLaunchKernelGGL(dimp_maps_kernel, dim3((n + 255) / 256), dim3(256), 0, s, m);

@@ -1,6 +1,7 @@
 // C ABI of the DiMP classifier inner loop (include/mmtrack.h, mmt_dimp_*).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -50,31 +51,6 @@ bool bad_dims(int I, int S, int C, int H, int W, int fh, int fw) {
 
 }  // namespace
 
-namespace {
-// pinned host staging of mmt_dimp_optimize's per-call constants (one per process; calls are serial per
-// the ABI's threading rule)
-struct ConstStage {
-  float* host = nullptr;
-  size_t cap = 0;
-  hipEvent_t done = nullptr;
-  bool pending = false;
-} g_stage;
-
-int stage_constants(size_t n) {
-  if (g_stage.pending && hipEventSynchronize(g_stage.done) != hipSuccess) return MMT_E_HIP;
-  g_stage.pending = false;
-  if (!g_stage.done && hipEventCreateWithFlags(&g_stage.done, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
-  if (g_stage.cap < n) {
-    if (g_stage.host) hipHostFree(g_stage.host);
-    g_stage.host = nullptr;
-    g_stage.cap = 0;
-    if (hipHostMalloc((void**)&g_stage.host, n * 4, hipHostMallocDefault) != hipSuccess) return MMT_E_HIP;
-    g_stage.cap = n;
-  }
-  return MMT_OK;
-}
-}  // namespace
-
 extern "C" {
 
 size_t mmt_dimp_workspace_bytes(int I, int S, int C, int H, int W, int fh, int fw, int num_iter) {
@@ -111,46 +87,13 @@ int mmt_dimp_feat_transpose(const float* feat, const float* r, float* grad, int 
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 
-int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
-                      const float* bb, const float* sample_weight, const mmt_dimp_params* p, int num_iter,
-                      void* workspace, size_t ws_bytes, float* losses, void* stream_) {
-  if (!feat || !weights || !bb || !p || !workspace || num_iter < 0 || bad_dims(I, S, C, H, W, fh, fw) ||
-      p->num_dist_bins <= 0 || p->num_dist_bins > 128)
-    return MMT_E_ARG;
-  const WsLayout L = layout(I, S, C, H, W, fh, fw, num_iter);
-  if (ws_bytes < L.total) return MMT_E_ARG;
-  hipStream_t st = (hipStream_t)stream_;
-  char* ws = static_cast<char*>(workspace);
+// the Gauss-Newton loop of mmt_dimp_optimize / _dev once the per-sample constants are in the workspace
+static int optimize_body(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
+                         const mmt_dimp_params* p, int num_iter, char* ws, const WsLayout& L, float* losses,
+                         hipStream_t st) {
   auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
   const int IS = I * S;
-  const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, n = Ho * Wo, nby = (n + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
-  // host-side per-sample constants (optimizer.py:108-125, same fp32 arithmetic)
-  std::vector<float> centers(2 * IS), sqrtsw(IS), params(3 * 128, 0.f);
-  const float off0 = (float)(fh % 2) / 2.0f, off1 = (float)(fw % 2) / 2.0f;
-  for (int k = 0; k < IS; ++k) {
-    const float* b = bb + 4 * k;
-    centers[2 * k] = (b[1] + b[3] / 2) / p->feat_stride - off0;       // flip((1,)) -> (y, x)
-    centers[2 * k + 1] = (b[0] + b[2] / 2) / p->feat_stride - off1;
-    sqrtsw[k] = sample_weight ? std::sqrt(sample_weight[k]) : (float)std::sqrt(1.0 / I);
-  }
-  std::memcpy(params.data(), p->label_w, 128 * 4);
-  std::memcpy(params.data() + 128, p->mask_w, 128 * 4);
-  std::memcpy(params.data() + 256, p->spatial_w, 128 * 4);
-  // the constants travel from a pinned staging buffer (never from these stack vectors: the copies are
-  // asynchronous); the buffer is reused only after the previous call's copies have completed
-  const size_t nconst = centers.size() + sqrtsw.size() + params.size();
-  if (stage_constants(nconst) != MMT_OK) return MMT_E_HIP;
-  float* h = g_stage.host;
-  std::memcpy(h, centers.data(), centers.size() * 4);
-  std::memcpy(h + centers.size(), sqrtsw.data(), sqrtsw.size() * 4);
-  std::memcpy(h + centers.size() + sqrtsw.size(), params.data(), params.size() * 4);
-  if (hipMemcpyAsync(F(L.centers), h, centers.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(F(L.sqrtsw), h + centers.size(), sqrtsw.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(F(L.params), h + centers.size() + sqrtsw.size(), params.size() * 4, hipMemcpyHostToDevice,
-                     st) != hipSuccess ||
-      hipEventRecord(g_stage.done, st) != hipSuccess)
-    return MMT_E_HIP;
-  g_stage.pending = true;
+  const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, nby = (Ho * Wo + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
   const float step = std::exp(p->log_step_length);
   const float reg = std::fmax(p->filter_reg * p->filter_reg, p->min_filter_reg * p->min_filter_reg);
 
@@ -203,6 +146,67 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
       return MMT_E_HIP;
   }
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
+                      const float* bb, const float* sample_weight, const mmt_dimp_params* p, int num_iter,
+                      void* workspace, size_t ws_bytes, float* losses, void* stream_) {
+  if (!feat || !weights || !bb || !p || !workspace || num_iter < 0 || bad_dims(I, S, C, H, W, fh, fw) ||
+      p->num_dist_bins <= 0 || p->num_dist_bins > 128)
+    return MMT_E_ARG;
+  const WsLayout L = layout(I, S, C, H, W, fh, fw, num_iter);
+  if (ws_bytes < L.total) return MMT_E_ARG;
+  hipStream_t st = (hipStream_t)stream_;
+  char* ws = static_cast<char*>(workspace);
+  auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
+  const int IS = I * S;
+  // optimizer.py:108-125's per-sample constants from the host values, passed by value to the kernels that
+  // store them in the workspace (no host staging buffer, nothing to wait for)
+  DimpPrepArgs pa{};
+  pa.I = I;
+  pa.has_sw = sample_weight ? 1 : 0;
+  pa.feat_stride = p->feat_stride;
+  pa.off0 = (float)(fh % 2) / 2.0f;
+  pa.off1 = (float)(fw % 2) / 2.0f;
+  pa.centers = F(L.centers);
+  pa.sqrtsw = F(L.sqrtsw);
+  for (int k0 = 0; k0 < IS; k0 += kDimpPrepChunk) {
+    pa.k0 = k0;
+    pa.n = std::min(kDimpPrepChunk, IS - k0);
+    std::memcpy(pa.bb, bb + 4 * k0, (size_t)pa.n * 16);
+    if (sample_weight) std::memcpy(pa.sw, sample_weight + k0, (size_t)pa.n * 4);
+    dimp_prep_args(pa, st);
+  }
+  DimpParamArgs pr{};
+  std::memcpy(pr.v, p->label_w, 128 * 4);
+  std::memcpy(pr.v + 128, p->mask_w, 128 * 4);
+  std::memcpy(pr.v + 256, p->spatial_w, 128 * 4);
+  pr.dst = F(L.params);
+  dimp_params(pr, st);
+  return optimize_body(feat, I, S, C, H, W, weights, fh, fw, p, num_iter, ws, L, losses, st);
+}
+
+int mmt_dimp_optimize_dev(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
+                          const float* bb_dev, const float* sample_weight_dev, const mmt_dimp_params* p, int num_iter,
+                          void* workspace, size_t ws_bytes, void* stream_) {
+  if (!feat || !weights || !bb_dev || !p || !workspace || num_iter < 0 || bad_dims(I, S, C, H, W, fh, fw) ||
+      p->num_dist_bins <= 0 || p->num_dist_bins > 128)
+    return MMT_E_ARG;
+  const WsLayout L = layout(I, S, C, H, W, fh, fw, num_iter);
+  if (ws_bytes < L.total) return MMT_E_ARG;
+  hipStream_t st = (hipStream_t)stream_;
+  char* ws = static_cast<char*>(workspace);
+  auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
+  DimpPrep pp{bb_dev, sample_weight_dev, I * S, I, p->feat_stride, (float)(fh % 2) / 2.0f, (float)(fw % 2) / 2.0f,
+              F(L.centers), F(L.sqrtsw)};
+  dimp_prep(pp, st);
+  DimpParamArgs pr{};
+  std::memcpy(pr.v, p->label_w, 128 * 4);
+  std::memcpy(pr.v + 128, p->mask_w, 128 * 4);
+  std::memcpy(pr.v + 256, p->spatial_w, 128 * 4);
+  pr.dst = F(L.params);
+  dimp_params(pr, st);
+  return optimize_body(feat, I, S, C, H, W, weights, fh, fw, p, num_iter, ws, L, nullptr, st);
 }
 
 }  // extern "C"

@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/mmtrack.h"
 #include "common.h"
 
@@ -173,16 +175,23 @@ __global__ __launch_bounds__(512) void conv_f16x3_kernel(const ConvF16Args a) {
       for (int j = 0; j < FN; ++j) acc[i][j] = mfma16<true>(bh[j], al[i], acc[i][j]);
   };
 
-  // K-tile k: loaded into register set k & 1 two tiles ahead, stashed into LDS stage k & 1 one tile ahead
+  // K-tile k: loaded into register set k & 1 two tiles ahead, stashed into LDS stage k & 1 one tile ahead.  The
+  // loop is unrolled by two so every register set and LDS stage index is a compile-time constant (a runtime
+  // index would put the register sets behind selects and make every stash wait for all loads in flight)
   load(0, 0);
   if (nk > 1) load(1, 1);
   stash(0, 0);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 2 < nk) load(kt + 2, kt & 1);
-    compute(kt & 1);
-    if (kt + 1 < nk) stash((kt + 1) & 1, (kt + 1) & 1);
+  auto step = [&](int kt, auto set_c) {
+    constexpr int S = decltype(set_c)::value;   // == kt & 1
+    if (kt + 2 < nk) load(kt + 2, S);
+    compute(S);
+    if (kt + 1 < nk) stash(1 - S, 1 - S);
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1>{});
   }
 
   // epilogue: lane holds channels n0 + wn * WN + j * 16 + 4 * (lane >> 4) + (0..3) of pixel m0 + wm * 32 + i * 16 +

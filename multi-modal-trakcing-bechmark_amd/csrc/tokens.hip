@@ -132,13 +132,34 @@ __device__ __forceinline__ Row12 apply_reduce(const Row12& x, const RowReduce& r
 // 512-thread block, 256 threads per part in the thread layout and reduction order of the former standalone
 // fovea kernel (channel = tid & 7, slot stripes of 32), so every block that needs a sequence's statistics
 // forms the same bits.  st[part * 16 + c] = max, st[part * 16 + 8 + c] = sum.
-__device__ __forceinline__ void fovea_stats(const float* a8seq, int Lz, int Lx, float sm, float* red, float* st) {
+// The sequence's a8 first goes to LDS with coalesced 16-B loads (fovea_stage, issued by the caller with its other
+// early loads; fovea_stats stores them and reduces from LDS, as the former fovea kernel did).
+constexpr int FOVEA_MAX_TOKENS = 1024;
+constexpr int FOVEA_STAGE = FOVEA_MAX_TOKENS * 8 / 4 / 512;   // float4 per thread (512-thread blocks)
+struct FoveaStage { float4 v[FOVEA_STAGE]; };
+__device__ __forceinline__ FoveaStage fovea_stage(const float* a8seq, int L) {
+  FoveaStage f;
+#pragma unroll
+  for (int k = 0; k < FOVEA_STAGE; ++k) {
+    const int e = threadIdx.x + 512 * k;
+    if (e < L * 2) f.v[k] = reinterpret_cast<const float4*>(a8seq)[e];
+  }
+  return f;
+}
+__device__ __forceinline__ void fovea_stats(const FoveaStage& fs, int Lz, int Lx, float sm, float* va, float* red,
+                                            float* st) {
+#pragma unroll
+  for (int k = 0; k < FOVEA_STAGE; ++k) {
+    const int e = threadIdx.x + 512 * k;
+    if (e < (Lz + Lx) * 2) reinterpret_cast<float4*>(va)[e] = fs.v[k];
+  }
+  __syncthreads();
   const int tid = threadIdx.x, part = tid >> 8, t = tid & 255;
   const int lo = part ? Lz : 0, n = part ? Lx : Lz;
   const int c = t & 7, stripe = t >> 3;
   float* rp = red + part * 32;
   float mx = -INFINITY;
-  for (int k = stripe; k < n; k += 32) mx = fmaxf(mx, a8seq[(lo + k) * 8 + c] * sm);
+  for (int k = stripe; k < n; k += 32) mx = fmaxf(mx, va[(lo + k) * 8 + c] * sm);
   mx = fmaxf(mx, dpp<DPP_ROR8>(mx));
   mx = xmax16(mx);
   mx = xmax32(mx);
@@ -148,7 +169,7 @@ __device__ __forceinline__ void fovea_stats(const float* a8seq, int Lz, int Lx, 
   __syncthreads();
   const float cm = st[part * 16 + c];
   float sum = 0.f;
-  for (int k = stripe; k < n; k += 32) sum += __expf(a8seq[(lo + k) * 8 + c] * sm - cm);
+  for (int k = stripe; k < n; k += 32) sum += __expf(va[(lo + k) * 8 + c] * sm - cm);
   sum += dpp<DPP_ROR8>(sum);
   sum = xsum16(sum, sum);
   sum = xsum32(sum, sum);
@@ -287,8 +308,10 @@ constexpr int TOK_ROWS = TOK_THREADS / 64;
 __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const PromptArgs a) {
   __shared__ float fold[FOLD_N];
   __shared__ __attribute__((aligned(16))) float W0[8 * C768];   // conv0_0 (LN_A affine folded in)
+  __shared__ __attribute__((aligned(16))) float va[FOVEA_MAX_TOKENS * 8];
   __shared__ float red[64], st[32];
   const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, b = blockIdx.y;
+  const FoveaStage fsg = fovea_stage(a.a8p + (int64_t)b * L * 8, L);
   const int s = blockIdx.x * TOK_ROWS + (threadIdx.x >> 6);   // slot of this wave
   const bool valid = s < L;
   const int pos = !valid ? -1 : s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];   // wave-uniform
@@ -305,7 +328,7 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
 #pragma unroll
   for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[threadIdx.x + TOK_THREADS * k] = wst[k];
   if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
-  fovea_stats(a.a8p + (int64_t)b * L * 8, a.Lz, a.Lx, a.smooth_p, red, st);   // ends with a barrier
+  fovea_stats(fsg, a.Lz, a.Lx, a.smooth_p, va, red, st);   // ends with a barrier
   if (!valid) return;
   if (pos >= 0 && a.rr.ws) {   // the previous block's fc2 update of this slot's residual row, written back
     x = apply_reduce(x, a.rr, xrow, lane);
@@ -373,8 +396,10 @@ template <int MODE>
 __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptArgs a) {
   __shared__ __attribute__((aligned(16))) float W1t[8 * C768];
   __shared__ __attribute__((aligned(16))) float cst[3 * C768];   // conv1x1 bias, norm1 weight, norm1 bias
+  __shared__ __attribute__((aligned(16))) float va[FOVEA_MAX_TOKENS * 8];
   __shared__ float red[64], st[32];
   const int lane = threadIdx.x & 63, b = blockIdx.y, L = a.Lz + a.Lx;
+  const FoveaStage fsg = fovea_stage(a.a8 + (int64_t)b * L * 8, L);
   const int t = blockIdx.x * TOK_ROWS + (threadIdx.x >> 6);
   const bool valid = t < a.rows_per_seq;
   const int tc = min(t, a.rows_per_seq - 1);
@@ -406,7 +431,7 @@ __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptAr
     const int e = threadIdx.x + TOK_THREADS * k;
     if (e < 3 * C768) cst[e] = cs[k];
   }
-  fovea_stats(a.a8 + (int64_t)b * L * 8, a.Lz, a.Lx, a.smooth, red, st);   // ends with a barrier
+  fovea_stats(fsg, a.Lz, a.Lx, a.smooth, va, red, st);   // ends with a barrier
   if (!valid) return;
   const float s8v = lane < 8 ? fovea_s8(av, cv, st, slot < a.Lz ? 0 : 1, lane, a.smooth) : 0.f;
   float f[8];

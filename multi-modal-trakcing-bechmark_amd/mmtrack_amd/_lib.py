@@ -65,6 +65,46 @@ class MmtPatchTf(ctypes.Structure):
     ]
 
 
+MMT_DIMP_MEMORY = 50
+
+
+class MmtDimpState(ctypes.Structure):
+    _fields_ = [
+        ("pos", ctypes.c_float * 2), ("target_sz", ctypes.c_float * 2), ("base_target_sz", ctypes.c_float * 2),
+        ("image_sz", ctypes.c_float * 2), ("target_scale", ctypes.c_float), ("min_scale_factor", ctypes.c_float),
+        ("max_scale_factor", ctypes.c_float), ("frame_num", ctypes.c_int), ("num_init", ctypes.c_int),
+        ("num_stored", ctypes.c_int), ("prev_replace", ctypes.c_int), ("coords", ctypes.c_float * 4),
+        ("sample_weights", ctypes.c_float * MMT_DIMP_MEMORY), ("target_boxes", (ctypes.c_float * 4) * MMT_DIMP_MEMORY),
+    ]
+
+
+class MmtDimpFrame(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("stride", ctypes.c_int64), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("C", ctypes.c_int), ("pad_", ctypes.c_int)]
+
+
+class MmtDimpTrackParams(ctypes.Structure):
+    _fields_ = [
+        ("img_sample_sz", ctypes.c_float * 2), ("feature_sz", ctypes.c_float * 2), ("kernel_size", ctypes.c_float * 2),
+        ("target_not_found_threshold", ctypes.c_double), ("uncertain_threshold", ctypes.c_double),
+        ("hard_sample_threshold", ctypes.c_double), ("distractor_threshold", ctypes.c_double),
+        ("hard_negative_threshold", ctypes.c_double), ("target_neighborhood_scale", ctypes.c_double),
+        ("dispalcement_scale", ctypes.c_double), ("target_inside_ratio", ctypes.c_double),
+        ("low_score_opt_threshold", ctypes.c_double), ("learning_rate", ctypes.c_float),
+        ("hard_negative_learning_rate", ctypes.c_float), ("init_samples_minimum_weight", ctypes.c_float),
+        ("sample_memory_size", ctypes.c_int), ("train_sample_interval", ctypes.c_int), ("train_skipping", ctypes.c_int),
+        ("net_opt_update_iter", ctypes.c_int), ("net_opt_hn_iter", ctypes.c_int), ("net_opt_low_iter", ctypes.c_int),
+        ("update_classifier", ctypes.c_int),
+    ]
+
+
+class MmtDimpResult(ctypes.Structure):
+    _fields_ = [("box", ctypes.c_float * 4), ("max_score", ctypes.c_float), ("flag", ctypes.c_int),
+                ("num_iter", ctypes.c_int), ("n_samples", ctypes.c_int), ("replace_ind", ctypes.c_int),
+                ("tv", ctypes.c_float * 2), ("sample_pos", ctypes.c_float * 2), ("sample_scale", ctypes.c_float),
+                ("aux", ctypes.c_int * 4)]
+
+
 # every symbol include/mmtrack.h declares: name -> (restype, argtypes)
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -115,6 +155,11 @@ SIGNATURES = {
     "mmt_dimp_feat_transpose": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_dimp_optimize": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, ctypes.POINTER(MmtDimpParams), _I, _P,
                                ctypes.c_size_t, _P, _P]),
+    "mmt_dimp_optimize_dev": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, ctypes.POINTER(MmtDimpParams), _I, _P,
+                                   ctypes.c_size_t, _P]),
+    "mmt_dimp_state_bytes": (ctypes.c_size_t, []),
+    "mmt_dimp_track_sample": (_I, [_P, _P, _I, ctypes.POINTER(MmtDimpTrackParams), _I, _I, _P, _P]),
+    "mmt_dimp_track_update": (_I, [_P, _I, _P, _I, _I, ctypes.POINTER(MmtDimpTrackParams), _P, _I64, _P, _P, _P]),
     "mmt_gemm_stamps": (_I, [_P]),
     "mmt_op_gemm": (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_gemm_force_config": (_I, [_I]),
