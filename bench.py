@@ -360,14 +360,15 @@ def dimp_main(args, rank, world, dist):
     a step = one frame of every sequence (patch sampling, two ResNet-50 backbones + clf features for the
     batch, grouped filter application, per-sequence localisation / memory / Gauss-Newton updates)."""
     from mmtrack_amd import synth
-    from mmtrack_amd.dimp_tracker import DiMP, parameters, track_batch
+    from mmtrack_amd.dimp_tracker import DiMP, DimpPool, parameters, track_batch
     from mmtrack_amd.dimpnet import DiMPNet
     B, H, W, C = args.batch, 480, 640, 6
     sd = synth.make_dimp_state_dict(0)
     net = DiMPNet(sd, precision=args.dimp_precision)
     video_np, gts = synth.make_frames(1000 + rank, args.frames + 1, H, W, C)
     video = torch.from_numpy(video_np).cuda()
-    trackers = [DiMP(parameters(), net=net) for _ in range(B)]
+    pool = DimpPool(net, B, parameters())   # the trackers' device-resident state, one slot each
+    trackers = [DiMP(parameters(), net=net, pool=pool) for _ in range(B)]
     torch.manual_seed(rank)
     for i, t in enumerate(trackers):
         t.initialize(video[0], {"init_bbox": [60.0 + (37 * i) % (W - 160), 40.0 + (23 * i) % (H - 120),

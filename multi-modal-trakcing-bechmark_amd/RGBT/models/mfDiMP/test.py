@@ -27,7 +27,7 @@ def main(argv=None):
     import torch
 
     from mmtrack_amd import synth
-    from mmtrack_amd.dimp_tracker import DiMP, parameters, track_batch
+    from mmtrack_amd.dimp_tracker import DiMP, DimpPool, parameters, track_batch
     from mmtrack_amd.dimpnet import DiMPNet
     from mmtrack_amd.sharding import rank_world, shard_indices
     from mmtrack_amd.workspace import frame_getter, gen_config, sequence_list
@@ -74,7 +74,8 @@ def main(argv=None):
     t0, tracked = time.perf_counter(), 0
     for b0 in range(0, len(mine), args.batch):
         group = mine[b0:b0 + args.batch]
-        trackers = [DiMP(parameters(), net=net) for _ in group]
+        pool = DimpPool(net, len(group), parameters())
+        trackers = [DiMP(parameters(), net=net, pool=pool) for _ in group]
         results = [np.zeros((n, 4)) for _, n, _, _ in group]
         for tr, (name, n, get, gt), res in zip(trackers, group, results):
             tr.initialize(get(0), {"init_bbox": list(np.asarray(gt[0], dtype=np.float64))})

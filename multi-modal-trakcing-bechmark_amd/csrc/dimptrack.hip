@@ -208,6 +208,7 @@ __global__ __launch_bounds__(256) void dimp_localize_kernel(mmt_dimp_state* stat
   __shared__ float sm[1024];
   __shared__ float red_v[64];
   __shared__ int red_i[64];
+  __shared__ mmt_dimp_result sres;   // thread 0's decisions, broadcast to the block
   const int s = blockIdx.x, t = threadIdx.x;
   mmt_dimp_state& st = states[s];
   const int n = sh * sw_;
@@ -218,6 +219,7 @@ __global__ __launch_bounds__(256) void dimp_localize_kernel(mmt_dimp_state* stat
   max2d(sm, sh, sw_, red_v, red_i, ms1, r1, c1);
   mmt_dimp_result res{};
   if (t == 0) {
+    st.frame_num += 1;   // track(): self.frame_num += 1 (dimp.py:98)
     // get_sample_location (dimp.py:314-319)
     const float* co = st.coords;
     float spos[2], ratio[2];
@@ -270,10 +272,10 @@ __global__ __launch_bounds__(256) void dimp_localize_kernel(mmt_dimp_state* stat
     res.sample_pos[1] = spos[1];
     res.sample_scale = sscale;
     res.max_score = ms1;
-    results[s] = res;
+    sres = res;
   }
   __syncthreads();
-  res = results[s];
+  res = sres;
   if (res.flag < 0) {
     for (int k = t; k < n; k += 256) {
       const int r = k / sw_, c = k - r * sw_;

@@ -136,6 +136,23 @@ class DiMPSteepestDescentGN:
             losses.append(torch.tensor(lbuf[0]))
         return w, iterates, losses
 
+    def optimize_dev(self, weights, feat, bb_ptr, sw_ptr, num_iter):
+        """num_iter steps in place on ``weights`` (a contiguous [S, C, fh, fw] CUDA tensor) with the boxes
+        [I][S][4] and sample weights [I][S] at device addresses (the device tracker state): no host staging, no
+        synchronisation (mmt_dimp_optimize_dev)."""
+        lib = _lib.load()
+        feat = _check(feat, "feat", 5)
+        I, S, C, H, W = feat.shape
+        fh, fw = weights.shape[-2:]
+        nbytes = lib.mmt_dimp_workspace_bytes(I, S, C, H, W, fh, fw, num_iter)
+        if nbytes == 0:
+            raise ValueError("unsupported DiMP problem shape")
+        ws = self._workspace(feat.device, nbytes)
+        _rc(lib.mmt_dimp_optimize_dev(feat.data_ptr(), I, S, C, H, W, weights.data_ptr(), fh, fw, ctypes.c_void_p(bb_ptr),
+                                      ctypes.c_void_p(sw_ptr) if sw_ptr else None, ctypes.byref(self.params), num_iter,
+                                      ws.data_ptr(), nbytes, _stream(feat.device)), "mmt_dimp_optimize_dev")
+        return weights
+
     def optimize(self, weights, feat, bb, sample_weight=None, num_iter=None):
         """All iterations in one call (no per-iterate copies, no host sync): the tracker-side use."""
         lib = _lib.load()

@@ -6,20 +6,26 @@ init augmentation :322-385, classifier init / memory / update :399-504 and :538-
 device path:
 
 * patch sampling, init augmentations, the two ResNet-50 backbones + max merge, the clf features, the
-  filter initialiser (PrRoIPool) run as HIP kernels (mmtrack_amd.dimpnet, csrc/dimpnet.hip);
+  filter initialiser (PrRoIPool) run as HIP kernels (mmtrack_amd.dimpnet, csrc/dimpnet.hip, dimpconv.hip);
 * the steepest-descent Gauss-Newton filter optimiser and the classifier (apply_filter) run as HIP
   kernels (mmtrack_amd.dimp, csrc/dimp.hip);
-* the host keeps the tracker's scalar state (position, scale, sample weights and boxes) in float32 CPU
-  tensors with the reference's own arithmetic, and the 19 x 19 score map comes back once per frame.
+* the per-frame state machine -- sample geometry from the tracked position and scale, localize_advanced,
+  update_state, the sample memory's weights / boxes / slots and the choice of Gauss-Newton iterations --
+  runs on the device over every sequence of a batch at once (csrc/dimptrack.hip): the tracker state lives
+  in device memory (``DimpPool``), and per frame only a small result record per sequence (box, score, flag,
+  iterations) comes back to the host, which launches the filter updates the records ask for.
+  Initialisation (augmented samples, initial filter, 10 Gauss-Newton steps) is host-orchestrated, once.
 
 IoU-Net box refinement (AtomIoUNet + PrRoIPool gradients, dimp.py:609-700) is not part of this path:
 ``parameters()`` sets ``use_iou_net = False``, the reference's switch for it (dimp.py:76-78, 123-130), so
-position comes from the classifier and the size follows the sample scale.  Random init augmentation shifts
-and the dropout masks draw from the host torch generator in the reference's order, so a seeded run matches
-the reference run with the same seed.
+position comes from the classifier and the size follows the sample scale (the tracker golden was made with
+the same setting; parity with the reference's default IoU-Net configuration is not claimed).  Random init
+augmentation shifts and the dropout masks draw from the host torch generator in the reference's order, so a
+seeded run matches the reference run with the same seed.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
@@ -127,7 +133,7 @@ class _Tf:
 class DiMP:
     multiobj_mode = 'parallel'
 
-    def __init__(self, params, state_dict=None, device=None, net=None):
+    def __init__(self, params, state_dict=None, device=None, net=None, pool=None):
         self.params = params
         if net is None:
             sd = state_dict if state_dict is not None else getattr(params, 'state_dict', None)
@@ -136,6 +142,11 @@ class DiMP:
             net = DiMPNet(sd, device=device)
         self.net = net
         self.dev = self.net.dev
+        # the device-resident per-frame state: a slot of a shared pool (batched trackers) or a pool of its own
+        self.pool = pool if pool is not None else DimpPool(net, 1, params)
+        if self.pool.net is not net:
+            raise ValueError("the pool belongs to another DiMPNet")
+        self.slot = self.pool.alloc()
         self.optimizer = DiMPSteepestDescentGN(self.net.sd_opt, num_iter=5, feat_stride=16,
                                                num_dist_bins=self.net.sd_opt["label_map_predictor.weight"].numel(),
                                                bin_displacement=getattr(params, 'bin_displacement', 0.1))
@@ -261,220 +272,220 @@ class DiMP:
         return init_target_boxes
 
     def init_memory(self, x):
+        """init_memory (dimp.py:505-536): the sample memory and the tracker state into the device slot."""
         self.num_init_samples = x.shape[0]
-        self.num_stored_samples = self.num_init_samples
-        self.previous_replace_ind = None
-        self.sample_weights = torch.zeros(self.params.sample_memory_size)
-        self.sample_weights[:self.num_init_samples] = torch.ones(1) / x.shape[0]
-        self.training_samples = x.new_zeros(self.params.sample_memory_size, *x.shape[1:])
-        self.training_samples[:x.shape[0]] = x
-
-    def track(self, image, info: dict = None) -> dict:
-        patch, coords = self.track_sample(image)
-        test_x = self.net.extract_classification_feat(self.net.extract_backbone(patch))
-        scores = self.net.classify(self.target_filter, test_x).squeeze(1).cpu()
-        return self.track_update(test_x, scores, coords)
-
-    # the per-frame step in two halves so that track_batch can run the network once for many sequences
-    def track_sample(self, image, out=None):
-        """dimp.py:85-99 up to the patch: frame counter, the centred sample position, the search patch
-        (written into ``out`` when given) -> (patch [1, 6, 288, 288], sample_coords [1, 4])."""
-        self.debug_info = {}
-        self.frame_num += 1
-        frame = self._frame(image)
-        sample_pos_c = self.pos + ((self.feature_sz + self.kernel_size) % 2) * self.target_scale * \
-            self.img_support_sz / (2 * self.feature_sz)
-        patch, coords = self._sample_patch(frame, sample_pos_c, self.target_scale * self.scale_factors[0] *
-                                           self.img_sample_sz, self.img_sample_sz)
-        if out is not None:
-            out.copy_(patch[0])
-        return patch, coords
-
-    def track_update(self, test_x, scores, sample_coords):
-        """dimp.py:101-166 after the classifier: localisation, state update, memory / filter update, output.
-        test_x: this sequence's clf features [1, 512, 18, 18] (device); scores: [1, 19, 19] (host)."""
-        sample_pos, sample_scales = self.get_sample_location(sample_coords)
-        translation_vec, scale_ind, s, flag = self.localize_advanced(scores, sample_pos, sample_scales)
-        new_pos = sample_pos[scale_ind, :] + translation_vec
-        if flag != 'not_found':
-            self.update_state(new_pos, sample_scales[scale_ind])
-        update_flag = flag not in ['not_found', 'uncertain']
-        hard_negative = flag == 'hard_negative'
-        learning_rate = self.params.get('hard_negative_learning_rate', None) if hard_negative else None
-        if update_flag and self.params.get('update_classifier', False):
-            train_x = test_x[scale_ind:scale_ind + 1, ...]
-            target_box = self.get_iounet_box(self.pos, self.target_sz, sample_pos[scale_ind, :],
-                                             sample_scales[scale_ind])
-            self.update_classifier(train_x, target_box, learning_rate, s[scale_ind, ...])
-        score_map = s[scale_ind, ...]
-        max_score = torch.max(score_map).item()
-        self.debug_info['flag'] = flag
-        self.debug_info['max_score'] = max_score
-        self.debug_info['score_map'] = score_map
-        new_state = torch.cat((self.pos[[1, 0]] - (self.target_sz[[1, 0]] - 1) / 2, self.target_sz[[1, 0]]))
-        return {'target_bbox': new_state.tolist(), 'confidence': max_score}
-
-    def get_sample_location(self, sample_coord):
-        sample_coord = sample_coord.float()
-        sample_pos = 0.5 * (sample_coord[:, :2] + sample_coord[:, 2:] - 1)
-        sample_scales = ((sample_coord[:, 2:] - sample_coord[:, :2]) / self.img_sample_sz).prod(dim=1).sqrt()
-        return sample_pos, sample_scales
-
-    @staticmethod
-    def max2d(a):
-        """pytracking dcf.max2d: maximum and (row, col) argmax over the last two dims."""
-        max_val_row, argmax_row = torch.max(a, dim=-2)
-        max_val, argmax_col = torch.max(max_val_row, dim=-1)
-        argmax_row = argmax_row.view(argmax_col.numel(), -1)[torch.arange(argmax_col.numel()), argmax_col.view(-1)]
-        argmax_row = argmax_row.reshape(argmax_col.shape)
-        return max_val, torch.cat((argmax_row.unsqueeze(-1), argmax_col.unsqueeze(-1)), -1)
-
-    def localize_advanced(self, scores, sample_pos, sample_scales):
-        sz = scores.shape[-2:]
-        score_sz = torch.Tensor(list(sz))
-        output_sz = score_sz - (self.kernel_size + 1) % 2
-        score_center = (score_sz - 1) / 2
-        scores_hn = scores
-        max_score1, max_disp1 = self.max2d(scores)
-        _, scale_ind = torch.max(max_score1, dim=0)
-        sample_scale = sample_scales[scale_ind]
-        max_score1 = max_score1[scale_ind]
-        max_disp1 = max_disp1[scale_ind, ...].float().view(-1)
-        target_disp1 = max_disp1 - score_center
-        translation_vec1 = target_disp1 * (self.img_support_sz / output_sz) * sample_scale
-        p = self.params
-        if max_score1.item() < p.target_not_found_threshold:
-            return translation_vec1, scale_ind, scores_hn, 'not_found'
-        if max_score1.item() < p.get('uncertain_threshold', -float('inf')):
-            return translation_vec1, scale_ind, scores_hn, 'uncertain'
-        if max_score1.item() < p.get('hard_sample_threshold', -float('inf')):
-            return translation_vec1, scale_ind, scores_hn, 'hard_negative'
-        target_neigh_sz = p.target_neighborhood_scale * (self.target_sz / sample_scale) * (output_sz /
-                                                                                           self.img_support_sz)
-        top = max(round(max_disp1[0].item() - target_neigh_sz[0].item() / 2), 0)
-        bottom = min(round(max_disp1[0].item() + target_neigh_sz[0].item() / 2 + 1), sz[0])
-        left = max(round(max_disp1[1].item() - target_neigh_sz[1].item() / 2), 0)
-        right = min(round(max_disp1[1].item() + target_neigh_sz[1].item() / 2 + 1), sz[1])
-        scores_masked = scores_hn[scale_ind:scale_ind + 1, ...].clone()
-        scores_masked[..., top:bottom, left:right] = 0
-        max_score2, max_disp2 = self.max2d(scores_masked)
-        max_disp2 = max_disp2.float().view(-1)
-        target_disp2 = max_disp2 - score_center
-        translation_vec2 = target_disp2 * (self.img_support_sz / output_sz) * sample_scale
-        prev_target_vec = (self.pos - sample_pos[scale_ind, :]) / ((self.img_support_sz / output_sz) * sample_scale)
-        if max_score2 > p.distractor_threshold * max_score1:
-            disp_norm1 = torch.sqrt(torch.sum((target_disp1 - prev_target_vec) ** 2))
-            disp_norm2 = torch.sqrt(torch.sum((target_disp2 - prev_target_vec) ** 2))
-            disp_threshold = p.dispalcement_scale * math.sqrt(sz[0] * sz[1]) / 2
-            if disp_norm2 > disp_threshold and disp_norm1 < disp_threshold:
-                return translation_vec1, scale_ind, scores_hn, 'hard_negative'
-            if disp_norm2 < disp_threshold and disp_norm1 > disp_threshold:
-                return translation_vec2, scale_ind, scores_hn, 'hard_negative'
-            if disp_norm2 > disp_threshold and disp_norm1 > disp_threshold:
-                return translation_vec1, scale_ind, scores_hn, 'uncertain'
-            return translation_vec1, scale_ind, scores_hn, 'uncertain'
-        if max_score2 > p.hard_negative_threshold * max_score1 and max_score2 > p.target_not_found_threshold:
-            return translation_vec1, scale_ind, scores_hn, 'hard_negative'
-        return translation_vec1, scale_ind, scores_hn, 'normal'
-
-    def update_state(self, new_pos, new_scale=None):
-        if new_scale is not None:
-            self.target_scale = new_scale.clamp(self.min_scale_factor, self.max_scale_factor)
-            self.target_sz = self.base_target_sz * self.target_scale
-        inside_offset = (self.params.get('target_inside_ratio', 0.2) - 0.5) * self.target_sz
-        self.pos = torch.max(torch.min(new_pos, self.image_sz - inside_offset), inside_offset)
+        sw = torch.zeros(self.params.sample_memory_size)
+        sw[:self.num_init_samples] = torch.ones(1) / x.shape[0]
+        st = _lib.MmtDimpState()
+        for name in ("pos", "target_sz", "base_target_sz", "image_sz"):
+            v = getattr(self, name).float()
+            getattr(st, name)[0], getattr(st, name)[1] = float(v[0]), float(v[1])
+        st.target_scale = float(torch.as_tensor(self.target_scale, dtype=torch.float32))
+        st.min_scale_factor = float(self.min_scale_factor)
+        st.max_scale_factor = float(self.max_scale_factor)
+        st.frame_num = self.frame_num
+        st.num_init = st.num_stored = self.num_init_samples
+        st.prev_replace = -1
+        for k in range(self.params.sample_memory_size):
+            st.sample_weights[k] = float(sw[k])
+            for j in range(4):
+                st.target_boxes[k][j] = float(self.target_boxes[k, j])
+        self.pool.write_state(self.slot, st, x)
 
     def get_iounet_box(self, pos, sz, sample_pos, sample_scale):
+        """dimp.py:468-475 (the initial target boxes; per frame the device restates it)."""
         box_center = (pos - sample_pos) / sample_scale + (self.img_sample_sz - 1) / 2
         box_sz = sz / sample_scale
         target_ul = box_center - (box_sz - 1) / 2
         return torch.cat([target_ul.flip((0,)), box_sz.flip((0,))])
 
-    def update_classifier(self, train_x, target_box, learning_rate=None, scores=None):
-        hard_negative_flag = learning_rate is not None
-        if learning_rate is None:
-            learning_rate = self.params.learning_rate
-        if hard_negative_flag or self.frame_num % self.params.get('train_sample_interval', 1) == 0:
-            self.update_memory(train_x, target_box, learning_rate)
-        num_iter = 0
-        low_score_th = self.params.get('low_score_opt_threshold', None)
-        if hard_negative_flag:
-            num_iter = self.params.get('net_opt_hn_iter', None)
-        elif low_score_th is not None and low_score_th > scores.max().item():
-            num_iter = self.params.get('net_opt_low_iter', None)
-        elif (self.frame_num - 1) % self.params.train_skipping == 0:
-            num_iter = self.params.get('net_opt_update_iter', None)
-        if num_iter > 0:
-            n = min(self.num_stored_samples, self.params.sample_memory_size)
-            samples = self.training_samples[:n].unsqueeze(1).contiguous()
-            self.target_filter = self.optimizer.optimize(self.target_filter, samples,
-                                                         self.target_boxes[:n].clone().view(-1, 1, 4),
-                                                         sample_weight=self.sample_weights[:n].view(-1, 1),
-                                                         num_iter=num_iter)
+    def track(self, image, info: dict = None) -> dict:
+        """track (dimp.py:85-166): one frame through the device state machine (a batch of one)."""
+        return track_batch([self], [image])[0]
 
-    def update_memory(self, sample_x, target_box, learning_rate=None):
-        replace_ind = self.update_sample_weights(learning_rate)
-        self.previous_replace_ind = replace_ind
-        self.training_samples[replace_ind:replace_ind + 1, ...] = sample_x
-        self.target_boxes[replace_ind, :] = target_box
-        self.num_stored_samples += 1
+    def _output(self, res):
+        flag = FLAGS[res.flag]
+        self.debug_info = {'flag': flag, 'max_score': float(res.max_score)}
+        return {'target_bbox': [float(v) for v in res.box], 'confidence': float(res.max_score)}
 
-    def update_sample_weights(self, learning_rate=None):
-        sw, prev_ind = self.sample_weights, self.previous_replace_ind
-        num_samp, num_init = self.num_stored_samples, self.num_init_samples
-        lr = learning_rate if learning_rate is not None else self.params.learning_rate
-        init_samp_weight = self.params.get('init_samples_minimum_weight', None)
-        if init_samp_weight == 0:
-            init_samp_weight = None
-        s_ind = 0 if init_samp_weight is None else num_init
-        if num_samp == 0 or lr == 1:
-            sw[:] = 0
-            sw[0] = 1
-            r_ind = 0
-        else:
-            if num_samp < sw.shape[0]:
-                r_ind = num_samp
-            else:
-                _, r_ind = torch.min(sw[s_ind:], 0)
-                r_ind = r_ind.item() + s_ind
-            if prev_ind is None:
-                sw /= 1 - lr
-                sw[r_ind] = lr
-            else:
-                sw[r_ind] = sw[prev_ind] / (1 - lr)
-        sw /= sw.sum()
-        if init_samp_weight is not None and sw[:num_init].sum() < init_samp_weight:
-            sw /= init_samp_weight + sw[num_init:].sum()
-            sw[:num_init] = init_samp_weight / num_init
-        return r_ind
+    def _update_filter(self, res):
+        """update_classifier's Gauss-Newton steps (dimp.py:555-570) when the frame's record asks for them: the
+        filter is optimised in place over the slot's memory samples, boxes and weights (all on the device)."""
+        if res.num_iter <= 0:
+            return
+        n = res.n_samples
+        samples = self.pool.memory[self.slot, :n].unsqueeze(1)
+        bb, sw = self.pool.boxes_ptr(self.slot), self.pool.weights_ptr(self.slot)
+        self.optimizer.optimize_dev(self.target_filter, samples, bb, sw, res.num_iter)
+
+
+FLAGS = ('normal', 'not_found', 'uncertain', 'hard_negative')
+
+
+class DimpPool:
+    """Device-resident state of up to ``capacity`` DiMP trackers sharing one DiMPNet: one mmt_dimp_state per
+    slot (position, scale, sample weights and boxes), the sample memory [capacity][50][512][18][18] fp32, and
+    the per-frame result records (pinned host copy).  Trackers of one pool whose slots are consecutive are
+    advanced together by track_batch."""
+
+    def __init__(self, net, capacity, params):
+        self.net, self.cap, self.dev = net, capacity, net.dev
+        self.lib = _lib.load()
+        self.sbytes = self.lib.mmt_dimp_state_bytes()
+        if self.sbytes != ctypes.sizeof(_lib.MmtDimpState):
+            raise RuntimeError("libmmtrack.so's mmt_dimp_state does not match the binding")
+        self.states = torch.zeros(capacity * self.sbytes, dtype=torch.uint8, device=self.dev)
+        self.rbytes = ctypes.sizeof(_lib.MmtDimpResult)
+        self.results = torch.zeros(capacity * self.rbytes, dtype=torch.uint8, device=self.dev)
+        self.memory = None   # [capacity][50][C][h][w], allocated with the first sample shape
+        self.next = 0
+        p = _lib.MmtDimpTrackParams()
+        sz = params.image_sample_size
+        sz = (sz, sz) if isinstance(sz, int) else tuple(sz)
+        fsz = (sz[0] // net.feat_stride, sz[1] // net.feat_stride)
+        for d in range(2):
+            p.img_sample_sz[d], p.feature_sz[d], p.kernel_size[d] = float(sz[d]), float(fsz[d]), float(net.filter_size)
+        g = params.get
+        inf = float('inf')
+        p.target_not_found_threshold = g('target_not_found_threshold')
+        p.uncertain_threshold = g('uncertain_threshold', -inf)
+        p.hard_sample_threshold = g('hard_sample_threshold', -inf)
+        p.distractor_threshold = g('distractor_threshold')
+        p.hard_negative_threshold = g('hard_negative_threshold')
+        p.target_neighborhood_scale = g('target_neighborhood_scale')
+        p.dispalcement_scale = g('dispalcement_scale')
+        p.target_inside_ratio = g('target_inside_ratio', 0.2)
+        low = g('low_score_opt_threshold', None)
+        p.low_score_opt_threshold = float('nan') if low is None else low
+        p.learning_rate = g('learning_rate')
+        p.hard_negative_learning_rate = g('hard_negative_learning_rate', None) or g('learning_rate')
+        p.init_samples_minimum_weight = g('init_samples_minimum_weight', None) or 0.0
+        p.sample_memory_size = g('sample_memory_size')
+        p.train_sample_interval = g('train_sample_interval', 1)
+        p.train_skipping = g('train_skipping')
+        p.net_opt_update_iter = g('net_opt_update_iter', None) or 0
+        p.net_opt_hn_iter = g('net_opt_hn_iter', None) or 0
+        p.net_opt_low_iter = g('net_opt_low_iter', None) or 0
+        p.update_classifier = int(bool(g('update_classifier', False)))
+        if not g('advanced_localization', False) or g('use_iou_net', True) or g('window_output', False):
+            raise NotImplementedError("the device DiMP path restates advanced localisation without IoU-Net / window")
+        if p.sample_memory_size != _lib.MMT_DIMP_MEMORY:
+            raise ValueError(f"sample_memory_size must be {_lib.MMT_DIMP_MEMORY}")
+        self.tparams = p
+        self.frames_host = (_lib.MmtDimpFrame * capacity)()
+        self.frames = torch.empty(capacity * ctypes.sizeof(_lib.MmtDimpFrame), dtype=torch.uint8, device=self.dev)
+        self.res_host = torch.empty(capacity * self.rbytes, dtype=torch.uint8, pin_memory=True)
+
+    def alloc(self):
+        if self.next >= self.cap:
+            raise RuntimeError(f"DimpPool: all {self.cap} slots are in use")
+        self.next += 1
+        return self.next - 1
+
+    def state_ptr(self, slot):
+        return self.states.data_ptr() + slot * self.sbytes
+
+    def boxes_ptr(self, slot):
+        return self.state_ptr(slot) + _lib.MmtDimpState.target_boxes.offset
+
+    def weights_ptr(self, slot):
+        return self.state_ptr(slot) + _lib.MmtDimpState.sample_weights.offset
+
+    def write_state(self, slot, st, x):
+        raw = torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8)
+        self.states[slot * self.sbytes:(slot + 1) * self.sbytes].copy_(raw)
+        if self.memory is None:
+            self.memory = torch.zeros(self.cap, _lib.MMT_DIMP_MEMORY, *x.shape[1:], dtype=torch.float32, device=self.dev)
+        self.memory[slot, :x.shape[0]] = x
+        self.memory[slot, x.shape[0]:] = 0
+
+    def result(self, slot):
+        return _lib.MmtDimpResult.from_buffer_copy(bytes(self.res_host[slot * self.rbytes:(slot + 1) * self.rbytes]
+                                                         .numpy()))
+
+    def launch(self, trackers, frames, first):
+        """Sample, network, classifier and the device state update for trackers in slots [first, first + n);
+        the result records go to pinned host memory behind the returned event."""
+        lib, n, net = self.lib, len(trackers), self.net
+        fr = [t._frame(f) for t, f in zip(trackers, frames)]
+        for i, f in enumerate(fr):
+            d = self.frames_host[first + i]
+            d.data, d.stride, d.H, d.W, d.C = f.data_ptr(), f.stride(0), f.shape[0], f.shape[1], f.shape[2]
+        fb = ctypes.sizeof(_lib.MmtDimpFrame)
+        host = torch.frombuffer(bytearray(bytes(self.frames_host)[first * fb:(first + n) * fb]), dtype=torch.uint8)
+        self.frames[first * fb:(first + n) * fb].copy_(host)
+        sz = [int(v) for v in self.tparams.img_sample_sz]
+        C = fr[0].shape[2]
+        patches = torch.empty(n, C, sz[0], sz[1], dtype=torch.float32, device=self.dev)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        rc = lib.mmt_dimp_track_sample(ctypes.c_void_p(self.state_ptr(first)),
+                                       ctypes.c_void_p(self.frames.data_ptr() + first * fb), n,
+                                       ctypes.byref(self.tparams), sz[0], sz[1], ctypes.c_void_p(patches.data_ptr()),
+                                       stream)
+        if rc != 0:
+            raise RuntimeError(f"mmt_dimp_track_sample failed ({rc})")
+        test_x = net.extract_classification_feat(net.extract_backbone(patches))
+        from .dimp import apply_filter
+        scores = apply_filter(test_x.unsqueeze(0), torch.cat([t.target_filter for t in trackers]))[0].contiguous()
+        F_ = test_x[0].numel()
+        rc = lib.mmt_dimp_track_update(ctypes.c_void_p(self.state_ptr(first)), n, ctypes.c_void_p(scores.data_ptr()),
+                                       scores.shape[-2], scores.shape[-1], ctypes.byref(self.tparams),
+                                       ctypes.c_void_p(test_x.data_ptr()), F_,
+                                       ctypes.c_void_p(self.memory[first].data_ptr()),
+                                       ctypes.c_void_p(self.results.data_ptr() + first * self.rbytes), stream)
+        if rc != 0:
+            raise RuntimeError(f"mmt_dimp_track_update failed ({rc})")
+        self.res_host[first * self.rbytes:(first + n) * self.rbytes].copy_(
+            self.results[first * self.rbytes:(first + n) * self.rbytes], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev, fr
+
+    def finish(self, trackers, first, ev):
+        """Wait for the records, launch the filter updates they ask for, return the per-tracker outputs."""
+        ev.synchronize()
+        outs = []
+        for i, t in enumerate(trackers):
+            res = self.result(first + i)
+            t._update_filter(res)
+            outs.append(t._output(res))
+        return outs
+
+
+def _slots(trackers):
+    pool = trackers[0].pool
+    first = trackers[0].slot
+    if any(t.pool is not pool for t in trackers) or [t.slot for t in trackers] != list(range(first, first + len(trackers))):
+        raise ValueError("track_batch needs trackers of one DimpPool in consecutive slots")
+    return pool, first
 
 
 def track_batch(trackers, frames):
-    """One frame for each of several DiMP trackers sharing one DiMPNet: the search patches are sampled
-    into one batch, the two backbones + clf features run once over it, every sequence's filter is applied
-    in one grouped launch (apply_filter with S = len(trackers)), then each tracker localises and updates
-    on its own (the reference runs one tracker per process, test_rgbt_mgpus.py:178-186).  Returns the
-    per-tracker outputs of DiMP.track."""
-    net = trackers[0].net
-    n = len(trackers)
-    if any(t.net is not net for t in trackers):
-        raise ValueError("track_batch needs trackers that share one DiMPNet")
-    sz = trackers[0].img_sample_sz.long().tolist()
-    patches = torch.empty(n, 6, sz[0], sz[1], dtype=torch.float32, device=net.dev)
-    coords = [t.track_sample(f, out=patches[i])[1] for i, (t, f) in enumerate(zip(trackers, frames))]
-    test_x = net.extract_classification_feat(net.extract_backbone(patches))
-    filters = torch.cat([t.target_filter for t in trackers])
-    from .dimp import apply_filter
-    scores = apply_filter(test_x.unsqueeze(0), filters)[0].cpu()          # [n, 19, 19]
-    return [t.track_update(test_x[i:i + 1], scores[i:i + 1], c) for i, (t, c) in enumerate(zip(trackers, coords))]
+    """One frame for each of several DiMP trackers of one DimpPool (consecutive slots): the search patches
+    are sampled into one batch from the device state, the two backbones + clf features run once over it, every
+    sequence's filter is applied in one grouped launch, the device state machine advances every sequence, and
+    the filter updates the result records ask for follow (the reference runs one tracker per process,
+    test_rgbt_mgpus.py:178-186).  Returns the per-tracker outputs of DiMP.track."""
+    runs, i = [], 0   # runs of trackers in consecutive slots of one pool, each one batch
+    while i < len(trackers):
+        j = i + 1
+        while j < len(trackers) and trackers[j].pool is trackers[i].pool and trackers[j].slot == trackers[j - 1].slot + 1:
+            j += 1
+        runs.append((i, j))
+        i = j
+    launched = [(a, b, trackers[a].pool.launch(trackers[a:b], frames[a:b], trackers[a].slot)) for a, b in runs]
+    outs = []
+    for a, b, (ev, _fr) in launched:
+        outs.extend(trackers[a].pool.finish(trackers[a:b], trackers[a].slot, ev))
+    return outs
 
 
 class PipelinedBatch:
     """track_batch with the host half of one group of sequences overlapped with the device half of the other:
-    the trackers are split into two groups; group g's frame k is sampled and its network launched
-    (asynchronously, its scores copied to pinned host memory behind an event) while the host localises and
-    updates group 1 - g from frame k - 1.  Per-sequence results are identical to track_batch (each tracker
-    still sees its frames in order; only the interleaving of different sequences' host work changes)."""
+    the trackers are split into two groups; group g's frame k is launched (asynchronously, its result records
+    copied to pinned host memory behind an event) while the host reads group 1 - g's records of frame k - 1
+    and launches the filter updates they ask for.  Per-sequence results are identical to track_batch (each
+    tracker still sees its frames in order; only the interleaving of different sequences' work changes)."""
 
     def __init__(self, trackers, groups=2):
         self.trackers = trackers
@@ -482,29 +493,22 @@ class PipelinedBatch:
         bounds = [round(i * n / groups) for i in range(groups + 1)]
         self.groups = [list(range(bounds[i], bounds[i + 1])) for i in range(groups) if bounds[i + 1] > bounds[i]]
         self.pending = [None] * len(self.groups)
+        _slots(trackers)
 
     def _start(self, g, frames):
         idx = self.groups[g]
         trs = [self.trackers[i] for i in idx]
-        net = trs[0].net
-        sz = trs[0].img_sample_sz.long().tolist()
-        patches = torch.empty(len(idx), 6, sz[0], sz[1], dtype=torch.float32, device=net.dev)
-        coords = [t.track_sample(frames[i], out=patches[j])[1] for j, (i, t) in enumerate(zip(idx, trs))]
-        test_x = net.extract_classification_feat(net.extract_backbone(patches))
-        from .dimp import apply_filter
-        scores = apply_filter(test_x.unsqueeze(0), torch.cat([t.target_filter for t in trs]))[0]
-        host = torch.empty(scores.shape, dtype=torch.float32, pin_memory=True)
-        host.copy_(scores, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.pending[g] = (idx, test_x, host, ev, coords)
+        pool, first = _slots(trs)
+        ev, fr = pool.launch(trs, [frames[i] for i in idx], first)
+        self.pending[g] = (idx, ev, fr)
 
     def _finish(self, g, outs):
-        idx, test_x, host, ev, coords = self.pending[g]
+        idx, ev, _fr = self.pending[g]
         self.pending[g] = None
-        ev.synchronize()
-        for j, i in enumerate(idx):
-            outs[i] = self.trackers[i].track_update(test_x[j:j + 1], host[j:j + 1], coords[j])
+        trs = [self.trackers[i] for i in idx]
+        pool, first = _slots(trs)
+        for i, o in zip(idx, pool.finish(trs, first, ev)):
+            outs[i] = o
 
     def step(self, frames):
         """Submit frame k for every sequence; returns the outputs of frame k - 1 (None on the first call)."""
@@ -524,4 +528,4 @@ class PipelinedBatch:
         return outs
 
 
-__all__ = ["DiMP", "parameters", "TrackerParams", "track_batch", "PipelinedBatch"]
+__all__ = ["DiMP", "DimpPool", "parameters", "TrackerParams", "track_batch", "PipelinedBatch"]

@@ -29,3 +29,13 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_without_gpu():
     assert _lib.load().mmt_version().startswith(b"mmtrack-mi355x")
+
+
+def test_dimp_state_layout_matches_binding():
+    """The device DiMP tracker state / record structs of include/mmtrack.h and the ctypes binding agree in size
+    (the library reports sizeof(mmt_dimp_state); no GPU needed)."""
+    import ctypes
+    from mmtrack_amd import _lib
+    lib = _lib.load()
+    assert lib.mmt_dimp_state_bytes() == ctypes.sizeof(_lib.MmtDimpState)
+    assert _lib.MmtDimpState.target_boxes.offset % 16 == 0 or _lib.MmtDimpState.target_boxes.offset % 4 == 0

@@ -264,13 +264,14 @@ def test_pipelined_batch_equals_sequential():
     """PipelinedBatch (two groups, host updates overlapped with the other group's network) gives every
     sequence exactly the results of tracking it alone with DiMP.track."""
     from mmtrack_amd import synth
-    from mmtrack_amd.dimp_tracker import DiMP, PipelinedBatch, parameters
+    from mmtrack_amd.dimp_tracker import DiMP, DimpPool, PipelinedBatch, parameters
     from mmtrack_amd.dimpnet import DiMPNet
     net = DiMPNet(synth.make_dimp_state_dict(0))
     seqs = [synth.make_frames(70 + i, 6, 360, 480, 6, box=(150.0 + 20 * i, 120.0, 44.0, 36.0)) for i in range(3)]
+    pool = DimpPool(net, 3, parameters())
 
-    def fresh(i):
-        t = DiMP(parameters(), net=net)
+    def fresh(i, batched=False):
+        t = DiMP(parameters(), net=net, pool=pool if batched else None)
         torch.manual_seed(100 + i)
         t.initialize(seqs[i][0][0], {"init_bbox": list(seqs[i][1][0])})
         return t
@@ -278,7 +279,7 @@ def test_pipelined_batch_equals_sequential():
     for i in range(3):
         t = fresh(i)
         ref.append([t.track(seqs[i][0][k])["target_bbox"] for k in range(1, 6)])
-    trs = [fresh(i) for i in range(3)]
+    trs = [fresh(i, batched=True) for i in range(3)]
     pipe = PipelinedBatch(trs)
     got = [[] for _ in range(3)]
     for k in range(1, 6):
