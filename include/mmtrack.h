@@ -281,7 +281,7 @@ typedef struct mmt_dimp_track_params {
   double target_not_found_threshold, uncertain_threshold, hard_sample_threshold;   /* -inf: unset        */
   double distractor_threshold, hard_negative_threshold, target_neighborhood_scale, dispalcement_scale;
   double target_inside_ratio, low_score_opt_threshold;                             /* NaN: unset         */
-  float learning_rate, hard_negative_learning_rate, init_samples_minimum_weight;
+  double learning_rate, hard_negative_learning_rate, init_samples_minimum_weight;   /* Python floats */
   int sample_memory_size, train_sample_interval, train_skipping;
   int net_opt_update_iter, net_opt_hn_iter, net_opt_low_iter, update_classifier;
 } mmt_dimp_track_params;

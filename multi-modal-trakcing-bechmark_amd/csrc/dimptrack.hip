@@ -159,12 +159,12 @@ __device__ void max2d(const float* m, int h, int w, float* red_v, int* red_i, fl
 }
 
 // update_sample_weights (dimp.py:585-607) on sw[kMem]; returns the replaced index
-__device__ int update_sample_weights(float* sw, int num_samp, int num_init, int prev_ind, float lr,
+__device__ int update_sample_weights(float* sw, int num_samp, int num_init, int prev_ind, double lr,
                                      const mmt_dimp_track_params& p) {
   const bool init_w = p.init_samples_minimum_weight != 0;   // 0 -> None
   const int s_ind = init_w ? num_init : 0;
   int r_ind;
-  if (num_samp == 0 || lr == 1.0f) {
+  if (num_samp == 0 || lr == 1.0) {
     for (int k = 0; k < kMem; ++k) sw[k] = 0.f;
     sw[0] = 1.f;
     r_ind = 0;
@@ -176,10 +176,10 @@ __device__ int update_sample_weights(float* sw, int num_samp, int num_init, int 
       for (int k = s_ind + 1; k < kMem; ++k)
         if (sw[k] < sw[r_ind]) r_ind = k;   // torch.min: first minimal index
     }
-    const float den = pyf(1.0 - (double)lr);
+    const float den = pyf(1.0 - lr);
     if (prev_ind < 0) {
       for (int k = 0; k < kMem; ++k) sw[k] = sw[k] / den;
-      sw[r_ind] = lr;
+      sw[r_ind] = pyf(lr);
     } else {
       sw[r_ind] = sw[prev_ind] / den;
     }
@@ -190,10 +190,10 @@ __device__ int update_sample_weights(float* sw, int num_samp, int num_init, int 
   if (init_w) {
     float init_sum = 0.f;
     for (int k = 0; k < num_init; ++k) init_sum += sw[k];
-    if (init_sum < p.init_samples_minimum_weight) {
+    if ((double)init_sum < p.init_samples_minimum_weight) {
       float rest = 0.f;
       for (int k = num_init; k < kMem; ++k) rest += sw[k];
-      const float d = p.init_samples_minimum_weight + rest;
+      const float d = pyf(p.init_samples_minimum_weight) + rest;
       for (int k = 0; k < kMem; ++k) sw[k] = sw[k] / d;
       const float v = pyf((double)p.init_samples_minimum_weight / num_init);
       for (int k = 0; k < num_init; ++k) sw[k] = v;
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void dimp_localize_kernel(mmt_dimp_state* stat
     tb[1] = c[0] - (bs[0] - 1.0f) / 2.0f;
     tb[2] = bs[1];
     tb[3] = bs[0];
-    const float lr = hard ? p.hard_negative_learning_rate : p.learning_rate;
+    const double lr = hard ? p.hard_negative_learning_rate : p.learning_rate;
     if (hard || st.frame_num % p.train_sample_interval == 0) {
       const int r = update_sample_weights(st.sample_weights, st.num_stored, st.num_init, st.prev_replace, lr, p);
       st.prev_replace = r;

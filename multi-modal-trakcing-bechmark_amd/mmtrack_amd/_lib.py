@@ -90,8 +90,8 @@ class MmtDimpTrackParams(ctypes.Structure):
         ("hard_sample_threshold", ctypes.c_double), ("distractor_threshold", ctypes.c_double),
         ("hard_negative_threshold", ctypes.c_double), ("target_neighborhood_scale", ctypes.c_double),
         ("dispalcement_scale", ctypes.c_double), ("target_inside_ratio", ctypes.c_double),
-        ("low_score_opt_threshold", ctypes.c_double), ("learning_rate", ctypes.c_float),
-        ("hard_negative_learning_rate", ctypes.c_float), ("init_samples_minimum_weight", ctypes.c_float),
+        ("low_score_opt_threshold", ctypes.c_double), ("learning_rate", ctypes.c_double),
+        ("hard_negative_learning_rate", ctypes.c_double), ("init_samples_minimum_weight", ctypes.c_double),
         ("sample_memory_size", ctypes.c_int), ("train_sample_interval", ctypes.c_int), ("train_skipping", ctypes.c_int),
         ("net_opt_update_iter", ctypes.c_int), ("net_opt_hn_iter", ctypes.c_int), ("net_opt_low_iter", ctypes.c_int),
         ("update_classifier", ctypes.c_int),
