@@ -232,6 +232,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="per CPU-baseline sample (4 samples)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry", action="store_true", help="no GPU: sleep for the step (tests the multi-rank plumbing)")
+    ap.add_argument("--dimp-groups", type=int, default=1, help="mfdimp: PipelinedBatch groups of sequences")
     ap.add_argument("--dimp-precision", default="f16x3", choices=("f16x3", "fp32"),
                     help="mfdimp_rgbt: ResNet-50 convs on fp32-faithful f16x3 split products (default) or fp32 MFMA")
     args = ap.parse_args()
@@ -376,11 +377,13 @@ def dimp_main(args, rank, world, dist):
     torch.cuda.synchronize()
 
     from mmtrack_amd.dimp_tracker import PipelinedBatch
-    pipe = PipelinedBatch(trackers) if not args.sync else None
+    pipe = PipelinedBatch(trackers, groups=args.dimp_groups) if not args.sync else None
 
     def run(k0, n):
         """n frames of every sequence, all results on the host before returning (--sync: track_batch per
-        frame; default: two groups of sequences pipelined, host updates of one under the other's network)."""
+        frame; default: PipelinedBatch over --dimp-groups groups of sequences -- with 2, the host updates of
+        one group run under the other's network; 1, the whole batch per launch, is faster on MI355X since the
+        grouped split-K convs want the larger M)."""
         for k in range(k0, k0 + n):
             frames = [video[1 + k % args.frames]] * B
             if pipe is None:

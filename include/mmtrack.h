@@ -192,6 +192,29 @@ int mmt_conv2d_f16x3(const float* x, int N, int H, int W, int Cin, const uint16_
                      float w_scale, int Kp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
                      const float* resid, float* y, const float* x_max, float x_scale, float* y_max, int flags,
                      void* hip_stream);
+/* one convolution of a grouped f16x3 launch: the operands of mmt_conv2d_f16x3 for one of the two backbones'
+ * twin layers (the same shape, their own weights, input, output and max words)                        */
+typedef struct mmt_conv_group {
+  const float* x;
+  const uint16_t* w_hi;
+  const uint16_t* w_lo;
+  float w_scale;
+  const float* bias;
+  const float* resid;
+  float* y;
+  const float* x_max;
+  float x_scale;
+  float* y_max;
+  int flags;
+} mmt_conv_group;
+/* the groups (1 or 2, disjoint outputs, no MAX merge when 2) in one launch; when the output tiles of the launch
+ * are too few to fill the GPU, K is split in slices whose fp32 partials go to ws and are summed in slice order
+ * by a second kernel that applies the epilogue (ws_bytes < mmt_conv2d_f16x3_ws_bytes(): no split)        */
+size_t mmt_conv2d_f16x3_ws_bytes(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pad,
+                                 int groups);
+int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int n_groups, int N, int H, int W, int Cin, int Kp,
+                            int Cout, int kh, int kw, int stride, int pad, void* ws, size_t ws_bytes,
+                            void* hip_stream);
 /* nn.MaxPool2d(k, stride, pad) over NHWC                                                           */
 int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y,
                       void* hip_stream);
@@ -199,9 +222,11 @@ int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int str
  * -> ((v / 255) - mean) / std as NHWC [N][H][W][3] per 3-channel half (out_b: the aux half)       */
 int mmt_image_normalize(const float* im, int N, int C, int H, int W, const float mean[3], const float std_[3],
                         float* out_a, float* out_b, void* hip_stream);
-/* InstanceL2Norm(size_average, eps, scale) (normalization.py:6-21) of NHWC x; y_nhwc / y_nchw may be NULL */
+/* InstanceL2Norm(size_average, eps, scale) (normalization.py:6-21) of NHWC x; y_nhwc / y_nchw may be NULL;
+ * ws: device scratch of mmt_instance_l2norm_ws_bytes(N, H, W) (per-chunk sums); C % 4 == 0, C <= 1024   */
+size_t mmt_instance_l2norm_ws_bytes(int N, int H, int W);
 int mmt_instance_l2norm(const float* x, int N, int H, int W, int C, float scale, float eps, float* y_nhwc,
-                        float* y_nchw, void* hip_stream);
+                        float* y_nchw, float* ws, void* hip_stream);
 /* PrRoIPool2D(PH, PW, spatial_scale) (ltr/external/PreciseRoIPooling), roi n on image n:
  * feat NHWC, rois device [N][4] = x0, y0, x1, y1 (image coordinates) -> out [N][C][PH][PW]          */
 int mmt_prroi_pool(const float* feat, int N, int H, int W, int C, const float* rois, float spatial_scale, int PH,
@@ -301,11 +326,19 @@ int mmt_dimp_track_sample(mmt_dimp_state* states, const mmt_dimp_frame* frames, 
 int mmt_dimp_track_update(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
                           const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
                           mmt_dimp_result* results, void* hip_stream);
-/* mmt_dimp_optimize with the boxes [I][S][4] and sample weights [I][S] (or NULL) in device memory: no host
- * staging and no synchronisation (losses are not returned)                                                  */
-int mmt_dimp_optimize_dev(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
-                          const float* bb_dev, const float* sample_weight_dev, const mmt_dimp_params* p, int num_iter,
-                          void* workspace, size_t ws_bytes, void* hip_stream);
+/* mmt_dimp_optimize with the boxes and sample weights (or NULL) in device memory: no host staging and no
+ * synchronisation (losses are not returned).  Strides in floats, 0 = the contiguous [I][S] layout: sample i
+ * of sequence s is feat + i * feat_img_stride + s * feat_seq_stride ([C][H][W]), its box bb_dev + i *
+ * bb_img_stride + s * bb_seq_stride (4 floats), its weight sample_weight_dev[i * sw_img_stride + s * sw_seq_stride] --
+ * so S sequences' memories in a pool of device states ([slot][MMT_DIMP_MEMORY] samples, mmt_dimp_state's
+ * target_boxes / sample_weights) are optimised in one call, their filters weights [S][C][fh][fw].  Samples
+ * with weight 0 contribute exact zeros: sequences with fewer stored samples than I give the same filter as
+ * a call over their own samples.                                                                           */
+int mmt_dimp_optimize_dev(const float* feat, int64_t feat_img_stride, int64_t feat_seq_stride, int I, int S, int C,
+                          int H, int W, float* weights, int fh, int fw, const float* bb_dev, int64_t bb_img_stride,
+                          int64_t bb_seq_stride, const float* sample_weight_dev, int64_t sw_img_stride,
+                          int64_t sw_seq_stride, const mmt_dimp_params* p, int num_iter, void* workspace,
+                          size_t ws_bytes, void* hip_stream);
 
 /* ---- operator-level entry points (device pointers; used by the parity tests and by hosts that
  *      compose their own pipelines).  epi: 0 bias->bf16, 1 bias+GELU->bf16, 2 C(f32) = R + acc + bias,

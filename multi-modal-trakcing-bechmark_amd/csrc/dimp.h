@@ -16,7 +16,8 @@ struct DimpMaps {                 // label / target-mask / sample-weight maps fr
   float* label; float* mask; float* sw;                                 // [IS][Ho][Wo]
 };
 struct DimpFilter {
-  const float* feat;              // [I][S][C][H][W]
+  const float* feat;              // [I][S][C][H][W]: sample (i, s) at feat + i * img_stride + s * seq_stride
+  int64_t img_stride, seq_stride; // floats
   const float* w;                 // [S][C][fh][fw]
   int I, S, C, H, W, fh, fw, Ho, Wo;
   int mode;                       // 0: scores, 1: residual step (out = mapped residual), 2: |J g|^2 partials
@@ -27,6 +28,7 @@ struct DimpFilter {
 };
 struct DimpTranspose {
   const float* feat; const float* r;   // r: [I][S][Ho][Wo]
+  int64_t img_stride, seq_stride;      // of feat, as DimpFilter
   const float* w; float reg;           // optional: grad += reg * w
   int I, S, C, H, W, fh, fw, Ho, Wo;
   float* grad;                         // [S][C][fh][fw]
@@ -41,8 +43,9 @@ struct DimpUpdate {
 // optimizer.py:108-125's per-sample constants, formed on the device: centers [IS][2] = ((y + h / 2) / stride - off0,
 // (x + w / 2) / stride - off1) of bb [IS][4] (x, y, w, h), sqrtsw [IS] = sqrt(sample_weight) (null: 1 / I)
 struct DimpPrep {
-  const float* bb; const float* sw;   // device
-  int IS, I;
+  const float* bb; const float* sw;   // device; sample (i, s) at bb + i * bb_i + s * bb_s, sw + i * sw_i + s * sw_s (floats)
+  int64_t bb_i, bb_s, sw_i, sw_s;
+  int IS, I, S;
   float feat_stride, off0, off1;
   float* centers; float* sqrtsw;
 };

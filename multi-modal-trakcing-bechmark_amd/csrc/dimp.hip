@@ -35,9 +35,16 @@ __global__ __launch_bounds__(256) void dimp_maps_kernel(DimpMaps m) {
 // One workgroup per (image * sequence, tile of kDimpPosPerBlock output positions): the 8 wave halves
 // (32 lanes each) take interleaved channel slices (c = group + 8 k) of the same 32 positions, so a frame's
 // 15-50 samples still spread over hundreds of workgroups; the 8 partial sums combine in a fixed order.
+// FH / FW > 0: the filter size as compile-time constants (the taps unroll, so a channel's loads are all in
+// flight together; the same summation order as the generic loop)
+template <int FH, int FW>
 __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   extern __shared__ float wsh[];
   __shared__ float part[8][kDimpPosPerBlock];
+  if constexpr (FH > 0) {
+    a.fh = FH;
+    a.fw = FW;
+  }
   const int is = blockIdx.x;                  // image * S + sequence
   const int s = is % a.S;
   const int T = a.fh * a.fw;
@@ -50,14 +57,17 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   if (p < n) {
     const int y = p / a.Wo, x = p - y * a.Wo;
     const int P0 = a.fh / 2, P1 = a.fw / 2;
-    const float* f = a.feat + (int64_t)is * a.C * a.H * a.W;
+    const float* f = a.feat + (int64_t)(is / a.S) * a.img_stride + (int64_t)s * a.seq_stride;
+#pragma unroll 4
     for (int c = cg; c < a.C; c += 8) {
       const float* fc = f + (int64_t)c * a.H * a.W;
       const float* wc = wsh + c * T;
-      for (int ky = 0; ky < a.fh; ++ky) {
+#pragma unroll
+      for (int ky = 0; ky < (FH > 0 ? FH : a.fh); ++ky) {
         const int yy = y + ky - P0;
         if (yy < 0 || yy >= a.H) continue;
-        for (int kx = 0; kx < a.fw; ++kx) {
+#pragma unroll
+        for (int kx = 0; kx < (FW > 0 ? FW : a.fw); ++kx) {
           const int xx = x + kx - P1;
           if (xx < 0 || xx >= a.W) continue;
           acc += fc[yy * a.W + xx] * wc[ky * a.fw + kx];
@@ -113,7 +123,7 @@ __global__ __launch_bounds__(256) void dimp_transpose_kernel(DimpTranspose a) {
     const int i = q / n, p = q - i * n;
     const int y = p / a.Wo, x = p - y * a.Wo;
     const float r = a.r[((int64_t)i * a.S + s) * n + p];
-    const float* fc = a.feat + (((int64_t)i * a.S + s) * a.C + c) * a.H * a.W;
+    const float* fc = a.feat + (int64_t)i * a.img_stride + (int64_t)s * a.seq_stride + (int64_t)c * a.H * a.W;
 #pragma unroll
     for (int t = 0; t < MAXT; ++t) {
       if (t >= T) break;
@@ -204,10 +214,11 @@ __global__ __launch_bounds__(256) void dimp_loss_kernel(const float* rsq, int np
 __global__ __launch_bounds__(256) void dimp_prep_kernel(DimpPrep a) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= a.IS) return;
-  const float* b = a.bb + 4 * k;
+  const int i = k / a.S, sq = k - i * a.S;
+  const float* b = a.bb + i * a.bb_i + sq * a.bb_s;
   a.centers[2 * k] = (b[1] + b[3] / 2) / a.feat_stride - a.off0;       // flip((1,)) -> (y, x)
   a.centers[2 * k + 1] = (b[0] + b[2] / 2) / a.feat_stride - a.off1;
-  a.sqrtsw[k] = a.sw ? sqrtf(a.sw[k]) : (float)sqrt(1.0 / a.I);
+  a.sqrtsw[k] = a.sw ? sqrtf(a.sw[i * a.sw_i + sq * a.sw_s]) : (float)sqrt(1.0 / a.I);
 }
 __global__ __launch_bounds__(256) void dimp_prep_args_kernel(DimpPrepArgs a) {
   const int j = threadIdx.x;
@@ -236,7 +247,11 @@ void dimp_maps(const DimpMaps& m, hipStream_t s) {
 }
 void dimp_filter(const DimpFilter& a, hipStream_t s) {
   const int nby = (a.Ho * a.Wo + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
-  hipLaunchKernelGGL(dimp_filter_kernel, dim3(a.I * a.S, nby), dim3(256), a.C * a.fh * a.fw * sizeof(float), s, a);
+  const size_t lds = a.C * a.fh * a.fw * sizeof(float);
+  if (a.fh == 4 && a.fw == 4)
+    hipLaunchKernelGGL((dimp_filter_kernel<4, 4>), dim3(a.I * a.S, nby), dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((dimp_filter_kernel<0, 0>), dim3(a.I * a.S, nby), dim3(256), lds, s, a);
 }
 void dimp_transpose(const DimpTranspose& a, hipStream_t s) {
   hipLaunchKernelGGL(dimp_transpose_kernel, dim3(a.S * a.C), dim3(256), 0, s, a);

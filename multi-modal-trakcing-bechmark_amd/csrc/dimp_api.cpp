@@ -65,6 +65,8 @@ int mmt_dimp_apply_filter(const float* feat, const float* w, float* scores, int 
   a.feat = feat;
   a.w = w;
   a.I = I; a.S = S; a.C = C; a.H = H; a.W = W; a.fh = fh; a.fw = fw;
+  a.seq_stride = (int64_t)C * H * W;
+  a.img_stride = S * a.seq_stride;
   a.Ho = H + 2 * (fh / 2) - fh + 1;
   a.Wo = W + 2 * (fw / 2) - fw + 1;
   a.mode = 0;
@@ -80,6 +82,8 @@ int mmt_dimp_feat_transpose(const float* feat, const float* r, float* grad, int 
   a.feat = feat;
   a.r = r;
   a.I = I; a.S = S; a.C = C; a.H = H; a.W = W; a.fh = fh; a.fw = fw;
+  a.seq_stride = (int64_t)C * H * W;
+  a.img_stride = S * a.seq_stride;
   a.Ho = H + 2 * (fh / 2) - fh + 1;
   a.Wo = W + 2 * (fw / 2) - fw + 1;
   a.grad = grad;
@@ -88,9 +92,9 @@ int mmt_dimp_feat_transpose(const float* feat, const float* r, float* grad, int 
 }
 
 // the Gauss-Newton loop of mmt_dimp_optimize / _dev once the per-sample constants are in the workspace
-static int optimize_body(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
-                         const mmt_dimp_params* p, int num_iter, char* ws, const WsLayout& L, float* losses,
-                         hipStream_t st) {
+static int optimize_body(const float* feat, int64_t img_stride, int64_t seq_stride, int I, int S, int C, int H, int W,
+                         float* weights, int fh, int fw, const mmt_dimp_params* p, int num_iter, char* ws,
+                         const WsLayout& L, float* losses, hipStream_t st) {
   auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
   const int IS = I * S;
   const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, nby = (Ho * Wo + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
@@ -103,6 +107,8 @@ static int optimize_body(const float* feat, int I, int S, int C, int H, int W, f
 
   DimpFilter fa{};
   fa.feat = feat;
+  fa.img_stride = img_stride;
+  fa.seq_stride = seq_stride;
   fa.I = I; fa.S = S; fa.C = C; fa.H = H; fa.W = W; fa.fh = fh; fa.fw = fw; fa.Ho = Ho; fa.Wo = Wo;
   fa.label = F(L.label);
   fa.mask = F(L.mask);
@@ -110,6 +116,8 @@ static int optimize_body(const float* feat, int I, int S, int C, int H, int W, f
   fa.smask = F(L.smask);
   DimpTranspose ta{};
   ta.feat = feat;
+  ta.img_stride = img_stride;
+  ta.seq_stride = seq_stride;
   ta.r = F(L.rm);
   ta.w = weights;
   ta.reg = reg;
@@ -183,22 +191,34 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
   std::memcpy(pr.v + 256, p->spatial_w, 128 * 4);
   pr.dst = F(L.params);
   dimp_params(pr, st);
-  return optimize_body(feat, I, S, C, H, W, weights, fh, fw, p, num_iter, ws, L, losses, st);
+  const int64_t chw = (int64_t)C * H * W;
+  return optimize_body(feat, S * chw, chw, I, S, C, H, W, weights, fh, fw, p, num_iter, ws, L, losses, st);
 }
 
-int mmt_dimp_optimize_dev(const float* feat, int I, int S, int C, int H, int W, float* weights, int fh, int fw,
-                          const float* bb_dev, const float* sample_weight_dev, const mmt_dimp_params* p, int num_iter,
-                          void* workspace, size_t ws_bytes, void* stream_) {
+int mmt_dimp_optimize_dev(const float* feat, int64_t feat_img_stride, int64_t feat_seq_stride, int I, int S, int C,
+                          int H, int W, float* weights, int fh, int fw, const float* bb_dev, int64_t bb_img_stride,
+                          int64_t bb_seq_stride, const float* sample_weight_dev, int64_t sw_img_stride,
+                          int64_t sw_seq_stride, const mmt_dimp_params* p, int num_iter, void* workspace,
+                          size_t ws_bytes, void* stream_) {
   if (!feat || !weights || !bb_dev || !p || !workspace || num_iter < 0 || bad_dims(I, S, C, H, W, fh, fw) ||
-      p->num_dist_bins <= 0 || p->num_dist_bins > 128)
+      p->num_dist_bins <= 0 || p->num_dist_bins > 128 || feat_img_stride < 0 || feat_seq_stride < 0 ||
+      bb_img_stride < 0 || bb_seq_stride < 0 || sw_img_stride < 0 || sw_seq_stride < 0)
     return MMT_E_ARG;
   const WsLayout L = layout(I, S, C, H, W, fh, fw, num_iter);
   if (ws_bytes < L.total) return MMT_E_ARG;
   hipStream_t st = (hipStream_t)stream_;
   char* ws = static_cast<char*>(workspace);
   auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
-  DimpPrep pp{bb_dev, sample_weight_dev, I * S, I, p->feat_stride, (float)(fh % 2) / 2.0f, (float)(fw % 2) / 2.0f,
-              F(L.centers), F(L.sqrtsw)};
+  const int64_t chw = (int64_t)C * H * W;
+  // strides 0: the contiguous [I][S] layouts
+  if (!feat_seq_stride) feat_seq_stride = chw;
+  if (!feat_img_stride) feat_img_stride = S * feat_seq_stride;
+  if (!bb_seq_stride) bb_seq_stride = 4;
+  if (!bb_img_stride) bb_img_stride = S * bb_seq_stride;
+  if (!sw_seq_stride) sw_seq_stride = 1;
+  if (!sw_img_stride) sw_img_stride = S * sw_seq_stride;
+  DimpPrep pp{bb_dev, sample_weight_dev, bb_img_stride, bb_seq_stride, sw_img_stride, sw_seq_stride, I * S, I, S,
+              p->feat_stride, (float)(fh % 2) / 2.0f, (float)(fw % 2) / 2.0f, F(L.centers), F(L.sqrtsw)};
   dimp_prep(pp, st);
   DimpParamArgs pr{};
   std::memcpy(pr.v, p->label_w, 128 * 4);
@@ -206,7 +226,8 @@ int mmt_dimp_optimize_dev(const float* feat, int I, int S, int C, int H, int W, 
   std::memcpy(pr.v + 256, p->spatial_w, 128 * 4);
   pr.dst = F(L.params);
   dimp_params(pr, st);
-  return optimize_body(feat, I, S, C, H, W, weights, fh, fw, p, num_iter, ws, L, nullptr, st);
+  return optimize_body(feat, feat_img_stride, feat_seq_stride, I, S, C, H, W, weights, fh, fw, p, num_iter, ws, L,
+                       nullptr, st);
 }
 
 }  // extern "C"

@@ -31,8 +31,9 @@
 namespace mmt {
 
 constexpr int kMaxShards = 64, kShardStride = 32;   // sharded max words: 64 x 128-B lines per tensor
+constexpr int kMaxGroups = 2, kMaxSplitK = 8;
 
-struct ConvF16Args {
+struct ConvGroupArgs {            // one convolution of a grouped launch (the RGB / aux backbones' twin layers)
   const float* x;                 // [N][H][W][Cin] fp32
   const uint16_t* wh;             // [Cout][Kp] fp16 halves of w * s_w
   const uint16_t* wl;
@@ -40,10 +41,16 @@ struct ConvF16Args {
   const float* resid;             // [M][Cout] or null
   float* y;                       // [M][Cout]
   const float* xmax;              // sharded max|x| words of the input, or null: xscale
-  float xscale;                   // static input scale (power of two) when xmax is null
   float* ymax;                    // sharded max|y| words of the output (accumulated), or null
+  float xscale;                   // static input scale (power of two) when xmax is null
   float inv_w;                    // 1 / s_w
-  int N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, Kp, flags;
+  int flags;
+};
+
+struct ConvF16Args {
+  ConvGroupArgs g[kMaxGroups];
+  float* part;                    // split-K partials [ks][G][M][Cout] (ks > 1)
+  int N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, Kp, ks;
 };
 
 __device__ __forceinline__ int cswz(int r, int c) { return r * 32 + ((c ^ ((r >> 2) & 2)) << 3); }   // gemm.hip swzk<32>
@@ -55,50 +62,94 @@ __device__ __forceinline__ float pow2_scale(float m) {   // 2^(14 - ceil(log2 m)
   return ldexpf(1.0f, 14 - c);
 }
 
+__device__ __forceinline__ ConvGroupArgs pick_group(const ConvF16Args& a, int grp) {
+  return grp ? a.g[1] : a.g[0];   // a select, not a dynamic index (which would copy the arguments to scratch)
+}
+
+// the epilogue arithmetic shared by the one-pass and the split-K paths: v (= acc / (s_w s_a)) + bias (+ residual),
+// ReLU, the backbones' running max; returns the stored value
+__device__ __forceinline__ f32x4 conv_out(const ConvGroupArgs& g, f32x4 v, int64_t mo, int no, int Cout) {
+  if (g.bias) {
+    const float4 b = *reinterpret_cast<const float4*>(g.bias + no);
+    v += f32x4{b.x, b.y, b.z, b.w};
+  }
+  if (g.resid) {
+    const float4 r = *reinterpret_cast<const float4*>(g.resid + mo * Cout + no);
+    v += f32x4{r.x, r.y, r.z, r.w};
+  }
+  if (g.flags & MMT_CONV_RELU)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+  float4* dst = reinterpret_cast<float4*>(g.y + mo * Cout + no);
+  if (g.flags & MMT_CONV_MAX) {
+    const float4 o = *dst;   // torch.max(color, depth) (dimpnet.py:103)
+    v = f32x4{fmaxf(o.x, v[0]), fmaxf(o.y, v[1]), fmaxf(o.z, v[2]), fmaxf(o.w, v[3])};
+  }
+  *dst = make_float4(v[0], v[1], v[2], v[3]);
+  return v;
+}
+
+__device__ __forceinline__ void fold_max(float* ymax, float ymx, int shard) {
+  ymx = wave_max(ymx);
+  if ((threadIdx.x & 63) == 0 && ymx > 0.f)
+    __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(ymax) + (shard % kMaxShards) * kShardStride,
+                           __float_as_uint(ymx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one K-tile's global operands in flight: 8 activations (fp32, split on the way into the LDS) and 8 fp16 halves
+// of each weight image; two named sets (no array, so nothing is indexed at run time and nothing goes to scratch)
+struct ConvRegs {
+  float4 a0, a1;
+  uint4 wh, wl;
+};
+
+// grid (ceil(M / 128), Cout / BN, G * ks): blockIdx.z = group * ks + K slice
 template <int BN, bool STEM>
-__global__ __launch_bounds__(512) void conv_f16x3_kernel(const ConvF16Args a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_f16x3_kernel(const ConvF16Args a) {
   constexpr int BM = 128, BK = 32;
   constexpr int WN = BN / 2, FM = 2, FN = WN / 16;
   __shared__ __attribute__((aligned(16))) uint16_t sA[2][2][BM * BK];   // [stage][hi, lo]
   __shared__ __attribute__((aligned(16))) uint16_t sW[2][2][BN * BK];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  const int grp = blockIdx.z / a.ks, slice = blockIdx.z - grp * a.ks;
+  const ConvGroupArgs g = pick_group(a, grp);
   const int M = a.N * a.Ho * a.Wo;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
 
   // input scale: the maximum over the producer's 64 shard words (every wave forms it itself)
-  float sa = a.xscale;
-  if (a.xmax) {
-    const float mx = wave_max(a.xmax[lane * kShardStride]);
+  float sa = g.xscale;
+  if (g.xmax) {
+    const float mx = wave_max(g.xmax[lane * kShardStride]);
     sa = mx > 0.f ? pow2_scale(mx) : 1.0f;
   }
-  const float inv = a.inv_w / sa;
+  const float inv = g.inv_w / sa;
 
   // A load slot: row (pixel) t >> 2, K chunk t & 3 (8 values); W load slot: row t >> 2, chunk t & 3
   const int ar = t >> 2, ac = t & 3;
   const int m = m0 + ar;
   const bool mval = m < M;
   int iy0 = 0, ix0 = 0;
-  const float* xb = a.x;
+  const float* xb = g.x;
   if (mval) {
     const int nimg = m / (a.Ho * a.Wo);
     const int r = m - nimg * a.Ho * a.Wo;
     const int oy = r / a.Wo, ox = r - oy * a.Wo;
     iy0 = oy * a.stride - a.pad;
     ix0 = ox * a.stride - a.pad;
-    xb = a.x + (int64_t)nimg * a.H * a.W * a.Cin;
+    xb = g.x + (int64_t)nimg * a.H * a.W * a.Cin;
   }
   const bool wload = ar < BN;
-  const uint16_t* wrh = a.wh + (int64_t)(n0 + (wload ? ar : 0)) * a.Kp + ac * 8;
-  const uint16_t* wrl = a.wl + (int64_t)(n0 + (wload ? ar : 0)) * a.Kp + ac * 8;
+  const uint16_t* wrh = g.wh + (int64_t)(n0 + (wload ? ar : 0)) * a.Kp + ac * 8;
+  const uint16_t* wrl = g.wl + (int64_t)(n0 + (wload ? ar : 0)) * a.Kp + ac * 8;
   const int nk = a.Kp / BK;
+  const int kt0 = (int)((int64_t)slice * nk / a.ks), nt = (int)((int64_t)(slice + 1) * nk / a.ks) - kt0;
   const int cpt = STEM ? 1 : a.Cin / BK;   // K-tiles per tap
 
-  float4 ra[2][2];
-  uint4 rwh[2], rwl[2];
-  auto load = [&](int kt, int set) {
+  auto load = [&](int kt, ConvRegs& r) {
     if constexpr (STEM) {
       // taps 8 kt + 2 ac, + 1: three channels each (the fourth is the weights' zero pad)
+      float4 v[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int tap = kt * 8 + ac * 2 + h;
@@ -106,37 +157,42 @@ __global__ __launch_bounds__(512) void conv_f16x3_kernel(const ConvF16Args a) {
         const int iy = iy0 + ky, ix = ix0 + kx;
         const bool ok = mval && tap < a.kh * a.kw && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
         const float* src = xb + ((int64_t)iy * a.W + ix) * 3;
-        ra[set][h] = ok ? make_float4(src[0], src[1], src[2], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[h] = ok ? make_float4(src[0], src[1], src[2], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+      r.a0 = v[0];
+      r.a1 = v[1];
     } else {
       const int tap = kt / cpt, c0 = (kt - tap * cpt) * BK + ac * 8;
       const int ky = tap / a.kw, kx = tap - ky * a.kw;
       const int iy = iy0 + ky, ix = ix0 + kx;
       const bool ok = mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
       const float4* src = reinterpret_cast<const float4*>(xb + ((int64_t)iy * a.W + ix) * a.Cin + c0);
-      ra[set][0] = ok ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
-      ra[set][1] = ok ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      r.a0 = ok ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+      r.a1 = ok ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (wload) {
-      rwh[set] = *reinterpret_cast<const uint4*>(wrh + kt * BK);
-      rwl[set] = *reinterpret_cast<const uint4*>(wrl + kt * BK);
+      r.wh = *reinterpret_cast<const uint4*>(wrh + kt * BK);
+      r.wl = *reinterpret_cast<const uint4*>(wrl + kt * BK);
     }
   };
-  auto stash = [&](int set, int st) {
-    const float v[8] = {ra[set][0].x, ra[set][0].y, ra[set][0].z, ra[set][0].w,
-                        ra[set][1].x, ra[set][1].y, ra[set][1].z, ra[set][1].w};
-    uint16_t h[8], l[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) split_h(v[e] * sa, h[e], l[e]);
-    const uint4 hv = make_uint4(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16, h[4] | (uint32_t)h[5] << 16,
-                                h[6] | (uint32_t)h[7] << 16);
-    const uint4 lv = make_uint4(l[0] | (uint32_t)l[1] << 16, l[2] | (uint32_t)l[3] << 16, l[4] | (uint32_t)l[5] << 16,
-                                l[6] | (uint32_t)l[7] << 16);
+  auto pack2 = [&](float x, float y, uint32_t& h, uint32_t& l) {
+    uint16_t hx, lx, hy, ly;
+    split_h(x * sa, hx, lx);
+    split_h(y * sa, hy, ly);
+    h = hx | (uint32_t)hy << 16;
+    l = lx | (uint32_t)ly << 16;
+  };
+  auto stash = [&](const ConvRegs& r, int st) {
+    uint4 hv, lv;
+    pack2(r.a0.x, r.a0.y, hv.x, lv.x);
+    pack2(r.a0.z, r.a0.w, hv.y, lv.y);
+    pack2(r.a1.x, r.a1.y, hv.z, lv.z);
+    pack2(r.a1.z, r.a1.w, hv.w, lv.w);
     *reinterpret_cast<uint4*>(&sA[st][0][cswz(ar, ac)]) = hv;
     *reinterpret_cast<uint4*>(&sA[st][1][cswz(ar, ac)]) = lv;
     if (wload) {
-      *reinterpret_cast<uint4*>(&sW[st][0][cswz(ar, ac)]) = rwh[set];
-      *reinterpret_cast<uint4*>(&sW[st][1][cswz(ar, ac)]) = rwl[set];
+      *reinterpret_cast<uint4*>(&sW[st][0][cswz(ar, ac)]) = r.wh;
+      *reinterpret_cast<uint4*>(&sW[st][1][cswz(ar, ac)]) = r.wl;
     }
   };
 
@@ -148,56 +204,77 @@ __global__ __launch_bounds__(512) void conv_f16x3_kernel(const ConvF16Args a) {
 
   auto compute = [&](int st) {
     const int c = lane >> 4;
-    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+    bf16x8 ah[FM], al[FM];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int row = wm * 32 + i * 16 + (lane & 15);
       ah[i] = *reinterpret_cast<const bf16x8*>(&sA[st][0][cswz(row, c)]);
       al[i] = *reinterpret_cast<const bf16x8*>(&sA[st][1][cswz(row, c)]);
     }
+    // weight fragments two column blocks at a time (fewer live registers: two workgroups per CU); each
+    // accumulator still takes Wh*Ah, Wl*Ah, Wh*Al in that order, four independent accumulators between
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int row = wn * WN + j * 16 + (lane & 15);
-      bh[j] = *reinterpret_cast<const bf16x8*>(&sW[st][0][cswz(row, c)]);
-      bl[j] = *reinterpret_cast<const bf16x8*>(&sW[st][1][cswz(row, c)]);
+    for (int j0 = 0; j0 < FN; j0 += 2) {
+      bf16x8 bh[2], bl[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wn * WN + (j0 + j) * 16 + (lane & 15);
+        bh[j] = *reinterpret_cast<const bf16x8*>(&sW[st][0][cswz(row, c)]);
+        bl[j] = *reinterpret_cast<const bf16x8*>(&sW[st][1][cswz(row, c)]);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma16<true>(bh[j], ah[i], acc[i][j0 + j]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma16<true>(bl[j], ah[i], acc[i][j0 + j]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma16<true>(bh[j], al[i], acc[i][j0 + j]);
     }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma16<true>(bh[j], ah[i], acc[i][j]);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma16<true>(bl[j], ah[i], acc[i][j]);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma16<true>(bh[j], al[i], acc[i][j]);
   };
 
-  // K-tile k: loaded into register set k & 1 two tiles ahead, stashed into LDS stage k & 1 one tile ahead.  The
-  // loop is unrolled by two so every register set and LDS stage index is a compile-time constant (a runtime
-  // index would put the register sets behind selects and make every stash wait for all loads in flight)
-  load(0, 0);
-  if (nk > 1) load(1, 1);
-  stash(0, 0);
+  // K-tile kt0 + i: loaded into register set i & 1 two tiles ahead, stashed into LDS stage i & 1 one tile ahead
+  ConvRegs r0, r1;
+  load(kt0, r0);
+  if (nt > 1) load(kt0 + 1, r1);
+  stash(r0, 0);
   __syncthreads();
-  auto step = [&](int kt, auto set_c) {
-    constexpr int S = decltype(set_c)::value;   // == kt & 1
-    if (kt + 2 < nk) load(kt + 2, S);
-    compute(S);
-    if (kt + 1 < nk) stash(1 - S, 1 - S);
+  for (int i = 0; i < nt; i += 2) {
+    if (i + 2 < nt) load(kt0 + i + 2, r0);
+    compute(0);
+    if (i + 1 < nt) stash(r1, 1);
     __syncthreads();
-  };
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(kt, std::integral_constant<int, 0>{});
-    if (kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1>{});
+    if (i + 1 < nt) {
+      if (i + 3 < nt) load(kt0 + i + 3, r1);
+      compute(1);
+      if (i + 2 < nt) stash(r0, 0);
+      __syncthreads();
+    }
   }
 
-  // epilogue: lane holds channels n0 + wn * WN + j * 16 + 4 * (lane >> 4) + (0..3) of pixel m0 + wm * 32 + i * 16 +
-  // (lane & 15): acc * inv + bias (+ residual), ReLU, the backbones' running max; max|y| into the shard words
-  float ymx = 0.f;
+  // lane holds channels n0 + wn * WN + j * 16 + 4 * (lane >> 4) + (0..3) of pixel m0 + wm * 32 + i * 16 + (lane & 15)
   const int li = lane & 15, lk = lane >> 4;
+  if (a.ks > 1) {   // a K slice: its share of acc / (s_w s_a), summed in slice order by conv_splitk_reduce
+    const int G = gridDim.z / a.ks;
+    float* pb = a.part + ((int64_t)slice * G + grp) * M * a.Cout;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int mo = m0 + wm * 32 + i * 16 + li;
+      if (mo >= M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int no = n0 + wn * WN + j * 16 + 4 * lk;
+        const f32x4 v = acc[i][j] * inv;
+        *reinterpret_cast<float4*>(pb + (int64_t)mo * a.Cout + no) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    return;
+  }
+  float ymx = 0.f;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int mo = m0 + wm * 32 + i * 16 + li;
@@ -205,73 +282,149 @@ __global__ __launch_bounds__(512) void conv_f16x3_kernel(const ConvF16Args a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int no = n0 + wn * WN + j * 16 + 4 * lk;
-      f32x4 v = acc[i][j] * inv;
-      if (a.bias) {
-        const float4 b = *reinterpret_cast<const float4*>(a.bias + no);
-        v += f32x4{b.x, b.y, b.z, b.w};
-      }
-      if (a.resid) {
-        const float4 r = *reinterpret_cast<const float4*>(a.resid + (int64_t)mo * a.Cout + no);
-        v += f32x4{r.x, r.y, r.z, r.w};
-      }
-      if (a.flags & MMT_CONV_RELU)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      float4* dst = reinterpret_cast<float4*>(a.y + (int64_t)mo * a.Cout + no);
-      if (a.flags & MMT_CONV_MAX) {
-        const float4 o = *dst;   // torch.max(color, depth) (dimpnet.py:103)
-        v = f32x4{fmaxf(o.x, v[0]), fmaxf(o.y, v[1]), fmaxf(o.z, v[2]), fmaxf(o.w, v[3])};
-      }
-      *dst = make_float4(v[0], v[1], v[2], v[3]);
+      const f32x4 v = conv_out(g, acc[i][j] * inv, mo, no, a.Cout);
 #pragma unroll
       for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
     }
   }
-  if (a.ymax) {
-    ymx = wave_max(ymx);
-    if (lane == 0 && ymx > 0.f)
-      __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(a.ymax) + ((blockIdx.x * 8 + wave) % kMaxShards) * kShardStride,
-                             __float_as_uint(ymx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (g.ymax) fold_max(g.ymax, ymx, blockIdx.x * 8 + wave);
+}
+
+// split-K: y = sum over the ks slices (in slice order) + bias (+ residual), ReLU, merge; grid (blocks, G), 4 channels
+// per thread
+__global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvF16Args a) {
+  const int grp = blockIdx.y, G = gridDim.y;
+  const ConvGroupArgs g = pick_group(a, grp);
+  const int64_t M = (int64_t)a.N * a.Ho * a.Wo, q = M * a.Cout / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float ymx = 0.f;
+  if (i < q) {
+    const int64_t mo = i * 4 / a.Cout;
+    const int no = (int)(i * 4 - mo * a.Cout);
+    float4 p[kMaxSplitK];
+#pragma unroll
+    for (int s = 0; s < kMaxSplitK; ++s)
+      if (s < a.ks) p[s] = reinterpret_cast<const float4*>(a.part + ((int64_t)s * G + grp) * M * a.Cout)[i];
+    f32x4 v{p[0].x, p[0].y, p[0].z, p[0].w};
+#pragma unroll
+    for (int s = 1; s < kMaxSplitK; ++s)
+      if (s < a.ks) v += f32x4{p[s].x, p[s].y, p[s].z, p[s].w};
+    v = conv_out(g, v, mo, no, a.Cout);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
   }
+  if (g.ymax) fold_max(g.ymax, ymx, blockIdx.x * 4 + (threadIdx.x >> 6));
+}
+
+// K slices for a launch of `tiles` output tiles over nk K-tiles, when the tiles alone leave the GPU's 512
+// workgroup slots (256 CUs x 2) under-filled: the split whose last round of workgroups is fullest (ties: the
+// fewest slices), at least 8 K-tiles per slice
+int conv_pick_ks(int64_t tiles, int nk) {
+  constexpr int64_t kSlots = 512;
+  if (tiles >= kSlots) return 1;
+  int best = 1;
+  double best_eff = 0.0;
+  for (int ks = 1; ks <= kMaxSplitK && nk / ks >= 8; ++ks) {
+    const int64_t w = tiles * ks, rounds = (w + kSlots - 1) / kSlots;
+    const double eff = (double)w / (double)(rounds * kSlots);
+    if (eff > best_eff + 0.02) {
+      best_eff = eff;
+      best = ks;
+    }
+  }
+  return best;
 }
 
 }  // namespace mmt
 
 using namespace mmt;
 
+namespace {
+
+int conv_shape(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pad, int& Ho, int& Wo, int& K) {
+  const bool stem = Cin == 3;
+  if (N <= 0 || H <= 0 || W <= 0 || Cout <= 0 || Cout % 64 || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 ||
+      (!stem && Cin % 32))
+    return MMT_E_ARG;
+  K = stem ? kh * kw * 4 : kh * kw * Cin;
+  Ho = (H + 2 * pad - kh) / stride + 1;
+  Wo = (W + 2 * pad - kw) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return MMT_E_ARG;
+  const int64_t M = (int64_t)N * Ho * Wo;
+  if (M > (int64_t)1 << 30 || (int64_t)Cout * K > (int64_t)1 << 30) return MMT_E_ARG;
+  return MMT_OK;
+}
+
+int conv_bn(int Cin, int Cout) { return Cin == 3 ? 64 : Cout % 128 == 0 ? 128 : 64; }
+
+int64_t conv_ks_for(int N, int Ho, int Wo, int Cin, int Cout, int Kp, int G) {
+  const int64_t gm = ((int64_t)N * Ho * Wo + 127) / 128;
+  return conv_pick_ks(gm * (Cout / conv_bn(Cin, Cout)) * G, Kp / 32);
+}
+
+}  // namespace
+
 extern "C" {
 
 size_t mmt_conv_max_words(void) { return (size_t)kMaxShards * kShardStride; }
+
+size_t mmt_conv2d_f16x3_ws_bytes(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pad,
+                                 int groups) {
+  int Ho, Wo, K;
+  if (groups < 1 || groups > kMaxGroups || conv_shape(N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, K) != MMT_OK)
+    return 0;
+  const int Kp = (K + 31) / 32 * 32;
+  const int64_t ks = conv_ks_for(N, Ho, Wo, Cin, Cout, Kp, groups);
+  return ks > 1 ? (size_t)(ks * groups * N * Ho * Wo * (int64_t)Cout * 4) : 0;
+}
+
+int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, int W, int Cin, int Kp, int Cout,
+                            int kh, int kw, int stride, int pad, void* ws, size_t ws_bytes, void* stream) {
+  int Ho, Wo, K;
+  if (!groups || G < 1 || G > kMaxGroups || conv_shape(N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, K) != MMT_OK ||
+      Kp != (K + 31) / 32 * 32)
+    return MMT_E_ARG;
+  ConvF16Args a{};
+  for (int i = 0; i < G; ++i) {
+    const mmt_conv_group& c = groups[i];
+    if (!c.x || !c.w_hi || !c.w_lo || !c.y || !(c.w_scale > 0) || (c.flags & ~(MMT_CONV_RELU | MMT_CONV_MAX)) ||
+        (!c.x_max && !(c.x_scale > 0)))
+      return MMT_E_ARG;
+    a.g[i] = ConvGroupArgs{c.x, c.w_hi, c.w_lo, c.bias, c.resid, c.y, c.x_max, c.y_max, c.x_scale, 1.0f / c.w_scale,
+                           c.flags};
+  }
+  // the twin layers of a grouped launch write disjoint outputs unless they merge (a MAX layer reads y)
+  if (G == 2 && (a.g[0].y == a.g[1].y || (a.g[0].flags | a.g[1].flags) & MMT_CONV_MAX)) return MMT_E_ARG;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad;
+  a.Ho = Ho; a.Wo = Wo; a.Kp = Kp;
+  const int64_t M = (int64_t)N * Ho * Wo;
+  int ks = (int)conv_ks_for(N, Ho, Wo, Cin, Cout, Kp, G);
+  if (ks > 1 && (!ws || ws_bytes < (size_t)(ks * G * M * (int64_t)Cout * 4))) ks = 1;
+  a.ks = ks;
+  a.part = static_cast<float*>(ws);
+  const unsigned gm = (unsigned)((M + 127) / 128);
+  const int bn = conv_bn(Cin, Cout);
+  const dim3 grid(gm, Cout / bn, G * ks);
+  const hipStream_t s = (hipStream_t)stream;
+  if (Cin == 3)
+    hipLaunchKernelGGL((conv_f16x3_kernel<64, true>), grid, dim3(512), 0, s, a);
+  else if (bn == 128)
+    hipLaunchKernelGGL((conv_f16x3_kernel<128, false>), grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_f16x3_kernel<64, false>), grid, dim3(512), 0, s, a);
+  if (ks > 1) {
+    const int64_t q = M * Cout / 4;
+    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((q + 255) / 256), G), dim3(256), 0, s, a);
+  }
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
 
 int mmt_conv2d_f16x3(const float* x, int N, int H, int W, int Cin, const uint16_t* w_hi, const uint16_t* w_lo,
                      float w_scale, int Kp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
                      const float* resid, float* y, const float* x_max, float x_scale, float* y_max, int flags,
                      void* stream) {
-  const bool stem = Cin == 3;
-  if (!x || !w_hi || !w_lo || !y || N <= 0 || H <= 0 || W <= 0 || Cout <= 0 || Cout % 64 || kh <= 0 || kw <= 0 ||
-      stride <= 0 || pad < 0 || !(w_scale > 0) || (flags & ~(MMT_CONV_RELU | MMT_CONV_MAX)) ||
-      (!stem && Cin % 32) || (!x_max && !(x_scale > 0)))
-    return MMT_E_ARG;
-  const int K = stem ? kh * kw * 4 : kh * kw * Cin;
-  if (Kp != (K + 31) / 32 * 32) return MMT_E_ARG;
-  ConvF16Args a{x, w_hi, w_lo, bias, resid, y, x_max, x_scale, y_max, 1.0f / w_scale, N, H, W, Cin, Cout, kh, kw,
-                stride, pad, 0, 0, Kp, flags};
-  a.Ho = (H + 2 * pad - kh) / stride + 1;
-  a.Wo = (W + 2 * pad - kw) / stride + 1;
-  if (a.Ho <= 0 || a.Wo <= 0) return MMT_E_ARG;
-  const int64_t M = (int64_t)N * a.Ho * a.Wo;
-  if (M > (int64_t)1 << 30 || (int64_t)Cout * Kp > (int64_t)1 << 30) return MMT_E_ARG;
-  const unsigned gm = (unsigned)((M + 127) / 128);
-  const hipStream_t s = (hipStream_t)stream;
-  if (stem) {
-    if (Cout % 64) return MMT_E_ARG;
-    hipLaunchKernelGGL((conv_f16x3_kernel<64, true>), dim3(gm, Cout / 64), dim3(512), 0, s, a);
-  } else if (Cout % 128 == 0) {
-    hipLaunchKernelGGL((conv_f16x3_kernel<128, false>), dim3(gm, Cout / 128), dim3(512), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((conv_f16x3_kernel<64, false>), dim3(gm, Cout / 64), dim3(512), 0, s, a);
-  }
-  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+  const mmt_conv_group g{x, w_hi, w_lo, w_scale, bias, resid, y, x_max, x_scale, y_max, flags};
+  return mmt_conv2d_f16x3_groups(&g, 1, N, H, W, Cin, Kp, Cout, kh, kw, stride, pad, nullptr, 0, stream);
 }
 
 }  // extern "C"

@@ -235,6 +235,32 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float* __restrict__ 
   y[i] = m;
 }
 
+// the same over 4 channels per thread (C % 4 == 0): float4 loads and stores
+__global__ __launch_bounds__(256) void maxpool4_kernel(const float4* __restrict__ x, int N, int H, int W, int C4, int k,
+                                                       int s, int pad, int Ho, int Wo, float4* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * Ho * Wo * C4;
+  if (i >= total) return;
+  const int c = (int)(i % C4);
+  int64_t r = i / C4;
+  const int ox = (int)(r % Wo);
+  r /= Wo;
+  const int oy = (int)(r % Ho);
+  const int n = (int)(r / Ho);
+  float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  for (int dy = 0; dy < k; ++dy) {
+    const int iy = oy * s - pad + dy;
+    if (iy < 0 || iy >= H) continue;
+    for (int dx = 0; dx < k; ++dx) {
+      const int ix = ox * s - pad + dx;
+      if (ix < 0 || ix >= W) continue;
+      const float4 v = x[(((int64_t)n * H + iy) * W + ix) * C4 + c];
+      m = make_float4(fmaxf(m.x, v.x), fmaxf(m.y, v.y), fmaxf(m.z, v.z), fmaxf(m.w, v.w));
+    }
+  }
+  y[i] = m;
+}
+
 // NCHW [N][C][H][W] pixel values (0..255) -> per 3-channel half NHWC ((v / 255) - mean) / std
 // (net_wrappers.py:62-72: color and depth halves normalised with the same ImageNet constants)
 __global__ __launch_bounds__(256) void normalize_kernel(const float* __restrict__ im, int N, int C, int H, int W,
@@ -257,31 +283,65 @@ __global__ __launch_bounds__(256) void normalize_kernel(const float* __restrict_
   }
 }
 
-// InstanceL2Norm (size_average): y = x * (scale * sqrt((1 / (sum x^2 + eps)) * C*H*W)); one workgroup per
-// sample, fixed-order tree reduction; writes NHWC and/or NCHW
-__global__ __launch_bounds__(1024) void l2norm_kernel(const float* __restrict__ x, int HW, int C, float scale,
-                                                      float eps, float* __restrict__ y_nhwc, float* __restrict__ y_nchw) {
-  __shared__ float red[1024];
-  const int n = blockIdx.x;
-  const int64_t L = (int64_t)HW * C;
-  const float* xs = x + n * L;
-  float s = 0.f;
-  for (int64_t i = threadIdx.x; i < L; i += 1024) s += xs[i] * xs[i];
-  red[threadIdx.x] = s;
+// InstanceL2Norm (size_average): y = x * (scale * sqrt((1 / (sum x^2 + eps)) * C*H*W)).  Two passes over
+// workgroups of kL2Pix pixels x C channels of one sample: the squares summed per workgroup (fixed order) into
+// ws[n][chunk]; then every workgroup sums its sample's chunk sums in chunk order and scales its pixels, writing
+// NHWC (float4) and / or NCHW (transposed through the LDS: runs of kL2Pix pixels per channel)
+constexpr int kL2Pix = 16, kL2MaxC = 1024;
+
+__device__ __forceinline__ float block_sum_256(float v, float* red) {   // fixed-order workgroup sum (256 threads)
+  red[threadIdx.x] = v;
   __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
+  for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  const float f = sqrtf((1.0f / (red[0] + eps)) * (float)L) * scale;
-  for (int64_t i = threadIdx.x; i < L; i += 1024) {
-    const float v = xs[i] * f;
-    if (y_nhwc) y_nhwc[n * L + i] = v;
-    if (y_nchw) {
-      const int c = (int)(i % C);
-      const int64_t p = i / C;
-      y_nchw[n * L + (int64_t)c * HW + p] = v;
-    }
+  return red[0];
+}
+
+__global__ __launch_bounds__(256) void l2norm_sumsq_kernel(const float* __restrict__ x, int HW, int C,
+                                                           float* __restrict__ ws) {
+  __shared__ float red[256];
+  const int n = blockIdx.y, p0 = blockIdx.x * kL2Pix, np = min(kL2Pix, HW - p0);
+  const float4* xs = reinterpret_cast<const float4*>(x + ((int64_t)n * HW + p0) * C);
+  const int q = np * C / 4;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < q; i += 256) {
+    const float4 v = xs[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  s = block_sum_256(s, red);
+  if (threadIdx.x == 0) ws[(int64_t)n * gridDim.x + blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void l2norm_scale_kernel(const float* __restrict__ x, int HW, int C, float scale,
+                                                           float eps, const float* __restrict__ ws,
+                                                           float* __restrict__ y_nhwc, float* __restrict__ y_nchw) {
+  __shared__ float tile[kL2Pix * kL2MaxC];
+  __shared__ float fsh;
+  const int n = blockIdx.y, p0 = blockIdx.x * kL2Pix, np = min(kL2Pix, HW - p0);
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < (int)gridDim.x; ++k) t += ws[(int64_t)n * gridDim.x + k];
+    fsh = sqrtf((1.0f / (t + eps)) * ((float)HW * (float)C)) * scale;
+  }
+  __syncthreads();
+  const float f = fsh;
+  const int64_t base = ((int64_t)n * HW + p0) * C;
+  const float4* xs = reinterpret_cast<const float4*>(x + base);
+  const int q = np * C / 4;
+  for (int i = threadIdx.x; i < q; i += 256) {
+    float4 v = xs[i];
+    v.x *= f; v.y *= f; v.z *= f; v.w *= f;
+    if (y_nhwc) reinterpret_cast<float4*>(y_nhwc + base)[i] = v;
+    if (y_nchw) *reinterpret_cast<float4*>(&tile[i * 4]) = v;
+  }
+  if (!y_nchw) return;
+  __syncthreads();
+  float* yo = y_nchw + (int64_t)n * C * HW + p0;
+  for (int i = threadIdx.x; i < kL2Pix * C; i += 256) {
+    const int c = i / kL2Pix, p = i - c * kL2Pix;
+    if (p < np) yo[(int64_t)c * HW + p] = tile[p * C + c];
   }
 }
 
@@ -478,8 +538,13 @@ int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int str
     return MMT_E_ARG;
   const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
   if (Ho <= 0 || Wo <= 0) return MMT_E_ARG;
-  hipLaunchKernelGGL(maxpool_kernel, dim3(blocks_for((int64_t)N * Ho * Wo * C)), dim3(256), 0, (hipStream_t)stream, x, N,
-                     H, W, C, k, stride, pad, Ho, Wo, y);
+  if (C % 4 == 0)
+    hipLaunchKernelGGL(maxpool4_kernel, dim3(blocks_for((int64_t)N * Ho * Wo * C / 4)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(x), N, H, W, C / 4, k, stride, pad, Ho, Wo,
+                       reinterpret_cast<float4*>(y));
+  else
+    hipLaunchKernelGGL(maxpool_kernel, dim3(blocks_for((int64_t)N * Ho * Wo * C)), dim3(256), 0, (hipStream_t)stream, x,
+                       N, H, W, C, k, stride, pad, Ho, Wo, y);
   return last_err();
 }
 
@@ -492,10 +557,20 @@ int mmt_image_normalize(const float* im, int N, int C, int H, int W, const float
   return last_err();
 }
 
+size_t mmt_instance_l2norm_ws_bytes(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return 0;
+  return (size_t)N * ((H * W + kL2Pix - 1) / kL2Pix) * sizeof(float);
+}
+
 int mmt_instance_l2norm(const float* x, int N, int H, int W, int C, float scale, float eps, float* y_nhwc, float* y_nchw,
-                        void* stream) {
-  if (!x || (!y_nhwc && !y_nchw) || N <= 0 || H <= 0 || W <= 0 || C <= 0) return MMT_E_ARG;
-  hipLaunchKernelGGL(l2norm_kernel, dim3(N), dim3(1024), 0, (hipStream_t)stream, x, H * W, C, scale, eps, y_nhwc, y_nchw);
+                        float* ws, void* stream) {
+  if (!x || !ws || (!y_nhwc && !y_nchw) || N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 || C > kL2MaxC)
+    return MMT_E_ARG;
+  const int HW = H * W;
+  const dim3 grid((HW + kL2Pix - 1) / kL2Pix, N);
+  hipLaunchKernelGGL(l2norm_sumsq_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, HW, C, ws);
+  hipLaunchKernelGGL(l2norm_scale_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, HW, C, scale, eps, ws, y_nhwc,
+                     y_nchw);
   return last_err();
 }
 

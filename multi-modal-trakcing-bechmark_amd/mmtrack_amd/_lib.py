@@ -98,6 +98,12 @@ class MmtDimpTrackParams(ctypes.Structure):
     ]
 
 
+class MmtConvGroup(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("w_hi", ctypes.c_void_p), ("w_lo", ctypes.c_void_p), ("w_scale", ctypes.c_float),
+                ("bias", ctypes.c_void_p), ("resid", ctypes.c_void_p), ("y", ctypes.c_void_p), ("x_max", ctypes.c_void_p),
+                ("x_scale", ctypes.c_float), ("y_max", ctypes.c_void_p), ("flags", ctypes.c_int)]
+
+
 class MmtDimpResult(ctypes.Structure):
     _fields_ = [("box", ctypes.c_float * 4), ("max_score", ctypes.c_float), ("flag", ctypes.c_int),
                 ("num_iter", ctypes.c_int), ("n_samples", ctypes.c_int), ("replace_ind", ctypes.c_int),
@@ -143,9 +149,12 @@ SIGNATURES = {
     "mmt_conv2d_f32": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
     "mmt_conv_max_words": (ctypes.c_size_t, []),
     "mmt_conv2d_f16x3": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _I, _P]),
+    "mmt_conv2d_f16x3_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
+    "mmt_conv2d_f16x3_groups": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, ctypes.c_size_t, _P]),
     "mmt_maxpool2d_f32": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "mmt_image_normalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
-    "mmt_instance_l2norm": (_I, [_P, _I, _I, _I, _I, _F, _F, _P, _P, _P]),
+    "mmt_instance_l2norm_ws_bytes": (ctypes.c_size_t, [_I, _I, _I]),
+    "mmt_instance_l2norm": (_I, [_P, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P]),
     "mmt_prroi_pool": (_I, [_P, _I, _I, _I, _I, _P, _F, _I, _I, _P, _P]),
     "mmt_sample_patch": (_I, [_P, _I, _I, _I, ctypes.c_int64, _P, _I, _I, _P, _P]),
     "mmt_patch_transform": (_I, [_P, _I, _I, _I, ctypes.POINTER(MmtPatchTf), _I, _I, _P, _P]),
@@ -155,8 +164,8 @@ SIGNATURES = {
     "mmt_dimp_feat_transpose": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_dimp_optimize": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, ctypes.POINTER(MmtDimpParams), _I, _P,
                                ctypes.c_size_t, _P, _P]),
-    "mmt_dimp_optimize_dev": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, ctypes.POINTER(MmtDimpParams), _I, _P,
-                                   ctypes.c_size_t, _P]),
+    "mmt_dimp_optimize_dev": (_I, [_P, _I64, _I64, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I64, _I64, _P, _I64, _I64,
+                                   ctypes.POINTER(MmtDimpParams), _I, _P, ctypes.c_size_t, _P]),
     "mmt_dimp_state_bytes": (ctypes.c_size_t, []),
     "mmt_dimp_track_sample": (_I, [_P, _P, _I, ctypes.POINTER(MmtDimpTrackParams), _I, _I, _P, _P]),
     "mmt_dimp_track_update": (_I, [_P, _I, _P, _I, _I, ctypes.POINTER(MmtDimpTrackParams), _P, _I64, _P, _P, _P]),

@@ -136,21 +136,29 @@ class DiMPSteepestDescentGN:
             losses.append(torch.tensor(lbuf[0]))
         return w, iterates, losses
 
-    def optimize_dev(self, weights, feat, bb_ptr, sw_ptr, num_iter):
-        """num_iter steps in place on ``weights`` (a contiguous [S, C, fh, fw] CUDA tensor) with the boxes
-        [I][S][4] and sample weights [I][S] at device addresses (the device tracker state): no host staging, no
-        synchronisation (mmt_dimp_optimize_dev)."""
+    def optimize_dev(self, weights, feat, bb_ptr, sw_ptr, num_iter, bb_strides=(0, 0), sw_strides=(0, 0)):
+        """num_iter steps in place on ``weights`` (a contiguous [S, C, fh, fw] CUDA tensor) over ``feat``
+        [I, S, C, H, W] -- any strides on the first two dims, e.g. a DimpPool's memory[a:b, :I].transpose(0, 1)
+        -- with the boxes and sample weights at device addresses (the device tracker state), strides in floats
+        as (sample, sequence), 0: contiguous [I][S]; no host staging, no synchronisation (mmt_dimp_optimize_dev)."""
         lib = _lib.load()
-        feat = _check(feat, "feat", 5)
+        if not (isinstance(feat, torch.Tensor) and feat.is_cuda and feat.dtype == torch.float32 and feat.dim() == 5):
+            raise ValueError("feat must be a 5-dim float32 CUDA tensor")
         I, S, C, H, W = feat.shape
+        if feat.stride()[2:] != (H * W, W, 1):
+            raise ValueError("feat must be contiguous over [C, H, W]")
+        if not (weights.is_contiguous() and tuple(weights.shape[:2]) == (S, C)):
+            raise ValueError("weights must be a contiguous [S, C, fh, fw] tensor")
         fh, fw = weights.shape[-2:]
         nbytes = lib.mmt_dimp_workspace_bytes(I, S, C, H, W, fh, fw, num_iter)
         if nbytes == 0:
             raise ValueError("unsupported DiMP problem shape")
         ws = self._workspace(feat.device, nbytes)
-        _rc(lib.mmt_dimp_optimize_dev(feat.data_ptr(), I, S, C, H, W, weights.data_ptr(), fh, fw, ctypes.c_void_p(bb_ptr),
-                                      ctypes.c_void_p(sw_ptr) if sw_ptr else None, ctypes.byref(self.params), num_iter,
-                                      ws.data_ptr(), nbytes, _stream(feat.device)), "mmt_dimp_optimize_dev")
+        _rc(lib.mmt_dimp_optimize_dev(feat.data_ptr(), feat.stride(0), feat.stride(1), I, S, C, H, W,
+                                      weights.data_ptr(), fh, fw, ctypes.c_void_p(bb_ptr), bb_strides[0],
+                                      bb_strides[1], ctypes.c_void_p(sw_ptr) if sw_ptr else None, sw_strides[0],
+                                      sw_strides[1], ctypes.byref(self.params), num_iter, ws.data_ptr(), nbytes,
+                                      _stream(feat.device)), "mmt_dimp_optimize_dev")
         return weights
 
     def optimize(self, weights, feat, bb, sample_weight=None, num_iter=None):

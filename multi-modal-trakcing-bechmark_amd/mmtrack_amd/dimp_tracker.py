@@ -258,8 +258,10 @@ class DiMP:
         target_boxes = self.init_target_boxes()
         w = self.net.init_filter(x_nhwc.contiguous(), target_boxes)
         num_iter = self.params.get('net_opt_iter', None)
-        self.target_filter = self.optimizer.optimize(w, x.unsqueeze(1).contiguous(), target_boxes.view(-1, 1, 4),
-                                                     num_iter=num_iter)
+        w = self.optimizer.optimize(w, x.unsqueeze(1).contiguous(), target_boxes.view(-1, 1, 4), num_iter=num_iter)
+        # the filter lives in the pool's filter array (one row per slot), so a batch's filters apply and update
+        # in place without gathering
+        self.target_filter = self.pool.write_filter(self.slot, w)
         self.init_memory(x)
 
     def init_target_boxes(self):
@@ -311,12 +313,8 @@ class DiMP:
     def _update_filter(self, res):
         """update_classifier's Gauss-Newton steps (dimp.py:555-570) when the frame's record asks for them: the
         filter is optimised in place over the slot's memory samples, boxes and weights (all on the device)."""
-        if res.num_iter <= 0:
-            return
-        n = res.n_samples
-        samples = self.pool.memory[self.slot, :n].unsqueeze(1)
-        bb, sw = self.pool.boxes_ptr(self.slot), self.pool.weights_ptr(self.slot)
-        self.optimizer.optimize_dev(self.target_filter, samples, bb, sw, res.num_iter)
+        if res.num_iter > 0:
+            self.pool.update_filters(self.slot, 1, res.n_samples, res.num_iter, self.optimizer)
 
 
 FLAGS = ('normal', 'not_found', 'uncertain', 'hard_negative')
@@ -338,6 +336,7 @@ class DimpPool:
         self.rbytes = ctypes.sizeof(_lib.MmtDimpResult)
         self.results = torch.zeros(capacity * self.rbytes, dtype=torch.uint8, device=self.dev)
         self.memory = None   # [capacity][50][C][h][w], allocated with the first sample shape
+        self.filters = None  # [capacity][C][fh][fw]: every slot's target filter
         self.next = 0
         p = _lib.MmtDimpTrackParams()
         sz = params.image_sample_size
@@ -399,6 +398,23 @@ class DimpPool:
         self.memory[slot, :x.shape[0]] = x
         self.memory[slot, x.shape[0]:] = 0
 
+    def write_filter(self, slot, w):
+        """Store slot's filter [1, C, fh, fw]; returns the slot's row (a view the tracker keeps)."""
+        if self.filters is None:
+            self.filters = torch.zeros(self.cap, *w.shape[1:], dtype=torch.float32, device=self.dev)
+        self.filters[slot] = w[0]
+        return self.filters[slot:slot + 1]
+
+    def update_filters(self, first, n, n_samples, num_iter, optimizer):
+        """num_iter Gauss-Newton steps on the filters of slots [first, first + n) in one optimiser call over their
+        memories ([n][50] samples read in place through strides) and device boxes / weights: I = the largest
+        stored-sample count; a slot's samples beyond its own count have weight 0 and add exact zeros, so each
+        filter is the one a call over its own samples gives (mmt_dimp_optimize_dev)."""
+        feat = self.memory[first:first + n, :n_samples].transpose(0, 1)   # [I][S][C][h][w]
+        sf = self.sbytes // 4   # the state stride in floats
+        optimizer.optimize_dev(self.filters[first:first + n], feat, self.boxes_ptr(first), self.weights_ptr(first),
+                               num_iter, bb_strides=(4, sf), sw_strides=(1, sf))
+
     def result(self, slot):
         return _lib.MmtDimpResult.from_buffer_copy(bytes(self.res_host[slot * self.rbytes:(slot + 1) * self.rbytes]
                                                          .numpy()))
@@ -426,7 +442,7 @@ class DimpPool:
             raise RuntimeError(f"mmt_dimp_track_sample failed ({rc})")
         test_x = net.extract_classification_feat(net.extract_backbone(patches))
         from .dimp import apply_filter
-        scores = apply_filter(test_x.unsqueeze(0), torch.cat([t.target_filter for t in trackers]))[0].contiguous()
+        scores = apply_filter(test_x.unsqueeze(0), self.filters[first:first + n])[0].contiguous()
         F_ = test_x[0].numel()
         rc = lib.mmt_dimp_track_update(ctypes.c_void_p(self.state_ptr(first)), n, ctypes.c_void_p(scores.data_ptr()),
                                        scores.shape[-2], scores.shape[-1], ctypes.byref(self.tparams),
@@ -444,12 +460,19 @@ class DimpPool:
     def finish(self, trackers, first, ev):
         """Wait for the records, launch the filter updates they ask for, return the per-tracker outputs."""
         ev.synchronize()
-        outs = []
-        for i, t in enumerate(trackers):
-            res = self.result(first + i)
-            t._update_filter(res)
-            outs.append(t._output(res))
-        return outs
+        recs = [self.result(first + i) for i in range(len(trackers))]
+        # the filter updates the records ask for, batched over runs of consecutive slots with the same number of
+        # steps (one optimiser call per run instead of one per sequence)
+        i = 0
+        while i < len(recs):
+            k = recs[i].num_iter
+            j = i + 1
+            while j < len(recs) and recs[j].num_iter == k:
+                j += 1
+            if k > 0:
+                self.update_filters(first + i, j - i, max(r.n_samples for r in recs[i:j]), k, trackers[i].optimizer)
+            i = j
+        return [t._output(res) for t, res in zip(trackers, recs)]
 
 
 def _slots(trackers):

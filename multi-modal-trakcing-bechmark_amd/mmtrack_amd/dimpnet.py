@@ -93,20 +93,38 @@ class _Conv:
     def out_hw(self, H, W):
         return (H + 2 * self.pad - self.kh) // self.stride + 1, (W + 2 * self.pad - self.kw) // self.stride + 1
 
+    def group(self, x, out, relu=False, resid=None, merge_max=False, x_max=None, x_scale=0.0, y_max=None):
+        """This conv's operands as one mmt_conv_group of an f16x3 launch."""
+        flags = (1 if relu else 0) | (2 if merge_max else 0)
+        ptr = (lambda t: t.data_ptr() if t is not None else None)
+        return _lib.MmtConvGroup(x.data_ptr(), self.wh.data_ptr(), self.wl.data_ptr(), self.w_scale, ptr(self.b),
+                                 ptr(resid), out.data_ptr(), ptr(x_max), float(x_scale), ptr(y_max), flags)
+
     def __call__(self, lib, x, N, H, W, out, stream, relu=False, resid=None, merge_max=False, x_max=None,
-                 x_scale=0.0, y_max=None):
+                 x_scale=0.0, y_max=None, ws=None):
         """f16x3: x_max = the input's sharded max words (or x_scale, a static power-of-two input scale), y_max =
-        the output's (accumulated by the epilogue; None: not tracked)."""
+        the output's (accumulated by the epilogue; None: not tracked); ws(nbytes) -> a device buffer for split-K
+        partials (None: no split)."""
         if self.f16x3:
-            flags = (1 if relu else 0) | (2 if merge_max else 0)
-            _rc(lib.mmt_conv2d_f16x3(_p(x), N, H, W, self.cin, _p(self.wh), _p(self.wl), self.w_scale, self.kp,
-                                     _p(self.b), self.cout, self.kh, self.kw, self.stride, self.pad, _p(resid),
-                                     _p(out), _p(x_max), float(x_scale), _p(y_max), flags, stream), "mmt_conv2d_f16x3")
+            run_f16x3(lib, self, [self.group(x, out, relu, resid, merge_max, x_max, x_scale, y_max)], N, H, W, ws,
+                      stream)
             return out
         flags = (1 if relu else 0) | (2 if merge_max else 0) | (4 if self.w4 else 0)
         _rc(lib.mmt_conv2d_f32(_p(x), N, H, W, self.cin, _p(self.w), _p(self.b), self.cout, self.kh, self.kw,
                                self.stride, self.pad, _p(resid), _p(out), flags, stream), "mmt_conv2d_f32")
         return out
+
+
+def run_f16x3(lib, conv, groups, N, H, W, ws, stream):
+    """One mmt_conv2d_f16x3_groups launch of conv's shape over groups (the twin layers of the two backbones, or
+    one); split-K partials in ws(nbytes) when the library asks for a split."""
+    G = len(groups)
+    need = lib.mmt_conv2d_f16x3_ws_bytes(N, H, W, conv.cin, conv.cout, conv.kh, conv.kw, conv.stride, conv.pad, G)
+    buf = ws(need) if (need and ws is not None) else None
+    arr = (_lib.MmtConvGroup * G)(*groups)
+    _rc(lib.mmt_conv2d_f16x3_groups(arr, G, N, H, W, conv.cin, conv.kp, conv.cout, conv.kh, conv.kw, conv.stride,
+                                    conv.pad, _p(buf), need if buf is not None else 0, stream),
+        "mmt_conv2d_f16x3_groups")
 
 
 class DiMPNet:
@@ -183,41 +201,69 @@ class DiMPNet:
             raise RuntimeError("DiMPNet: out of max-word slots")
         return self._max_words[k * MAX_WORDS:(k + 1) * MAX_WORDS]
 
-    def _resnet(self, bb, x, N, H, W, out, merge_max, s, out_max):
-        """One ResNet-50 to layer3 of NHWC x [N, H, W, 3]; writes (or max-merges into) out [N, H/16, W/16, 1024].
-        f16x3: every conv reads its input's max words and accumulates its output's (out_max for layer3, shared
-        by the two backbones so it bounds the merged map)."""
+    def _ws(self, nbytes):
+        return self._buf("splitk", (nbytes + 3) // 4)
+
+    def _layer(self, convs, kws, N, H, W, s):
+        """The same layer of each backbone: f16x3 runs the twins as one grouped launch (unless one merges into
+        the other's output); fp32 runs them in backbone order."""
+        if self.precision == "f16x3" and len(convs) > 1 and not any(kw.get("merge_max") for kw in kws):
+            run_f16x3(self.lib, convs[0], [c.group(**kw) for c, kw in zip(convs, kws)], N, H, W, self._ws, s)
+            return
+        for c, kw in zip(convs, kws):
+            c(self.lib, kw.pop("x"), N, H, W, kw.pop("out"), s, ws=self._ws, **kw)
+
+    def _resnets(self, xs, N, H, W, out, s, out_max):
+        """Both ResNet-50s to layer3, layer by layer, of NHWC xs[k] [N, H, W, 3]; the RGB backbone writes out
+        [N, H/16, W/16, 1024] and the aux backbone's last conv max-merges into it (dimpnet.py:103).  f16x3: every
+        conv reads its input's max words and accumulates its output's (out_max for layer3, shared by the two
+        backbones so it bounds the merged map)."""
         lib = self.lib
-        stem, blocks = bb
-        h, w = stem.out_hw(H, W)
-        t0 = self._buf("stem", N * h * w * 64)
-        t0_max = self._slot()
-        stem(lib, x, N, H, W, t0, s, relu=True, x_scale=self.image_scale, y_max=t0_max)
+        K = range(len(self.backbones))
+        stems = [bb[0] for bb in self.backbones]
+        h, w = stems[0].out_hw(H, W)
+        t0 = [self._buf(f"stem{k}", N * h * w * 64) for k in K]
+        t0_max = [self._slot() for k in K]
+        self._layer(stems, [dict(x=xs[k], out=t0[k], relu=True, x_scale=self.image_scale, y_max=t0_max[k])
+                            for k in K], N, H, W, s)
         H2, W2 = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
-        cur = self._buf("ping", N * H2 * W2 * 256)
-        _rc(lib.mmt_maxpool2d_f32(_p(t0), N, h, w, 64, 3, 2, 1, _p(cur), s), "mmt_maxpool2d_f32")
+        cur = [self._buf(f"ping{k}", N * H2 * W2 * 256) for k in K]
+        for k in K:
+            _rc(lib.mmt_maxpool2d_f32(_p(t0[k]), N, h, w, 64, 3, 2, 1, _p(cur[k]), s), "mmt_maxpool2d_f32")
         cur_max = t0_max   # a max-pool never exceeds its input's maximum
-        H, W, C = H2, W2, 64
+        H, W = H2, W2
         nxt_name = "pong"
-        for i, (c1, c2, c3, ds) in enumerate(blocks):
-            Ho, Wo = c2.out_hw(H, W)
-            a = self._buf("a", N * H * W * c1.cout)
-            a_max = self._slot()
-            c1(lib, cur, N, H, W, a, s, relu=True, x_max=cur_max, y_max=a_max)
-            b = self._buf("b", N * Ho * Wo * c2.cout)
-            b_max = self._slot()
-            c2(lib, a, N, H, W, b, s, relu=True, x_max=a_max, y_max=b_max)
-            if ds is not None:
-                res = self._buf("res", N * Ho * Wo * ds.cout)
-                ds(lib, cur, N, H, W, res, s, x_max=cur_max)   # only ever a residual operand: no max words
+        nblocks = len(self.backbones[0][1])
+        for i in range(nblocks):
+            c1s, c2s, c3s, dss = zip(*[bb[1][i] for bb in self.backbones])
+            Ho, Wo = c2s[0].out_hw(H, W)
+            a = [self._buf(f"a{k}", N * H * W * c1s[0].cout) for k in K]
+            a_max = [self._slot() for k in K]
+            self._layer(c1s, [dict(x=cur[k], out=a[k], relu=True, x_max=cur_max[k], y_max=a_max[k]) for k in K],
+                        N, H, W, s)
+            b = [self._buf(f"b{k}", N * Ho * Wo * c2s[0].cout) for k in K]
+            b_max = [self._slot() for k in K]
+            self._layer(c2s, [dict(x=a[k], out=b[k], relu=True, x_max=a_max[k], y_max=b_max[k]) for k in K],
+                        N, H, W, s)
+            if dss[0] is not None:
+                res = [self._buf(f"res{k}", N * Ho * Wo * dss[0].cout) for k in K]
+                # only ever a residual operand: no max words
+                self._layer(dss, [dict(x=cur[k], out=res[k], x_max=cur_max[k]) for k in K], N, H, W, s)
             else:
                 res = cur
-            last = i == len(blocks) - 1
-            o = out if last else self._buf(nxt_name, N * Ho * Wo * c3.cout)
-            o_max = out_max if last else self._slot()
-            c3(lib, b, N, Ho, Wo, o, s, relu=True, resid=res, merge_max=merge_max and last, x_max=b_max, y_max=o_max)
+            last = i == nblocks - 1
+            if last:
+                o, o_max = [out] * len(K), [out_max] * len(K)
+                for k in K:   # the RGB map first, then the aux map merged into it
+                    self._layer([c3s[k]], [dict(x=b[k], out=out, relu=True, resid=res[k], merge_max=k > 0,
+                                                x_max=b_max[k], y_max=out_max)], N, Ho, Wo, s)
+            else:
+                o = [self._buf(f"{nxt_name}{k}", N * Ho * Wo * c3s[0].cout) for k in K]
+                o_max = [self._slot() for k in K]
+                self._layer(c3s, [dict(x=b[k], out=o[k], relu=True, resid=res[k], x_max=b_max[k], y_max=o_max[k])
+                                  for k in K], N, Ho, Wo, s)
             cur, cur_max, nxt_name = o, o_max, ("ping" if nxt_name == "pong" else "pong")
-            H, W, C = Ho, Wo, c3.cout
+            H, W = Ho, Wo
         return H, W
 
     def flops(self, H=288, W=288):
@@ -256,9 +302,7 @@ class DiMPNet:
             self._max_words.zero_()
             self._nslot = 0
         out_max = self._slot()
-        # the aux backbone's last conv max-merges into the RGB backbone's layer3 (dimpnet.py:103)
-        h, w = self._resnet(self.backbones[0], xa, N, H, W, out, False, s, out_max)
-        self._resnet(self.backbones[1], xb, N, H, W, out, True, s, out_max)
+        h, w = self._resnets([xa, xb], N, H, W, out, s, out_max)
         assert (h, w) == (Hf, Wf)
         self._layer3_max = (out, out_max)
         return out
@@ -271,11 +315,12 @@ class DiMPNet:
         lm = getattr(self, "_layer3_max", None)
         if self.precision == "f16x3" and (lm is None or lm[0] is not layer3):
             raise ValueError("f16x3: extract_classification_feat takes the layer3 map of the last extract_backbone")
-        self.clf(self.lib, layer3, N, h, w, t, s, x_max=lm[1] if lm else None)
+        self.clf(self.lib, layer3, N, h, w, t, s, x_max=lm[1] if lm else None, ws=self._ws)
         out = torch.empty(N, self.out_dim, h, w, dtype=torch.float32, device=self.dev)
         out_nhwc = torch.empty(N, h, w, self.out_dim, dtype=torch.float32, device=self.dev) if nhwc else None
-        _rc(self.lib.mmt_instance_l2norm(_p(t), N, h, w, self.out_dim, self.norm_scale, 1e-5, _p(out_nhwc), _p(out), s),
-            "mmt_instance_l2norm")
+        l2ws = self._buf("l2ws", (self.lib.mmt_instance_l2norm_ws_bytes(N, h, w) + 3) // 4)
+        _rc(self.lib.mmt_instance_l2norm(_p(t), N, h, w, self.out_dim, self.norm_scale, 1e-5, _p(out_nhwc), _p(out),
+                                         _p(l2ws), s), "mmt_instance_l2norm")
         return (out, out_nhwc) if nhwc else out
 
     def init_filter(self, feat_nhwc, bb):
@@ -285,7 +330,7 @@ class DiMPNet:
         s = self._stream()
         f = self._buf("fconv", N * h * w * C)
         # the InstanceL2Norm output: |y| <= norm_scale * sqrt(C h w) (normalization.py:6-21)
-        self.fconv(self.lib, feat_nhwc, N, h, w, f, s, x_scale=self.l2_scale(C * h * w))
+        self.fconv(self.lib, feat_nhwc, N, h, w, f, s, x_scale=self.l2_scale(C * h * w), ws=self._ws)
         bb = torch.as_tensor(bb, dtype=torch.float32).reshape(-1, 4).clone()
         bb[:, 2:4] = bb[:, 0:2] + bb[:, 2:4]
         rois = bb.to(self.dev)
@@ -325,22 +370,26 @@ def patch_transform_device(img, tf, out_hw):
 
 
 def conv2d(x_nchw, w, bias=None, stride=1, pad=0, resid=None, relu=False, w4=True, precision="fp32", x_max=None,
-           y_max=None):
+           y_max=None, split=False, merge_into=None):
     """Test / tool helper: torch NCHW conv through mmt_conv2d_f32 or (precision "f16x3") mmt_conv2d_f16x3
-    (weights nn.Conv2d layout; f16x3 input range: x_max words, else the static scale of max|x|)."""
+    (weights nn.Conv2d layout; f16x3 input range: x_max words, else the static scale of max|x|; split: give the
+    library a split-K workspace; merge_into: an NHWC map the output is max-merged into (and returned))."""
     lib = _lib.load()
     f16 = precision == "f16x3"
     conv = _Conv(w, bias=bias, stride=stride, pad=pad, dev=x_nchw.device, w4=w4, f16x3=f16)
     N, C, H, W = x_nchw.shape
     Ho, Wo = conv.out_hw(H, W)
     x = x_nchw.permute(0, 2, 3, 1).contiguous()
-    out = torch.empty(N, Ho, Wo, conv.cout, dtype=torch.float32, device=x.device)
+    out = merge_into if merge_into is not None else torch.empty(N, Ho, Wo, conv.cout, dtype=torch.float32,
+                                                                device=x.device)
     r = resid.permute(0, 2, 3, 1).contiguous() if resid is not None else None
     kw = {}
     if f16:
         kw = dict(x_max=x_max, x_scale=0.0 if x_max is not None else range_scale(float(x.abs().max())), y_max=y_max)
+        if split:
+            kw["ws"] = lambda n: torch.empty((n + 3) // 4, dtype=torch.float32, device=x.device)
     conv(lib, x, N, H, W, out, ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream), relu=relu, resid=r,
-         **kw)
+         merge_max=merge_into is not None, **kw)
     return out.permute(0, 3, 1, 2)
 
 

@@ -76,6 +76,53 @@ def test_conv2d_f16x3_vs_fp64(N, C, H, W, Co, k, s, p):
     assert torch.equal(got3, got)
 
 
+@pytest.mark.parametrize("N,C,H,W,Co,k,s,p", [(1, 1024, 18, 18, 256, 3, 1, 1), (2, 1024, 18, 18, 512, 3, 1, 1),
+                                             (3, 512, 18, 18, 256, 1, 1, 0), (1, 256, 35, 33, 128, 3, 2, 1)])
+def test_conv2d_f16x3_groups_and_splitk(N, C, H, W, Co, k, s, p):
+    """The grouped launch (the two backbones' twin layers, mmt_conv2d_f16x3_groups) with its K split in slices
+    (few output tiles): each group's output against float64 within 1e-5 of its scale, each group's max words
+    exactly its max|y|, split vs unsplit within 1e-5 (the slices change the fp32 summation order), and a
+    split launch that max-merges into an existing map (MMT_CONV_MAX in the slice-reduce kernel)."""
+    import ctypes
+    from mmtrack_amd import _lib, dimpnet
+    lib = _lib.load()
+    assert lib.mmt_conv2d_f16x3_ws_bytes(N, H, W, C, Co, k, k, s, p, 2) > 0, "shape expected to split"
+    g = torch.Generator().manual_seed(N * 7 + C + Co + k)
+    xs = [torch.randn(N, C, H, W, generator=g) * (1.0 + 2 * i) for i in range(2)]
+    ws = [torch.randn(Co, C, k, k, generator=g) / math.sqrt(C * k * k) for _ in range(2)]
+    bs = [torch.randn(Co, generator=g) * 0.1 for _ in range(2)]
+    convs = [dimpnet._Conv(ws[i], bias=bs[i], stride=s, pad=p, dev="cuda", f16x3=True) for i in range(2)]
+    Ho, Wo = convs[0].out_hw(H, W)
+    refs = [F.conv2d(xs[i].double(), ws[i].double(), bs[i].double(), stride=s, padding=p) for i in range(2)]
+    rs = [torch.randn(refs[0].shape, generator=g) for _ in range(2)]
+    xd = [x.permute(0, 2, 3, 1).contiguous().cuda() for x in xs]
+    rd = [r.permute(0, 2, 3, 1).contiguous().cuda() for r in rs]
+    outs = [torch.empty(N, Ho, Wo, Co, device="cuda") for _ in range(2)]
+    words = [torch.zeros(lib.mmt_conv_max_words(), device="cuda") for _ in range(2)]
+    groups = [convs[i].group(xd[i], outs[i], relu=True, resid=rd[i], x_scale=dimpnet.range_scale(float(xs[i].abs().max())),
+                             y_max=words[i]) for i in range(2)]
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    wsf = lambda n: torch.empty((n + 3) // 4, device="cuda")
+    dimpnet.run_f16x3(lib, convs[0], groups, N, H, W, wsf, stream)
+    for i in range(2):
+        got = outs[i].permute(0, 3, 1, 2).cpu()
+        close(got, F.relu(refs[i] + rs[i].double()), 1e-5)
+        assert float(words[i].max()) == float(got.abs().max())
+    # the same conv split and unsplit
+    one = dimpnet.conv2d(xs[0].cuda(), ws[0], bias=bs[0], stride=s, pad=p, precision="f16x3").cpu()
+    spl = dimpnet.conv2d(xs[0].cuda(), ws[0], bias=bs[0], stride=s, pad=p, precision="f16x3", split=True).cpu()
+    close(spl, refs[0], 1e-5)
+    close(one, spl, 1e-5)
+    # a split launch max-merging into group 0's map
+    base = outs[0].clone()
+    merged = dimpnet.conv2d(xs[1].cuda(), ws[1], bias=bs[1], stride=s, pad=p, precision="f16x3", split=True,
+                            merge_into=base).cpu()
+    close(merged, torch.maximum(F.relu(refs[0] + rs[0].double()), refs[1]), 1e-5)
+    # twin layers writing the same output, or merging, are refused
+    bad = (_lib.MmtConvGroup * 2)(groups[0], groups[0])
+    assert lib.mmt_conv2d_f16x3_groups(bad, 2, N, H, W, C, convs[0].kp, Co, k, k, s, p, None, 0, stream) == -1
+
+
 def test_conv2d_stem_w4():
     """The 3-channel stem through MMT_CONV_W4 (weights padded to 4 channels per tap) and through the generic
     per-element path agree with torch and each other (summation orders differ: fp32 rounding)."""
@@ -130,8 +177,10 @@ def test_maxpool_l2norm_prroi():
     o_nchw = torch.empty(3, 512, 18, 18, device="cuda")
     o_nhwc = torch.empty(3, 18, 18, 512, device="cuda")
     sc = math.sqrt(1.0 / (512 * 16))
+    l2ws = torch.empty(lib.mmt_instance_l2norm_ws_bytes(3, 18, 18) // 4, device="cuda")
     assert lib.mmt_instance_l2norm(ctypes.c_void_p(fd.data_ptr()), 3, 18, 18, 512, sc, 1e-5,
-                                   ctypes.c_void_p(o_nhwc.data_ptr()), ctypes.c_void_p(o_nchw.data_ptr()), s) == 0
+                                   ctypes.c_void_p(o_nhwc.data_ptr()), ctypes.c_void_p(o_nchw.data_ptr()),
+                                   ctypes.c_void_p(l2ws.data_ptr()), s) == 0
     ref = odn.instance_l2norm(f, sc)
     close(o_nchw.cpu(), ref, 1e-5)
     close(o_nhwc.permute(0, 3, 1, 2).cpu(), ref, 1e-5)
