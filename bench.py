@@ -425,6 +425,10 @@ def dimp_main(args, rank, world, dist):
             "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": None,
             "flop_per_launch_group": flops, "avg_batch_ms": round(feat_ms, 4),
+            # the feature net is partly HBM-bound (fp32 activations, 1x1 convs of K = 64..256): its per-layer
+            # roofline (sum over layers of max(FLOPs / peak, min bytes / 8 TB/s)) and the fraction of it reached
+            "layer_roofline_ms": round(net.roofline_ms(B, peak, PEAK_HBM_GBS / 1e3), 4),
+            "frac_of_layer_roofline": round(net.roofline_ms(B, peak, PEAK_HBM_GBS / 1e3) / feat_ms, 4),
             "peak_note": ("f16x3 split products (Wh*Ah + Wl*Ah + Wh*Al, fp16 MFMA at the bf16 rate): dense 2500 TF/s / 3 "
                           "of algorithmic FLOPs, fp32-faithful (the reference runs fp32)") if f16 else
                          "dense fp32 matrix (v_mfma_f32_16x16x4_f32): the DiMP path runs at the reference's fp32"}

@@ -283,6 +283,36 @@ class DiMPNet:
                 h, w = ho, wo
         return total + 2 * h * w * self.clf.cout * 9 * self.clf.cin
 
+    def layer_work(self, H=288, W=288):
+        """(FLOPs, minimum HBM bytes) of every conv and max-pool of extract_backbone + the clf conv for one
+        [6, H, W] image: each layer's input read once, its output written once (and read back by the MAX merge),
+        the residual read, fp32 activations, f16x3 weights (hi + lo, read once per launch -- amortised over
+        the batch, so not counted per image).  The per-layer roofline of a batch is the sum over layers of
+        max(FLOPs / matrix peak, bytes / HBM bandwidth)."""
+        out = []
+        for bi, (stem, blocks) in enumerate(self.backbones):
+            h, w = stem.out_hw(H, W)
+            out.append((2 * h * w * stem.cout * stem.kh * stem.kw * stem.cin, 4 * (H * W * 3 + h * w * stem.cout)))
+            h2, w2 = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
+            out.append((0, 4 * (h * w * 64 + h2 * w2 * 64)))   # max-pool
+            h, w, cin = h2, w2, 64
+            for k, (c1, c2, c3, ds) in enumerate(blocks):
+                ho, wo = c2.out_hw(h, w)
+                out.append((2 * h * w * c1.cout * c1.cin, 4 * (h * w * cin + h * w * c1.cout)))
+                out.append((2 * ho * wo * c2.cout * 9 * c2.cin, 4 * (h * w * c2.cin + ho * wo * c2.cout)))
+                merge = bi > 0 and k == len(blocks) - 1
+                out.append((2 * ho * wo * c3.cout * c3.cin,
+                            4 * (ho * wo * c3.cin + (3 if merge else 2) * ho * wo * c3.cout)))
+                if ds is not None:
+                    out.append((2 * ho * wo * ds.cout * ds.cin, 4 * (h * w * cin + ho * wo * ds.cout)))
+                h, w, cin = ho, wo, c3.cout
+        out.append((2 * h * w * self.clf.cout * 9 * self.clf.cin, 4 * (h * w * self.clf.cin + h * w * self.clf.cout)))
+        return out
+
+    def roofline_ms(self, n, peak_tflops, hbm_tbps, H=288, W=288):
+        """The per-layer roofline time (ms) of extract_backbone + clf conv over a batch of n images."""
+        return sum(max(n * f / (peak_tflops * 1e12), n * b / (hbm_tbps * 1e12)) for f, b in self.layer_work(H, W)) * 1e3
+
     # ------------------------------------------------------------------ the network's tracker-side entry points
     def extract_backbone(self, im):
         """im: [N, 6, H, W] fp32 CUDA pixel values (0..255) -> merged layer3 NHWC [N, H/16, W/16, 1024]."""
