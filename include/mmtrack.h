@@ -326,6 +326,15 @@ int mmt_dimp_track_sample(mmt_dimp_state* states, const mmt_dimp_frame* frames, 
 int mmt_dimp_track_update(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
                           const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
                           mmt_dimp_result* results, void* hip_stream);
+/* the filter updates the frame's records ask for, decided on the device: for each of the n sequences (slots
+ * of states / results / filters, memory [n][MMT_DIMP_MEMORY][C][H][W]) results[s].num_iter Gauss-Newton steps
+ * over its first results[s].n_samples memory samples with its state's boxes and sample weights, in one
+ * launch sequence of max_iter steps (a sequence with fewer, or none, skips the rest); bitwise the filter
+ * mmt_dimp_optimize_dev gives over the same samples.  Nothing comes back to the host.                   */
+size_t mmt_dimp_track_optimize_ws_bytes(int n, int C, int H, int W, int fh, int fw, int max_iter);
+int mmt_dimp_track_optimize(const mmt_dimp_state* states, int n, const mmt_dimp_result* results, const float* memory,
+                            int C, int H, int W, float* filters, int fh, int fw, const mmt_dimp_params* p,
+                            int max_iter, void* workspace, size_t ws_bytes, void* hip_stream);
 /* mmt_dimp_optimize with the boxes and sample weights (or NULL) in device memory: no host staging and no
  * synchronisation (losses are not returned).  Strides in floats, 0 = the contiguous [I][S] layout: sample i
  * of sequence s is feat + i * feat_img_stride + s * feat_seq_stride ([C][H][W]), its box bb_dev + i *

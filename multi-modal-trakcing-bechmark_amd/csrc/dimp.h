@@ -5,7 +5,39 @@
 
 namespace mmt {
 
-constexpr int kDimpPosPerBlock = 32;   // output positions per dimp_filter workgroup (partial-sum granularity)
+#include "../../include/mmtrack.h"
+
+constexpr int kDimpStage = 24;   // staged floats per thread per chunk (6144 per workgroup and LDS buffer)
+
+// launch geometry of the correlation kernels for C channels of H x W maps and an fh x fw filter: dimp_filter
+// takes bands of RB output rows (RB * Wo <= 64 positions; partial sums per band: nbands per image * sequence)
+// and chunks of CC channels; dimp_transpose CT channels per workgroup (CT * taps <= 128)
+struct DimpGeo {
+  int Ho, Wo, RB, nbands, CC, CT, filter_stage, transpose_stage;
+};
+inline DimpGeo dimp_geo(int C, int H, int W, int fh, int fw) {
+  DimpGeo g{};
+  g.Ho = H + (fh + 1) % 2;
+  g.Wo = W + (fw + 1) % 2;
+  g.RB = g.Wo >= 64 ? 1 : 64 / g.Wo;
+  if (g.RB > g.Ho) g.RB = g.Ho;
+  g.nbands = (g.Ho + g.RB - 1) / g.RB;
+  const int T = fh * fw, Wp = g.Wo + fw - 1;
+  const int fplane = (g.RB + fh - 1) * Wp, tplane = (g.Ho + fh - 1) * Wp;
+  g.CC = 32;   // channels per chunk: a divisor of C
+  while (g.CC > 1 && (g.CC * (fplane + T) > kDimpStage * 256 || C % g.CC)) g.CC /= 2;
+  g.filter_stage = g.CC * (fplane + T);
+  g.CT = 16;   // a divisor of C
+  while (g.CT > 1 && (g.CT * T > 128 || g.CT * tplane + g.Ho * g.Wo > kDimpStage * 256 || C % g.CT)) g.CT /= 2;
+  g.transpose_stage = g.CT * tplane + g.Ho * g.Wo;
+  return g;
+}
+// the shapes the staging supports: a chunk of one channel (filter) / one channel + the residual map
+// (transpose) fits the per-thread registers, Wo <= 64
+inline bool dimp_geo_ok(int C, int H, int W, int fh, int fw) {
+  const DimpGeo g = dimp_geo(C, H, W, fh, fw);
+  return g.Wo <= 64 && g.filter_stage <= kDimpStage * 256 && g.transpose_stage <= kDimpStage * 256;
+}
 
 struct DimpMaps {                 // label / target-mask / sample-weight maps from the distance bins
   int IS, Ho, Wo, nbins;
@@ -24,7 +56,10 @@ struct DimpFilter {
   float* out;
   const float* label; const float* mask; const float* sw;
   float* smask;                   // mode 1 writes the activation derivative, mode 2 reads it
-  float* partial;                 // [I*S][ceil(Ho*Wo/256)] block partial sums of squares (or null)
+  float* partial;                 // [I*S][nbands] band partial sums of squares (or null)
+  const mmt_dimp_result* ctl;     // per-sequence steps / sample counts (device), or null: all
+  int it;                         // the Gauss-Newton step this launch belongs to (with ctl)
+  int RB, CC;                     // set by dimp_filter (dimp_geo)
 };
 struct DimpTranspose {
   const float* feat; const float* r;   // r: [I][S][Ho][Wo]
@@ -33,11 +68,16 @@ struct DimpTranspose {
   int I, S, C, H, W, fh, fw, Ho, Wo;
   float* grad;                         // [S][C][fh][fw]
   float* gsq;                          // [S][C] partial |g|^2 (or null)
+  const mmt_dimp_result* ctl;          // as DimpFilter
+  int it;
+  int CT;                              // set by dimp_transpose (dimp_geo)
 };
 struct DimpUpdate {
   float* w; const float* grad; const float* gsq; const float* sgsq;
   int I, S, C, fh, fw, nby;
   float reg, alpha_eps, step;
+  const mmt_dimp_result* ctl;     // as DimpFilter
+  int it;
 };
 
 // optimizer.py:108-125's per-sample constants, formed on the device: centers [IS][2] = ((y + h / 2) / stride - off0,

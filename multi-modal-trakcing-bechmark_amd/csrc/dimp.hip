@@ -8,8 +8,6 @@
 
 namespace mmt {
 
-constexpr int MAXT = 25;   // filter taps (<= 5x5)
-
 __global__ __launch_bounds__(256) void dimp_maps_kernel(DimpMaps m) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
   const int n = m.Ho * m.Wo;
@@ -31,58 +29,105 @@ __global__ __launch_bounds__(256) void dimp_maps_kernel(DimpMaps m) {
   m.sw[idx] = m.sqrt_sw[is] * spw;
 }
 
+// Both correlation kernels stage their operands through the LDS in double-buffered chunks: each thread
+// issues its share of the next chunk's global loads (kDimpStage registers) before it multiplies the current
+// one, so a chunk's load latency hides under the previous chunk's FMAs.  Out-of-map taps are staged as
+// zeros (the padded image), so the inner loops carry no bounds checks; a zero tap adds an exact zero.
+
 // scores[i,s,y,x] = sum_c,ky,kx feat[i,s,c,y+ky-P,x+kx-P] * w[s,c,ky,kx]; mode 1/2 epilogues below.
-// One workgroup per (image * sequence, tile of kDimpPosPerBlock output positions): the 8 wave halves
-// (32 lanes each) take interleaved channel slices (c = group + 8 k) of the same 32 positions, so a frame's
-// 15-50 samples still spread over hundreds of workgroups; the 8 partial sums combine in a fixed order.
-// FH / FW > 0: the filter size as compile-time constants (the taps unroll, so a channel's loads are all in
-// flight together; the same summation order as the generic loop)
+// One workgroup per (image * sequence, band of RB output rows, RB * Wo <= 64 positions): the 4 waves take
+// interleaved channels (c = wave + 4 k) of chunks of CC channels, every lane one output position; the 4
+// partial sums combine in a fixed order, the band's squares (mode 1 / 2) in position order into
+// partial[is][band].  ctl: sequence s skips (no output) when it >= ctl[s].num_iter or i >= n_samples.
 template <int FH, int FW>
 __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
-  extern __shared__ float wsh[];
-  __shared__ float part[8][kDimpPosPerBlock];
+  extern __shared__ float sm[];   // 2 x ([CC][rows][Wp] padded feature rows + [CC][T] weights)
+  __shared__ float red[4][64];
   if constexpr (FH > 0) {
     a.fh = FH;
     a.fw = FW;
   }
-  const int is = blockIdx.x;                  // image * S + sequence
-  const int s = is % a.S;
-  const int T = a.fh * a.fw;
-  for (int k = threadIdx.x; k < a.C * T; k += 256) wsh[k] = a.w[(int64_t)s * a.C * T + k];
-  __syncthreads();
-  const int n = a.Ho * a.Wo;
-  const int lp = threadIdx.x & (kDimpPosPerBlock - 1), cg = threadIdx.x / kDimpPosPerBlock;
-  const int p = blockIdx.y * kDimpPosPerBlock + lp;
+  const int is = blockIdx.x, band = blockIdx.y;
+  const int i = is / a.S, s = is - i * a.S;
+  if (a.ctl && (a.it >= a.ctl[s].num_iter || i >= a.ctl[s].n_samples)) return;   // uniform over the workgroup
+  const int T = a.fh * a.fw, P0 = a.fh / 2, P1 = a.fw / 2;
+  const int y0 = band * a.RB, nrow = min(a.RB, a.Ho - y0);
+  const int Wp = a.Wo + a.fw - 1, plane = (a.RB + a.fh - 1) * Wp, CC = a.CC;
+  const int fsz = CC * plane, stage = fsz + CC * T;
+  const float* f = a.feat + (int64_t)i * a.img_stride + (int64_t)s * a.seq_stride;
+  const float* wsrc = a.w + (int64_t)s * a.C * T;
+  const int nch = (a.C + CC - 1) / CC;
+  const int t = threadIdx.x;
+  // each staged element's source offset within its chunk (fixed over the chunks; -1: a zero pad tap), so a
+  // chunk's fetch is one add and one load per register
+  int soff[kDimpStage];
+#pragma unroll
+  for (int k = 0; k < kDimpStage; ++k) {
+    const int e = t + k * 256;
+    int o = -1;
+    if (e < fsz) {
+      const int c = e / plane, r = e - c * plane, py = r / Wp, px = r - py * Wp;
+      const int yy = y0 + py - P0, xx = px - P1;
+      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) o = c * a.H * a.W + yy * a.W + xx;
+    } else if (e < stage) {
+      o = e - fsz;
+    }
+    soff[k] = o;
+  }
+  float rg[kDimpStage];
+  auto fetch = [&](int ch) {
+    const float* fb = f + (int64_t)ch * CC * a.H * a.W;   // C % CC == 0 (dimp_geo)
+    const float* wb = wsrc + ch * CC * T;
+#pragma unroll
+    for (int k = 0; k < kDimpStage; ++k) {
+      const int e = t + k * 256;
+      rg[k] = soff[k] < 0 ? 0.f : (e < fsz ? fb : wb)[soff[k]];
+    }
+  };
+  auto put = [&](int buf) {
+    float* d = sm + buf * stage;
+#pragma unroll
+    for (int k = 0; k < kDimpStage; ++k) {
+      const int e = t + k * 256;
+      if (e < stage) d[e] = rg[k];
+    }
+  };
+  const int g = t >> 6, slot = t & 63;
+  const int ly = slot / a.Wo, x = slot - ly * a.Wo;
+  const bool pv = slot < nrow * a.Wo;
   float acc = 0.f;
-  if (p < n) {
-    const int y = p / a.Wo, x = p - y * a.Wo;
-    const int P0 = a.fh / 2, P1 = a.fw / 2;
-    const float* f = a.feat + (int64_t)(is / a.S) * a.img_stride + (int64_t)s * a.seq_stride;
-#pragma unroll 4
-    for (int c = cg; c < a.C; c += 8) {
-      const float* fc = f + (int64_t)c * a.H * a.W;
-      const float* wc = wsh + c * T;
+  fetch(0);
+  put(0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    if (ch + 1 < nch) fetch(ch + 1);
+    const float* sf = sm + (ch & 1) * stage;
+    const float* sw = sf + fsz;
+    if (pv) {
+      for (int c = g; c < CC; c += 4) {
+        const float* fp = sf + c * plane + ly * Wp + x;
+        const float* wp = sw + c * T;
+        if constexpr (FH > 0) {
 #pragma unroll
-      for (int ky = 0; ky < (FH > 0 ? FH : a.fh); ++ky) {
-        const int yy = y + ky - P0;
-        if (yy < 0 || yy >= a.H) continue;
+          for (int ky = 0; ky < FH; ++ky)
 #pragma unroll
-        for (int kx = 0; kx < (FW > 0 ? FW : a.fw); ++kx) {
-          const int xx = x + kx - P1;
-          if (xx < 0 || xx >= a.W) continue;
-          acc += fc[yy * a.W + xx] * wc[ky * a.fw + kx];
+            for (int kx = 0; kx < FW; ++kx) acc += fp[ky * Wp + kx] * wp[ky * FW + kx];
+        } else {
+          for (int ky = 0; ky < a.fh; ++ky)
+            for (int kx = 0; kx < a.fw; ++kx) acc += fp[ky * Wp + kx] * wp[ky * a.fw + kx];
         }
       }
     }
+    if (ch + 1 < nch) put((ch + 1) & 1);
+    __syncthreads();
   }
-  part[cg][lp] = acc;
+  red[g][slot] = acc;
   __syncthreads();
   float r2 = 0.f;
-  if (cg == 0 && p < n) {
-    acc = part[0][lp];
-#pragma unroll
-    for (int g = 1; g < 8; ++g) acc += part[g][lp];
-    const int64_t o = (int64_t)is * n + p;
+  if (g == 0 && pv) {
+    acc = ((red[0][slot] + red[1][slot]) + red[2][slot]) + red[3][slot];
+    const int npos = a.Ho * a.Wo;
+    const int64_t o = (int64_t)is * npos + (y0 + ly) * a.Wo + x;
     if (a.mode == 0) {
       a.out[o] = acc;
     } else if (a.mode == 1) {            // residuals (optimizer.py:137-146)
@@ -95,59 +140,118 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
       if (a.smask) a.smask[o] = dm;
       r2 = r * r;
     } else {                              // scores_grad (optimizer.py:151-152)
-      const float g = a.sw[o] * (a.smask[o] * acc);
-      r2 = g * g;
+      const float gs = a.sw[o] * (a.smask[o] * acc);
+      r2 = gs * gs;
     }
   }
   if (!a.partial) return;   // uniform over the workgroup
-  __syncthreads();          // every group has read its sums
-  if (cg == 0) part[0][lp] = r2;
+  __syncthreads();          // every group has read the sums
+  if (g == 0) red[0][slot] = r2;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int k = 0; k < kDimpPosPerBlock; ++k) t += part[0][k];
-    a.partial[(int64_t)is * gridDim.y + blockIdx.y] = t;
+  if (t == 0) {
+    float tot = 0.f;
+    for (int k = 0; k < nrow * a.Wo; ++k) tot += red[0][k];
+    a.partial[(int64_t)is * gridDim.y + band] = tot;
   }
 }
 
-// grad[s,c,ky,kx] = sum_i,y,x r[i,s,y,x] * feat[i,s,c,y+ky-P,x+kx-P] (+ reg * w), one block per (s, c)
+// grad[s,c,ky,kx] = sum_i,y,x r[i,s,y,x] * feat[i,s,c,y+ky-P,x+kx-P] (+ reg * w).  One workgroup per
+// (sequence, CT channels), looping over the samples i < I (ctl: < n_samples; the sequence skips when it >=
+// num_iter): the sample's padded planes of the CT channels and its residual map are staged double-buffered;
+// G = 256 / (CT T) threads per (channel, tap) take interleaved positions, combined in a fixed order.
+template <int FH, int FW>
 __global__ __launch_bounds__(256) void dimp_transpose_kernel(DimpTranspose a) {
-  __shared__ float red[256][MAXT + 1];
-  const int s = blockIdx.x / a.C, c = blockIdx.x % a.C;
-  const int T = a.fh * a.fw, n = a.Ho * a.Wo;
-  const int P0 = a.fh / 2, P1 = a.fw / 2;
-  float acc[MAXT];
-#pragma unroll
-  for (int t = 0; t < MAXT; ++t) acc[t] = 0.f;
-  for (int q = threadIdx.x; q < a.I * n; q += 256) {
-    const int i = q / n, p = q - i * n;
-    const int y = p / a.Wo, x = p - y * a.Wo;
-    const float r = a.r[((int64_t)i * a.S + s) * n + p];
-    const float* fc = a.feat + (int64_t)i * a.img_stride + (int64_t)s * a.seq_stride + (int64_t)c * a.H * a.W;
-#pragma unroll
-    for (int t = 0; t < MAXT; ++t) {
-      if (t >= T) break;
-      const int ky = t / a.fw, kx = t - ky * a.fw;
-      const int yy = y + ky - P0, xx = x + kx - P1;
-      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) acc[t] += r * fc[yy * a.W + xx];
-    }
+  extern __shared__ float sm[];   // 2 x ([CT][Hp][Wp] padded planes + [npos] residuals)
+  __shared__ float red[256];
+  if constexpr (FH > 0) {
+    a.fh = FH;
+    a.fw = FW;
   }
-  for (int t = 0; t < T; ++t) red[threadIdx.x][t] = acc[t];
+  const int s = blockIdx.x, c0 = blockIdx.y * a.CT;
+  if (a.ctl && a.it >= a.ctl[s].num_iter) return;
+  const int nI = a.ctl ? min(a.I, a.ctl[s].n_samples) : a.I;
+  const int T = a.fh * a.fw, P0 = a.fh / 2, P1 = a.fw / 2, npos = a.Ho * a.Wo;
+  const int Wp = a.Wo + a.fw - 1, plane = (a.Ho + a.fh - 1) * Wp, CT = a.CT;
+  const int fsz = CT * plane, stage = fsz + npos;
+  const int t = threadIdx.x;
+  int soff[kDimpStage];   // as dimp_filter_kernel: fixed over the samples
+#pragma unroll
+  for (int k = 0; k < kDimpStage; ++k) {
+    const int e = t + k * 256;
+    int o = -1;
+    if (e < fsz) {
+      const int c = e / plane, r = e - c * plane, py = r / Wp, px = r - py * Wp;
+      const int yy = py - P0, xx = px - P1;
+      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) o = (c0 + c) * a.H * a.W + yy * a.W + xx;
+    } else if (e < stage) {
+      o = e - fsz;
+    }
+    soff[k] = o;
+  }
+  float rg[kDimpStage];
+  auto fetch = [&](int i) {
+    const float* f = a.feat + (int64_t)i * a.img_stride + (int64_t)s * a.seq_stride;
+    const float* rs = a.r + ((int64_t)i * a.S + s) * npos;
+#pragma unroll
+    for (int k = 0; k < kDimpStage; ++k) {
+      const int e = t + k * 256;
+      rg[k] = soff[k] < 0 ? 0.f : (e < fsz ? f : rs)[soff[k]];
+    }
+  };
+  auto put = [&](int buf) {
+    float* d = sm + buf * stage;
+#pragma unroll
+    for (int k = 0; k < kDimpStage; ++k) {
+      const int e = t + k * 256;
+      if (e < stage) d[e] = rg[k];
+    }
+  };
+  const int G = 256 / (CT * T);
+  const int pair = t / G, sub = t - pair * G;
+  const bool active = pair < CT * T;
+  const int c = pair / T, tt = pair - c * T, ky = tt / a.fw, kx = tt - ky * a.fw;
+  float acc = 0.f;
+  if (nI > 0) {
+    fetch(0);
+    put(0);
+  }
   __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
-    if (threadIdx.x < st)
-      for (int t = 0; t < T; ++t) red[threadIdx.x][t] += red[threadIdx.x + st][t];
+  for (int i = 0; i < nI; ++i) {
+    if (i + 1 < nI) fetch(i + 1);
+    const float* sf = sm + (i & 1) * stage;
+    const float* sr = sf + fsz;
+    if (active) {
+      const float* fp = sf + c * plane + ky * Wp + kx;
+      int y = sub / a.Wo, x = sub - y * a.Wo;
+      for (int p = sub; p < npos; p += G) {
+        acc += sr[p] * fp[y * Wp + x];
+        x += G;
+        while (x >= a.Wo) {
+          x -= a.Wo;
+          ++y;
+        }
+      }
+    }
+    if (i + 1 < nI) put((i + 1) & 1);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  red[t] = acc;
+  __syncthreads();
+  float gv = 0.f;
+  const bool own = t < CT * T && c0 + t / T < a.C;
+  if (own) {
+    for (int u = 0; u < G; ++u) gv += red[t * G + u];
+    const int64_t o = ((int64_t)s * a.C + c0) * T + t;
+    gv += a.w ? a.reg * a.w[o] : 0.f;
+    a.grad[o] = gv;
+  }
+  __syncthreads();
+  if (own) red[t] = gv;
+  __syncthreads();
+  if (a.gsq && t < CT && c0 + t < a.C) {
     float sq = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const int64_t o = ((int64_t)s * a.C + c) * T + t;
-      const float g = red[0][t] + (a.w ? a.reg * a.w[o] : 0.f);
-      a.grad[o] = g;
-      sq += g * g;
-    }
-    if (a.gsq) a.gsq[(int64_t)s * a.C + c] = sq;
+    for (int k = 0; k < T; ++k) sq += red[t * T + k] * red[t * T + k];
+    a.gsq[(int64_t)s * a.C + c0 + t] = sq;
   }
 }
 
@@ -156,6 +260,8 @@ __global__ __launch_bounds__(256) void dimp_update_kernel(DimpUpdate a) {
   __shared__ float red[256];
   __shared__ float num_sh, den_sh;
   const int s = blockIdx.x;
+  if (a.ctl && a.it >= a.ctl[s].num_iter) return;
+  const int nI = a.ctl ? min(a.I, a.ctl[s].n_samples) : a.I;
   float v = 0.f;
   for (int c = threadIdx.x; c < a.C; c += 256) v += a.gsq[(int64_t)s * a.C + c];
   red[threadIdx.x] = v;
@@ -167,7 +273,7 @@ __global__ __launch_bounds__(256) void dimp_update_kernel(DimpUpdate a) {
   if (threadIdx.x == 0) num_sh = red[0];
   __syncthreads();
   v = 0.f;
-  for (int k = threadIdx.x; k < a.I * a.nby; k += 256) {
+  for (int k = threadIdx.x; k < nI * a.nby; k += 256) {
     const int i = k / a.nby, by = k - i * a.nby;
     v += a.sgsq[((int64_t)i * a.S + s) * a.nby + by];
   }
@@ -245,16 +351,28 @@ void dimp_maps(const DimpMaps& m, hipStream_t s) {
   const int n = m.IS * m.Ho * m.Wo;
   hipLaunchKernelGGL(dimp_maps_kernel, dim3((n + 255) / 256), dim3(256), 0, s, m);
 }
-void dimp_filter(const DimpFilter& a, hipStream_t s) {
-  const int nby = (a.Ho * a.Wo + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
-  const size_t lds = a.C * a.fh * a.fw * sizeof(float);
+void dimp_filter(const DimpFilter& a_, hipStream_t s) {
+  DimpFilter a = a_;
+  const DimpGeo g = dimp_geo(a.C, a.H, a.W, a.fh, a.fw);
+  a.RB = g.RB;
+  a.CC = g.CC;
+  const size_t lds = 2 * (size_t)g.filter_stage * sizeof(float);
+  const dim3 grid(a.I * a.S, g.nbands);
   if (a.fh == 4 && a.fw == 4)
-    hipLaunchKernelGGL((dimp_filter_kernel<4, 4>), dim3(a.I * a.S, nby), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((dimp_filter_kernel<4, 4>), grid, dim3(256), lds, s, a);
   else
-    hipLaunchKernelGGL((dimp_filter_kernel<0, 0>), dim3(a.I * a.S, nby), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((dimp_filter_kernel<0, 0>), grid, dim3(256), lds, s, a);
 }
-void dimp_transpose(const DimpTranspose& a, hipStream_t s) {
-  hipLaunchKernelGGL(dimp_transpose_kernel, dim3(a.S * a.C), dim3(256), 0, s, a);
+void dimp_transpose(const DimpTranspose& a_, hipStream_t s) {
+  DimpTranspose a = a_;
+  const DimpGeo g = dimp_geo(a.C, a.H, a.W, a.fh, a.fw);
+  a.CT = g.CT;
+  const size_t lds = 2 * (size_t)g.transpose_stage * sizeof(float);
+  const dim3 grid(a.S, (a.C + g.CT - 1) / g.CT);
+  if (a.fh == 4 && a.fw == 4)
+    hipLaunchKernelGGL((dimp_transpose_kernel<4, 4>), grid, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((dimp_transpose_kernel<0, 0>), grid, dim3(256), lds, s, a);
 }
 void dimp_update(const DimpUpdate& a, hipStream_t s) {
   hipLaunchKernelGGL(dimp_update_kernel, dim3(a.S), dim3(256), 0, s, a);

@@ -19,7 +19,7 @@ struct WsLayout {
 
 WsLayout layout(int I, int S, int C, int H, int W, int fh, int fw, int num_iter) {
   const size_t Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, n = Ho * Wo, IS = (size_t)I * S;
-  const size_t nby = (n + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
+  const size_t nby = dimp_geo(C, H, W, fh, fw).nbands;
   WsLayout L{};
   size_t off = 0;
   auto take = [&](size_t floats) {
@@ -46,7 +46,8 @@ WsLayout layout(int I, int S, int C, int H, int W, int fh, int fw, int num_iter)
 }
 
 bool bad_dims(int I, int S, int C, int H, int W, int fh, int fw) {
-  return I <= 0 || S <= 0 || C <= 0 || H <= 0 || W <= 0 || fh <= 0 || fw <= 0 || fh * fw > 25 || C * fh * fw > 15360;   // weight tile in LDS <= 60 KB
+  return I <= 0 || S <= 0 || C <= 0 || H <= 0 || W <= 0 || fh <= 0 || fw <= 0 || fh * fw > 25 ||
+         !dimp_geo_ok(C, H, W, fh, fw);
 }
 
 }  // namespace
@@ -92,12 +93,13 @@ int mmt_dimp_feat_transpose(const float* feat, const float* r, float* grad, int 
 }
 
 // the Gauss-Newton loop of mmt_dimp_optimize / _dev once the per-sample constants are in the workspace
+// ctl: per-sequence steps / sample counts in device memory (null: num_iter steps over all I samples)
 static int optimize_body(const float* feat, int64_t img_stride, int64_t seq_stride, int I, int S, int C, int H, int W,
                          float* weights, int fh, int fw, const mmt_dimp_params* p, int num_iter, char* ws,
-                         const WsLayout& L, float* losses, hipStream_t st) {
+                         const WsLayout& L, float* losses, hipStream_t st, const mmt_dimp_result* ctl = nullptr) {
   auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
   const int IS = I * S;
-  const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, nby = (Ho * Wo + kDimpPosPerBlock - 1) / kDimpPosPerBlock;
+  const int Ho = H + (fh + 1) % 2, Wo = W + (fw + 1) % 2, nby = dimp_geo(C, H, W, fh, fw).nbands;
   const float step = std::exp(p->log_step_length);
   const float reg = std::fmax(p->filter_reg * p->filter_reg, p->min_filter_reg * p->min_filter_reg);
 
@@ -114,6 +116,7 @@ static int optimize_body(const float* feat, int64_t img_stride, int64_t seq_stri
   fa.mask = F(L.mask);
   fa.sw = F(L.sw);
   fa.smask = F(L.smask);
+  fa.ctl = ctl;
   DimpTranspose ta{};
   ta.feat = feat;
   ta.img_stride = img_stride;
@@ -124,9 +127,11 @@ static int optimize_body(const float* feat, int64_t img_stride, int64_t seq_stri
   ta.I = I; ta.S = S; ta.C = C; ta.H = H; ta.W = W; ta.fh = fh; ta.fw = fw; ta.Ho = Ho; ta.Wo = Wo;
   ta.grad = F(L.grad);
   ta.gsq = F(L.gsq);
-  DimpUpdate ua{weights, F(L.grad), F(L.gsq), F(L.sgsq), I, S, C, fh, fw, nby, reg, p->alpha_eps, step};
+  ta.ctl = ctl;
+  DimpUpdate ua{weights, F(L.grad), F(L.gsq), F(L.sgsq), I, S, C, fh, fw, nby, reg, p->alpha_eps, step, ctl, 0};
   const int nw = S * C * fh * fw;
   for (int it = 0; it < num_iter; ++it) {
+    fa.it = ta.it = ua.it = it;
     fa.mode = 1;               // residuals at the current filter
     fa.w = weights;
     fa.out = F(L.rm);
@@ -228,6 +233,39 @@ int mmt_dimp_optimize_dev(const float* feat, int64_t feat_img_stride, int64_t fe
   dimp_params(pr, st);
   return optimize_body(feat, feat_img_stride, feat_seq_stride, I, S, C, H, W, weights, fh, fw, p, num_iter, ws, L,
                        nullptr, st);
+}
+
+size_t mmt_dimp_track_optimize_ws_bytes(int n, int C, int H, int W, int fh, int fw, int max_iter) {
+  return mmt_dimp_workspace_bytes(MMT_DIMP_MEMORY, n, C, H, W, fh, fw, max_iter);
+}
+
+int mmt_dimp_track_optimize(const mmt_dimp_state* states, int n, const mmt_dimp_result* results, const float* memory,
+                            int C, int H, int W, float* filters, int fh, int fw, const mmt_dimp_params* p, int max_iter,
+                            void* workspace, size_t ws_bytes, void* stream_) {
+  constexpr int I = MMT_DIMP_MEMORY;
+  if (!states || !results || !memory || !filters || !p || !workspace || n <= 0 || max_iter < 0 ||
+      bad_dims(I, n, C, H, W, fh, fw) || p->num_dist_bins <= 0 || p->num_dist_bins > 128)
+    return MMT_E_ARG;
+  const WsLayout L = layout(I, n, C, H, W, fh, fw, max_iter);
+  if (ws_bytes < L.total) return MMT_E_ARG;
+  if (max_iter == 0) return MMT_OK;
+  hipStream_t st = (hipStream_t)stream_;
+  char* ws = static_cast<char*>(workspace);
+  auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
+  const int64_t chw = (int64_t)C * H * W, sf = (int64_t)(sizeof(mmt_dimp_state) / sizeof(float));
+  static_assert(sizeof(mmt_dimp_state) % sizeof(float) == 0, "state stride in floats");
+  // every sequence's boxes / weights in its state, its samples in its memory slot ([n][I][C][H][W])
+  DimpPrep pp{states->target_boxes[0], states->sample_weights, 4, sf, 1, sf, I * n, I, n, p->feat_stride,
+              (float)(fh % 2) / 2.0f, (float)(fw % 2) / 2.0f, F(L.centers), F(L.sqrtsw)};
+  dimp_prep(pp, st);
+  DimpParamArgs pr{};
+  std::memcpy(pr.v, p->label_w, 128 * 4);
+  std::memcpy(pr.v + 128, p->mask_w, 128 * 4);
+  std::memcpy(pr.v + 256, p->spatial_w, 128 * 4);
+  pr.dst = F(L.params);
+  dimp_params(pr, st);
+  return optimize_body(memory, chw, I * chw, I, n, C, H, W, filters, fh, fw, p, max_iter, ws, L, nullptr, st,
+                       results);
 }
 
 }  // extern "C"

@@ -167,6 +167,9 @@ SIGNATURES = {
     "mmt_dimp_optimize_dev": (_I, [_P, _I64, _I64, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I64, _I64, _P, _I64, _I64,
                                    ctypes.POINTER(MmtDimpParams), _I, _P, ctypes.c_size_t, _P]),
     "mmt_dimp_state_bytes": (ctypes.c_size_t, []),
+    "mmt_dimp_track_optimize_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I]),
+    "mmt_dimp_track_optimize": (_I, [_P, _I, _P, _P, _I, _I, _I, _P, _I, _I, ctypes.POINTER(MmtDimpParams), _I, _P,
+                                     ctypes.c_size_t, _P]),
     "mmt_dimp_track_sample": (_I, [_P, _P, _I, ctypes.POINTER(MmtDimpTrackParams), _I, _I, _P, _P]),
     "mmt_dimp_track_update": (_I, [_P, _I, _P, _I, _I, ctypes.POINTER(MmtDimpTrackParams), _P, _I64, _P, _P, _P]),
     "mmt_gemm_stamps": (_I, [_P]),

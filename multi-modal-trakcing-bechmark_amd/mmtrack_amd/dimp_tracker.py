@@ -310,13 +310,6 @@ class DiMP:
         self.debug_info = {'flag': flag, 'max_score': float(res.max_score)}
         return {'target_bbox': [float(v) for v in res.box], 'confidence': float(res.max_score)}
 
-    def _update_filter(self, res):
-        """update_classifier's Gauss-Newton steps (dimp.py:555-570) when the frame's record asks for them: the
-        filter is optimised in place over the slot's memory samples, boxes and weights (all on the device)."""
-        if res.num_iter > 0:
-            self.pool.update_filters(self.slot, 1, res.n_samples, res.num_iter, self.optimizer)
-
-
 FLAGS = ('normal', 'not_found', 'uncertain', 'hard_negative')
 
 
@@ -373,7 +366,11 @@ class DimpPool:
         self.tparams = p
         self.frames_host = (_lib.MmtDimpFrame * capacity)()
         self.frames = torch.empty(capacity * ctypes.sizeof(_lib.MmtDimpFrame), dtype=torch.uint8, device=self.dev)
-        self.res_host = torch.empty(capacity * self.rbytes, dtype=torch.uint8, pin_memory=True)
+        # two pinned record buffers: frame k + 1 may be launched (its records copied) before frame k's are read
+        self.res_host = [torch.empty(capacity * self.rbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self._parity = {}   # per first slot: the record buffer its next launch uses
+        self.max_iter = max(p.net_opt_update_iter, p.net_opt_hn_iter, p.net_opt_low_iter) if p.update_classifier else 0
+        self._opt_ws = None
 
     def alloc(self):
         if self.next >= self.cap:
@@ -405,18 +402,8 @@ class DimpPool:
         self.filters[slot] = w[0]
         return self.filters[slot:slot + 1]
 
-    def update_filters(self, first, n, n_samples, num_iter, optimizer):
-        """num_iter Gauss-Newton steps on the filters of slots [first, first + n) in one optimiser call over their
-        memories ([n][50] samples read in place through strides) and device boxes / weights: I = the largest
-        stored-sample count; a slot's samples beyond its own count have weight 0 and add exact zeros, so each
-        filter is the one a call over its own samples gives (mmt_dimp_optimize_dev)."""
-        feat = self.memory[first:first + n, :n_samples].transpose(0, 1)   # [I][S][C][h][w]
-        sf = self.sbytes // 4   # the state stride in floats
-        optimizer.optimize_dev(self.filters[first:first + n], feat, self.boxes_ptr(first), self.weights_ptr(first),
-                               num_iter, bb_strides=(4, sf), sw_strides=(1, sf))
-
-    def result(self, slot):
-        return _lib.MmtDimpResult.from_buffer_copy(bytes(self.res_host[slot * self.rbytes:(slot + 1) * self.rbytes]
+    def result(self, slot, buf=0):
+        return _lib.MmtDimpResult.from_buffer_copy(bytes(self.res_host[buf][slot * self.rbytes:(slot + 1) * self.rbytes]
                                                          .numpy()))
 
     def launch(self, trackers, frames, first):
@@ -451,28 +438,37 @@ class DimpPool:
                                        ctypes.c_void_p(self.results.data_ptr() + first * self.rbytes), stream)
         if rc != 0:
             raise RuntimeError(f"mmt_dimp_track_update failed ({rc})")
-        self.res_host[first * self.rbytes:(first + n) * self.rbytes].copy_(
+        # update_classifier's Gauss-Newton steps where the records ask for them (dimp.py:555-570), decided on
+        # the device: one launch sequence over the batch, no host round trip
+        if self.max_iter > 0:
+            opt = trackers[0].optimizer
+            C, h, w = self.memory.shape[2:]
+            fh, fw = self.filters.shape[-2:]
+            nbytes = lib.mmt_dimp_track_optimize_ws_bytes(n, C, h, w, fh, fw, self.max_iter)
+            if self._opt_ws is None or self._opt_ws.numel() < nbytes:
+                self._opt_ws = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+            rc = lib.mmt_dimp_track_optimize(ctypes.c_void_p(self.state_ptr(first)), n,
+                                             ctypes.c_void_p(self.results.data_ptr() + first * self.rbytes),
+                                             ctypes.c_void_p(self.memory[first].data_ptr()), C, h, w,
+                                             ctypes.c_void_p(self.filters[first].data_ptr()), fh, fw,
+                                             ctypes.byref(opt.params), self.max_iter,
+                                             ctypes.c_void_p(self._opt_ws.data_ptr()), nbytes, stream)
+            if rc != 0:
+                raise RuntimeError(f"mmt_dimp_track_optimize failed ({rc})")
+        buf = self._parity.get(first, 0)
+        self._parity[first] = buf ^ 1
+        self.res_host[buf][first * self.rbytes:(first + n) * self.rbytes].copy_(
             self.results[first * self.rbytes:(first + n) * self.rbytes], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return ev, fr
+        return ev, buf
 
-    def finish(self, trackers, first, ev):
-        """Wait for the records, launch the filter updates they ask for, return the per-tracker outputs."""
+    def finish(self, trackers, first, ticket):
+        """Wait for a launch's records (its filter updates are already queued on the device) and return the
+        per-tracker outputs."""
+        ev, buf = ticket
         ev.synchronize()
-        recs = [self.result(first + i) for i in range(len(trackers))]
-        # the filter updates the records ask for, batched over runs of consecutive slots with the same number of
-        # steps (one optimiser call per run instead of one per sequence)
-        i = 0
-        while i < len(recs):
-            k = recs[i].num_iter
-            j = i + 1
-            while j < len(recs) and recs[j].num_iter == k:
-                j += 1
-            if k > 0:
-                self.update_filters(first + i, j - i, max(r.n_samples for r in recs[i:j]), k, trackers[i].optimizer)
-            i = j
-        return [t._output(res) for t, res in zip(trackers, recs)]
+        return [t._output(self.result(first + i, buf)) for i, t in enumerate(trackers)]
 
 
 def _slots(trackers):
@@ -498,19 +494,20 @@ def track_batch(trackers, frames):
         i = j
     launched = [(a, b, trackers[a].pool.launch(trackers[a:b], frames[a:b], trackers[a].slot)) for a, b in runs]
     outs = []
-    for a, b, (ev, _fr) in launched:
-        outs.extend(trackers[a].pool.finish(trackers[a:b], trackers[a].slot, ev))
+    for a, b, ticket in launched:
+        outs.extend(trackers[a].pool.finish(trackers[a:b], trackers[a].slot, ticket))
     return outs
 
 
 class PipelinedBatch:
-    """track_batch with the host half of one group of sequences overlapped with the device half of the other:
-    the trackers are split into two groups; group g's frame k is launched (asynchronously, its result records
-    copied to pinned host memory behind an event) while the host reads group 1 - g's records of frame k - 1
-    and launches the filter updates they ask for.  Per-sequence results are identical to track_batch (each
-    tracker still sees its frames in order; only the interleaving of different sequences' work changes)."""
+    """track_batch with the host one frame behind the device: frame k of every group of sequences is launched
+    (asynchronously -- the state machine and the filter updates run on the device, the result records are
+    copied to pinned host memory behind an event) before the host reads frame k - 1's records, so the device
+    always has the next frame queued.  groups > 1 splits the sequences into launches of their own.
+    Per-sequence results are identical to track_batch (each tracker sees its frames in order; only the
+    interleaving of different sequences' work changes)."""
 
-    def __init__(self, trackers, groups=2):
+    def __init__(self, trackers, groups=1):
         self.trackers = trackers
         n = len(trackers)
         bounds = [round(i * n / groups) for i in range(groups + 1)]
@@ -522,15 +519,13 @@ class PipelinedBatch:
         idx = self.groups[g]
         trs = [self.trackers[i] for i in idx]
         pool, first = _slots(trs)
-        ev, fr = pool.launch(trs, [frames[i] for i in idx], first)
-        self.pending[g] = (idx, ev, fr)
+        self.pending[g] = pool.launch(trs, [frames[i] for i in idx], first)
 
-    def _finish(self, g, outs):
-        idx, ev, _fr = self.pending[g]
-        self.pending[g] = None
+    def _finish(self, g, ticket, outs):
+        idx = self.groups[g]
         trs = [self.trackers[i] for i in idx]
         pool, first = _slots(trs)
-        for i, o in zip(idx, pool.finish(trs, first, ev)):
+        for i, o in zip(idx, pool.finish(trs, first, ticket)):
             outs[i] = o
 
     def step(self, frames):
@@ -538,16 +533,18 @@ class PipelinedBatch:
         outs = [None] * len(self.trackers)
         had = self.pending[0] is not None
         for g in range(len(self.groups)):
-            if self.pending[g] is not None:
-                self._finish(g, outs)
+            prev = self.pending[g]
             self._start(g, frames)
+            if prev is not None:
+                self._finish(g, prev, outs)
         return outs if had else None
 
     def flush(self):
         outs = [None] * len(self.trackers)
         for g in range(len(self.groups)):
             if self.pending[g] is not None:
-                self._finish(g, outs)
+                self._finish(g, self.pending[g], outs)
+                self.pending[g] = None
         return outs
 
 

@@ -83,3 +83,62 @@ def test_errors():
         dimp.apply_filter(torch.zeros(1, 2, 4, 8, 8).cuda(), torch.zeros(1, 4, 3, 3).cuda())   # S mismatch
     with pytest.raises(ValueError):
         dimp.apply_filter(torch.zeros(1, 1, 4, 8, 8).cuda(), torch.zeros(1, 4, 7, 7).cuda())   # > 25 taps
+
+
+def test_track_optimize_matches_per_sequence():
+    """mmt_dimp_track_optimize (the tracker's filter updates decided on the device: per-sequence step counts and
+    sample counts read from the result records, boxes / weights from the states, samples from the pool memory
+    through strides) gives bit for bit the filter of a separate mmt_dimp_optimize call over each sequence's own
+    samples; a sequence asking for no steps keeps its filter."""
+    import ctypes
+
+    from mmtrack_amd import _lib, dimp
+    lib = _lib.load()
+    n, C, H, W, fk, I = 3, 512, 18, 18, 4, _lib.MMT_DIMP_MEMORY
+    steps, counts = [2, 0, 1], [50, 20, 35]
+    g = torch.Generator().manual_seed(91)
+    mem = (torch.randn(n, I, C, H, W, generator=g) * 0.5).cuda()
+    filt = torch.randn(n, C, fk, fk, generator=g) * 0.02
+    bb = torch.rand(n, I, 4, generator=g) * torch.tensor([200.0, 200.0, 60, 60]) + 8.0
+    sw = torch.rand(n, I, generator=g) + 0.1
+    sd = {"log_step_length": torch.tensor([0.3]), "filter_reg": torch.tensor([0.05]),
+          "label_map_predictor.weight": torch.linspace(1.0, -0.2, 10).view(1, 10, 1, 1),
+          "target_mask_predictor.0.weight": torch.linspace(3.0, -3.0, 10).view(1, 10, 1, 1),
+          "spatial_weight_predictor.weight": torch.ones(1, 10, 1, 1)}
+    opt = dimp.DiMPSteepestDescentGN(sd)
+    states = (_lib.MmtDimpState * n)()
+    results = (_lib.MmtDimpResult * n)()
+    for s in range(n):
+        for k in range(I):
+            states[s].sample_weights[k] = float(sw[s, k]) if k < counts[s] else 0.0
+            for j in range(4):
+                states[s].target_boxes[k][j] = float(bb[s, k, j])
+        results[s].num_iter, results[s].n_samples = steps[s], counts[s]
+    st_d = torch.frombuffer(bytearray(bytes(states)), dtype=torch.uint8).cuda()
+    res_d = torch.frombuffer(bytearray(bytes(results)), dtype=torch.uint8).cuda()
+    fd = filt.clone().cuda()
+    nbytes = lib.mmt_dimp_track_optimize_ws_bytes(n, C, H, W, fk, fk, max(steps))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.mmt_dimp_track_optimize(ctypes.c_void_p(st_d.data_ptr()), n, ctypes.c_void_p(res_d.data_ptr()),
+                                       ctypes.c_void_p(mem.data_ptr()), C, H, W, ctypes.c_void_p(fd.data_ptr()),
+                                       fk, fk, ctypes.byref(opt.params), max(steps), ctypes.c_void_p(ws.data_ptr()),
+                                       nbytes, stream) == 0
+    for s in range(n):
+        m = counts[s]
+        if steps[s] == 0:
+            assert torch.equal(fd[s].cpu(), filt[s])
+            continue
+        ref = opt.optimize(filt[s:s + 1].cuda(), mem[s, :m].unsqueeze(1).contiguous(), bb[s, :m].view(m, 1, 4),
+                           sample_weight=sw[s, :m].view(m, 1), num_iter=steps[s])
+        assert torch.equal(fd[s:s + 1].cpu(), ref.cpu()), s
+    # the strided optimize_dev over the pool layout (sequences 0 and 2 as one call, sequence 1 given zero steps)
+    fd2 = filt.clone().cuda()
+    feat = mem[:, :I].transpose(0, 1)
+    sbytes = ctypes.sizeof(_lib.MmtDimpState)
+    box0 = st_d.data_ptr() + _lib.MmtDimpState.target_boxes.offset
+    w0 = st_d.data_ptr() + _lib.MmtDimpState.sample_weights.offset
+    opt.optimize_dev(fd2[0:1], feat[:, 0:1], box0, w0, 2, bb_strides=(4, sbytes // 4), sw_strides=(1, sbytes // 4))
+    ref0 = opt.optimize(filt[0:1].cuda(), mem[0].unsqueeze(1).contiguous(), bb[0].view(I, 1, 4),
+                        sample_weight=sw[0].view(I, 1), num_iter=2)
+    assert torch.equal(fd2[0:1].cpu(), ref0.cpu())
