@@ -22,6 +22,30 @@ __device__ __forceinline__ float bf2f(bf16_t x) {
 // (three fp16 MFMAs at the bf16 rate; the dropped lo*lo is 2^-22 relative).  The GEMM / attention
 // epilogues multiply the fp32 accumulator by 1 / (s_a s_w), exact for powers of two.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// a value the compiler cannot prove wave-uniform (e.g. selected from kernel arguments by blockIdx, or CSE'd with
+// a per-lane product) moved to SGPRs, so a buffer resource built from it needs no waterfall loop
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>((uint64_t)hi << 32 | lo);
+}
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
+  // raw buffer: stride 0, num_records = bytes (loads past it return 0), gfx9 dword3; callers pass wave-uniform
+  // operands, made SGPR-resident here
+  const int n = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffff ? bytes : (int64_t)0x7fffffff));
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(p)), (short)0, n, 0x00020000);
+}
+constexpr uint32_t kBufOob = 0x80000000u;   // a buffer offset past every resource: the load returns zeros
+// the same descriptor as four dwords (for inline-asm buffer instructions, "s" operand)
+__device__ __forceinline__ u32x4 make_rsrc_words(const void* p, int64_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(uniform_ptr(p));
+  const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffff ? bytes : (int64_t)0x7fffffff));
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, n, 0x00020000u};
+}
 __device__ __forceinline__ uint16_t f2h(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }  // RNE
 __device__ __forceinline__ float h2f(uint16_t x) { return (float)__builtin_bit_cast(_Float16, x); }
 __device__ __forceinline__ void split_h(float v, uint16_t& hi, uint16_t& lo) {

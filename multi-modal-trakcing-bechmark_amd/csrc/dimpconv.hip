@@ -96,21 +96,24 @@ __device__ __forceinline__ void fold_max(float* ymax, float ymx, int shard) {
                            __float_as_uint(ymx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one K-tile's global operands in flight: 8 activations (fp32, split on the way into the LDS) and 8 fp16 halves
-// of each weight image; two named sets (no array, so nothing is indexed at run time and nothing goes to scratch)
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// one K-tile's activations in flight: 8 fp32 values of one output pixel (split into fp16 hi / lo on the way
+// into the LDS); two named sets (no array, so nothing is indexed at run time and nothing goes to scratch)
 struct ConvRegs {
   float4 a0, a1;
-  uint4 wh, wl;
 };
 
 // grid (ceil(M / 128), Cout / BN, G * ks): blockIdx.z = group * ks + K slice
 template <int BN, bool STEM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_f16x3_kernel(const ConvF16Args a) {
-  constexpr int BM = 128, BK = 32;
+  constexpr int BM = 128, BK = 32, NWS = 3;   // W ring depth
   constexpr int WN = BN / 2, FM = 2, FN = WN / 16;
-  __shared__ __attribute__((aligned(16))) uint16_t sA[2][2][BM * BK];   // [stage][hi, lo]
-  __shared__ __attribute__((aligned(16))) uint16_t sW[2][2][BN * BK];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr int NW = BN / 64;                  // W LDS-DMA pieces (16 rows x 64 B) per wave per K-tile
+  constexpr int NA = STEM ? 6 : 2;             // A loads per thread per K-tile
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][2][BM * BK];     // [stage][hi, lo]
+  __shared__ __attribute__((aligned(16))) uint16_t sW[NWS][2][BN * BK];
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int grp = blockIdx.z / a.ks, slice = blockIdx.z - grp * a.ks;
   const ConvGroupArgs g = pick_group(a, grp);
@@ -125,54 +128,76 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   }
   const float inv = g.inv_w / sa;
 
-  // A load slot: row (pixel) t >> 2, K chunk t & 3 (8 values); W load slot: row t >> 2, chunk t & 3
+  // A load slot: row (pixel) t >> 2, K chunk t & 3 (8 values)
   const int ar = t >> 2, ac = t & 3;
   const int m = m0 + ar;
   const bool mval = m < M;
   int iy0 = 0, ix0 = 0;
-  const float* xb = g.x;
+  uint32_t xrow = 0;   // the pixel's image base (elements)
   if (mval) {
     const int nimg = m / (a.Ho * a.Wo);
     const int r = m - nimg * a.Ho * a.Wo;
     const int oy = r / a.Wo, ox = r - oy * a.Wo;
     iy0 = oy * a.stride - a.pad;
     ix0 = ox * a.stride - a.pad;
-    xb = g.x + (int64_t)nimg * a.H * a.W * a.Cin;
+    xrow = (uint32_t)(nimg * a.H * a.W * a.Cin);
   }
-  const bool wload = ar < BN;
-  const uint16_t* wrh = g.wh + (int64_t)(n0 + (wload ? ar : 0)) * a.Kp + ac * 8;
-  const uint16_t* wrl = g.wl + (int64_t)(n0 + (wload ? ar : 0)) * a.Kp + ac * 8;
+  // operands through raw buffer loads: a tap outside the image, a row past M or a K-tile past the slice takes
+  // an offset past the resource and reads zeros, so every load is issued unconditionally (a branch around a
+  // load makes the compiler wait for it in place)
+  const rsrc_t rX = make_rsrc(g.x, (int64_t)a.N * a.H * a.W * a.Cin * 4);
   const int nk = a.Kp / BK;
   const int kt0 = (int)((int64_t)slice * nk / a.ks), nt = (int)((int64_t)(slice + 1) * nk / a.ks) - kt0;
   const int cpt = STEM ? 1 : a.Cin / BK;   // K-tiles per tap
 
-  auto load = [&](int kt, ConvRegs& r) {
+  auto load_a = [&](int kt, bool kv, ConvRegs& r) {   // kv false: zeros (a tile past the slice, no traffic)
     if constexpr (STEM) {
       // taps 8 kt + 2 ac, + 1: three channels each (the fourth is the weights' zero pad)
-      float4 v[2];
+      float v[2][3];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int tap = kt * 8 + ac * 2 + h;
         const int ky = tap / a.kw, kx = tap - ky * a.kw;
         const int iy = iy0 + ky, ix = ix0 + kx;
-        const bool ok = mval && tap < a.kh * a.kw && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-        const float* src = xb + ((int64_t)iy * a.W + ix) * 3;
-        v[h] = ok ? make_float4(src[0], src[1], src[2], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool ok = kv && mval && tap < a.kh * a.kw && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        const uint32_t vo = ok ? (xrow + (uint32_t)((iy * a.W + ix) * 3)) * 4 : kBufOob;
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          v[h][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rX, vo + 4 * e, 0, 0));
       }
-      r.a0 = v[0];
-      r.a1 = v[1];
+      r.a0 = make_float4(v[0][0], v[0][1], v[0][2], 0.f);
+      r.a1 = make_float4(v[1][0], v[1][1], v[1][2], 0.f);
     } else {
       const int tap = kt / cpt, c0 = (kt - tap * cpt) * BK + ac * 8;
       const int ky = tap / a.kw, kx = tap - ky * a.kw;
       const int iy = iy0 + ky, ix = ix0 + kx;
-      const bool ok = mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      const float4* src = reinterpret_cast<const float4*>(xb + ((int64_t)iy * a.W + ix) * a.Cin + c0);
-      r.a0 = ok ? src[0] : make_float4(0.f, 0.f, 0.f, 0.f);
-      r.a1 = ok ? src[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool ok = kv && mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const uint32_t vo = ok ? (xrow + (uint32_t)((iy * a.W + ix) * a.Cin + c0)) * 4 : kBufOob;
+      r.a0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rX, vo, 0, 0));
+      r.a1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rX, vo + 16, 0, 0));
     }
-    if (wload) {
-      r.wh = *reinterpret_cast<const uint4*>(wrh + kt * BK);
-      r.wl = *reinterpret_cast<const uint4*>(wrl + kt * BK);
+  };
+  // W by LDS-DMA (buffer_load ... lds, no VGPRs): piece p = wave * NW + j holds rows 16 (p % (BN / 16)) .. + 15
+  // of image p / (BN / 16); lane writes LDS chunk lane & 3 of row lane >> 2 and loads the source chunk that the
+  // cswz swizzle puts there
+  // the W pieces are issued as inline asm: the compiler neither orders LDS reads behind them (it cannot tell the
+  // ring stages apart and would wait for every DMA before each fragment read) nor counts them; the K loop waits
+  // for them itself, and the compiler's own vmcnt waits for the A registers only ever wait longer because of them
+  const u32x4 qWh = make_rsrc_words(g.wh, (int64_t)a.Cout * a.Kp * 2);
+  const u32x4 qWl = make_rsrc_words(g.wl, (int64_t)a.Cout * a.Kp * 2);
+  auto load_w = [&](int kt, bool kv, int st) {
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int p = wave * NW + j, img = p / (BN / 16), rb = p % (BN / 16);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(lptr_t)(&sW[st][img][rb * 16 * BK]));
+      const int row = rb * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 2);
+      const uint32_t vo = kv ? (uint32_t)(((n0 + row) * a.Kp + c * 8) * 2) : kBufOob;
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(kt * BK * 2));
+      if (img)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWl), "s"(so), "{m0}"(dst) : "memory");
+      else
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWh), "s"(so), "{m0}"(dst) : "memory");
     }
   };
   auto pack2 = [&](float x, float y, uint32_t& h, uint32_t& l) {
@@ -190,10 +215,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     pack2(r.a1.z, r.a1.w, hv.w, lv.w);
     *reinterpret_cast<uint4*>(&sA[st][0][cswz(ar, ac)]) = hv;
     *reinterpret_cast<uint4*>(&sA[st][1][cswz(ar, ac)]) = lv;
-    if (wload) {
-      *reinterpret_cast<uint4*>(&sW[st][0][cswz(ar, ac)]) = r.wh;
-      *reinterpret_cast<uint4*>(&sW[st][1][cswz(ar, ac)]) = r.wl;
-    }
   };
 
   f32x4 acc[FM][FN];
@@ -202,59 +223,69 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int st) {
+  auto compute = [&](int sta, int stw) {
     const int c = lane >> 4;
     bf16x8 ah[FM], al[FM];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int row = wm * 32 + i * 16 + (lane & 15);
-      ah[i] = *reinterpret_cast<const bf16x8*>(&sA[st][0][cswz(row, c)]);
-      al[i] = *reinterpret_cast<const bf16x8*>(&sA[st][1][cswz(row, c)]);
+      ah[i] = *reinterpret_cast<const bf16x8*>(&sA[sta][0][cswz(row, c)]);
+      al[i] = *reinterpret_cast<const bf16x8*>(&sA[sta][1][cswz(row, c)]);
     }
-    // weight fragments two column blocks at a time (fewer live registers: two workgroups per CU); each
-    // accumulator still takes Wh*Ah, Wl*Ah, Wh*Al in that order, four independent accumulators between
+    // weight fragments one column block at a time (fewer live registers: two workgroups per CU; a dependent
+    // 16x16x32 MFMA chain issues at the full rate, MI355X_MICROARCH.md); each accumulator takes Wh*Ah, Wl*Ah,
+    // Wh*Al in that order
 #pragma unroll
-    for (int j0 = 0; j0 < FN; j0 += 2) {
-      bf16x8 bh[2], bl[2];
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * WN + j * 16 + (lane & 15);
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(&sW[stw][0][cswz(row, c)]);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&sW[stw][1][cswz(row, c)]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = wn * WN + (j0 + j) * 16 + (lane & 15);
-        bh[j] = *reinterpret_cast<const bf16x8*>(&sW[st][0][cswz(row, c)]);
-        bl[j] = *reinterpret_cast<const bf16x8*>(&sW[st][1][cswz(row, c)]);
+      for (int i = 0; i < FM; ++i) {
+        acc[i][j] = mfma16<true>(bh, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bl, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bh, al[i], acc[i][j]);
       }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma16<true>(bh[j], ah[i], acc[i][j0 + j]);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma16<true>(bl[j], ah[i], acc[i][j0 + j]);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma16<true>(bh[j], al[i], acc[i][j0 + j]);
     }
   };
 
-  // K-tile kt0 + i: loaded into register set i & 1 two tiles ahead, stashed into LDS stage i & 1 one tile ahead
+  // K-tile kt0 + i: A loaded into register set i & 1 two tiles ahead and stashed (split) into LDS stage i & 1
+  // one tile ahead; W DMA'd into ring stage i % 3 right after the stash of the tile before (one tile ahead).
+  // Issue order per tile: A(i + 2), multiply i, stash A(i + 1) (the compiler's wait for its registers leaves
+  // A(i + 2) in flight and retires W(i + 1), issued before it), W(i + 2), then the wait that leaves exactly
+  // A(i + 2) and W(i + 2) in flight, and a raw s_barrier (__syncthreads() would wait for every load).  Loads
+  // past the slice are zeros into stages nobody reads, so every load and stash is unconditional.
+  auto tile_wait = [&]() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NW) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
   ConvRegs r0, r1;
-  load(kt0, r0);
-  if (nt > 1) load(kt0 + 1, r1);
+  load_a(kt0, true, r0);
+  load_w(kt0, true, 0);
+  load_a(kt0 + 1, nt > 1, r1);
   stash(r0, 0);
-  __syncthreads();
+  load_w(kt0 + 1, nt > 1, 1);
+  tile_wait();
+  int sw = 0;   // i % 3
   for (int i = 0; i < nt; i += 2) {
-    if (i + 2 < nt) load(kt0 + i + 2, r0);
-    compute(0);
-    if (i + 1 < nt) stash(r1, 1);
-    __syncthreads();
-    if (i + 1 < nt) {
-      if (i + 3 < nt) load(kt0 + i + 3, r1);
-      compute(1);
-      if (i + 2 < nt) stash(r0, 0);
-      __syncthreads();
-    }
+    const int sw2 = sw == 0 ? 2 : sw - 1;   // (i + 2) % 3
+    load_a(kt0 + i + 2, i + 2 < nt, r0);
+    compute(0, sw);
+    stash(r1, 1);
+    load_w(kt0 + i + 2, i + 2 < nt, sw2);
+    tile_wait();
+    sw = sw == 2 ? 0 : sw + 1;
+    if (i + 1 >= nt) break;
+    const int sw3 = sw == 0 ? 2 : sw - 1;   // (i + 3) % 3
+    load_a(kt0 + i + 3, i + 3 < nt, r1);
+    compute(1, sw);
+    stash(r0, 0);
+    load_w(kt0 + i + 3, i + 3 < nt, sw3);
+    tile_wait();
+    sw = sw == 2 ? 0 : sw + 1;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the zero-loads past the slice, before the LDS is left
 
   // lane holds channels n0 + wn * WN + j * 16 + 4 * (lane >> 4) + (0..3) of pixel m0 + wm * 32 + i * 16 + (lane & 15)
   const int li = lane & 15, lk = lane >> 4;

@@ -71,13 +71,6 @@ __device__ unsigned long long* g_gemm_stamps = nullptr;
       g_gemm_stamps[(size_t)blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memtime();          \
   } while (0)
 
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
-  // raw buffer: stride 0, num_records = bytes (loads past it return 0), gfx9 dword3
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)min(bytes, (int64_t)0x7fffffff),
-                                           0x00020000);
-}
 
 // fused epilogue for one lane's 4 consecutive outputs C[m][n..n+3]
 template <int EPI, bool SPLIT>
