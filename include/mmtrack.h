@@ -186,7 +186,8 @@ int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w,
  * ceil(K / 32) * 32; x_max: the input's max words (mmt_conv_max_words() floats: sharded max|x| that a
  * producing conv accumulated into its y_max) or NULL with x_scale = the static power-of-two input scale;
  * y_max: the output's max words (accumulated with agent-scope atomic max; zero them before the producer) or
- * NULL.  Cin % 32 == 0 or Cin == 3; flags RELU / MAX.                                                  */
+ * NULL.  Cin % 32 == 0, Cin == 3, or Cin == 4 (a 3-channel image padded to 4, same weights); flags RELU /
+ * MAX.                                                                                                  */
 size_t mmt_conv_max_words(void);
 int mmt_conv2d_f16x3(const float* x, int N, int H, int W, int Cin, const uint16_t* w_hi, const uint16_t* w_lo,
                      float w_scale, int Kp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
@@ -222,6 +223,10 @@ int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int str
  * -> ((v / 255) - mean) / std as NHWC [N][H][W][3] per 3-channel half (out_b: the aux half)       */
 int mmt_image_normalize(const float* im, int N, int C, int H, int W, const float mean[3], const float std_[3],
                         float* out_a, float* out_b, void* hip_stream);
+/* the same with each pixel padded to 4 channels (a zero fourth): [N][H][W][4], what the f16x3 stem reads as one
+ * 16-B load per tap (mmt_conv2d_f16x3* with Cin = 4)                                                     */
+int mmt_image_normalize4(const float* im, int N, int C, int H, int W, const float mean[3], const float std_[3],
+                         float* out_a, float* out_b, void* hip_stream);
 /* InstanceL2Norm(size_average, eps, scale) (normalization.py:6-21) of NHWC x; y_nhwc / y_nchw may be NULL;
  * ws: device scratch of mmt_instance_l2norm_ws_bytes(N, H, W) (per-chunk sums); C % 4 == 0, C <= 1024   */
 size_t mmt_instance_l2norm_ws_bytes(int N, int H, int W);

@@ -46,6 +46,8 @@ struct DimpMaps {                 // label / target-mask / sample-weight maps fr
   const float* sqrt_sw;           // [IS] sqrt of the per-sample weight
   const float* label_w; const float* mask_w; const float* spatial_w;   // [nbins] (device)
   float* label; float* mask; float* sw;                                 // [IS][Ho][Wo]
+  int S;                          // sequences (is = i * S + s)
+  const mmt_dimp_result* ctl;     // sequences with no steps this frame are skipped (null: none skipped)
 };
 struct DimpFilter {
   const float* feat;              // [I][S][C][H][W]: sample (i, s) at feat + i * img_stride + s * seq_stride

@@ -13,6 +13,7 @@ __global__ __launch_bounds__(256) void dimp_maps_kernel(DimpMaps m) {
   const int n = m.Ho * m.Wo;
   if (idx >= m.IS * n) return;
   const int is = idx / n, p = idx - is * n;
+  if (m.ctl && m.ctl[is % m.S].num_iter <= 0) return;
   const int y = p / m.Wo, x = p - y * m.Wo;
   const float d0 = (float)y - m.centers[2 * is], d1 = (float)x - m.centers[2 * is + 1];
   const float dist = sqrtf(d0 * d0 + d1 * d1);
@@ -206,41 +207,84 @@ __global__ __launch_bounds__(256) void dimp_transpose_kernel(DimpTranspose a) {
       if (e < stage) d[e] = rg[k];
     }
   };
-  const int G = 256 / (CT * T);
-  const int pair = t / G, sub = t - pair * G;
-  const bool active = pair < CT * T;
-  const int c = pair / T, tt = pair - c * T, ky = tt / a.fw, kx = tt - ky * a.fw;
-  float acc = 0.f;
   if (nI > 0) {
     fetch(0);
     put(0);
   }
   __syncthreads();
-  for (int i = 0; i < nI; ++i) {
-    if (i + 1 < nI) fetch(i + 1);
-    const float* sf = sm + (i & 1) * stage;
-    const float* sr = sf + fsz;
-    if (active) {
-      const float* fp = sf + c * plane + ky * Wp + kx;
-      int y = sub / a.Wo, x = sub - y * a.Wo;
-      for (int p = sub; p < npos; p += G) {
-        acc += sr[p] * fp[y * Wp + x];
-        x += G;
-        while (x >= a.Wo) {
-          x -= a.Wo;
-          ++y;
-        }
-      }
-    }
-    if (i + 1 < nI) put((i + 1) & 1);
-    __syncthreads();
-  }
-  red[t] = acc;
-  __syncthreads();
   float gv = 0.f;
   const bool own = t < CT * T && c0 + t / T < a.C;
+  if constexpr (FH > 0) {
+    // register-blocked: thread (channel c, position group pg) keeps all FH x FW taps of its channel in registers
+    // and reads each residual once and each padded-plane value once per tap it feeds (~1 LDS read per FMA
+    // instead of 2); the PG group sums of a (channel, tap) combine in group order at the end
+    constexpr int TT = FH * FW;
+    const int PG = 256 / CT;
+    const int c = t / PG, pg = t - c * PG;
+    float accb[TT];
+#pragma unroll
+    for (int k = 0; k < TT; ++k) accb[k] = 0.f;
+    for (int i = 0; i < nI; ++i) {
+      if (i + 1 < nI) fetch(i + 1);
+      const float* sf = sm + (i & 1) * stage;
+      const float* sr = sf + fsz;
+      if (c < CT) {
+        int y = pg / a.Wo, x = pg - y * a.Wo;
+        for (int p = pg; p < npos; p += PG) {
+          const float rv = sr[p];
+          const float* fp = sf + c * plane + y * Wp + x;
+#pragma unroll
+          for (int ky = 0; ky < FH; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < FW; ++kx) accb[ky * FW + kx] += rv * fp[ky * Wp + kx];
+          x += PG;
+          while (x >= a.Wo) {
+            x -= a.Wo;
+            ++y;
+          }
+        }
+      }
+      if (i + 1 < nI) put((i + 1) & 1);
+      __syncthreads();
+    }
+    float* part = sm;   // the staging buffers are free now: [CT][TT][PG]
+    if (c < CT)
+#pragma unroll
+      for (int k = 0; k < TT; ++k) part[(c * TT + k) * PG + pg] = accb[k];
+    __syncthreads();
+    if (own)
+      for (int u = 0; u < PG; ++u) gv += part[t * PG + u];
+  } else {
+    const int G = 256 / (CT * T);
+    const int pair = t / G, sub = t - pair * G;
+    const bool active = pair < CT * T;
+    const int c = pair / T, tt = pair - c * T, ky = tt / a.fw, kx = tt - ky * a.fw;
+    float acc = 0.f;
+    for (int i = 0; i < nI; ++i) {
+      if (i + 1 < nI) fetch(i + 1);
+      const float* sf = sm + (i & 1) * stage;
+      const float* sr = sf + fsz;
+      if (active) {
+        const float* fp = sf + c * plane + ky * Wp + kx;
+        int y = sub / a.Wo, x = sub - y * a.Wo;
+        for (int p = sub; p < npos; p += G) {
+          acc += sr[p] * fp[y * Wp + x];
+          x += G;
+          while (x >= a.Wo) {
+            x -= a.Wo;
+            ++y;
+          }
+        }
+      }
+      if (i + 1 < nI) put((i + 1) & 1);
+      __syncthreads();
+    }
+    red[t] = acc;
+    __syncthreads();
+    if (own)
+      for (int u = 0; u < G; ++u) gv += red[t * G + u];
+  }
   if (own) {
-    for (int u = 0; u < G; ++u) gv += red[t * G + u];
     const int64_t o = ((int64_t)s * a.C + c0) * T + t;
     gv += a.w ? a.reg * a.w[o] : 0.f;
     a.grad[o] = gv;
@@ -369,7 +413,7 @@ void dimp_transpose(const DimpTranspose& a_, hipStream_t s) {
   a.CT = g.CT;
   const size_t lds = 2 * (size_t)g.transpose_stage * sizeof(float);
   const dim3 grid(a.S, (a.C + g.CT - 1) / g.CT);
-  if (a.fh == 4 && a.fw == 4)
+  if (a.fh == 4 && a.fw == 4 && 2 * g.transpose_stage >= 256 * 16)   // the blocked form's group sums fit the staging
     hipLaunchKernelGGL((dimp_transpose_kernel<4, 4>), grid, dim3(256), lds, s, a);
   else
     hipLaunchKernelGGL((dimp_transpose_kernel<0, 0>), grid, dim3(256), lds, s, a);

@@ -104,7 +104,7 @@ static int optimize_body(const float* feat, int64_t img_stride, int64_t seq_stri
   const float reg = std::fmax(p->filter_reg * p->filter_reg, p->min_filter_reg * p->min_filter_reg);
 
   DimpMaps m{IS, Ho, Wo, p->num_dist_bins, p->bin_displacement, F(L.centers), F(L.sqrtsw), F(L.params),
-             F(L.params) + 128, F(L.params) + 256, F(L.label), F(L.mask), F(L.sw)};
+             F(L.params) + 128, F(L.params) + 256, F(L.label), F(L.mask), F(L.sw), S, ctl};
   dimp_maps(m, st);
 
   DimpFilter fa{};

@@ -89,11 +89,21 @@ __device__ __forceinline__ f32x4 conv_out(const ConvGroupArgs& g, f32x4 v, int64
   return v;
 }
 
-__device__ __forceinline__ void fold_max(float* ymax, float ymx, int shard) {
+// the workgroup's max|y| into shard word blockIdx-derived: one agent-scope atomic max per workgroup (a per-wave
+// atomic put ~1 300 atomics on each of the 64 words for the stem's 10 368 workgroups); every thread calls it
+template <int NWAVES>
+__device__ __forceinline__ void fold_max(float* ymax, float ymx, int shard, float* wmax /* LDS, NWAVES floats */) {
   ymx = wave_max(ymx);
-  if ((threadIdx.x & 63) == 0 && ymx > 0.f)
-    __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(ymax) + (shard % kMaxShards) * kShardStride,
-                           __float_as_uint(ymx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = ymx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = wmax[0];
+#pragma unroll
+    for (int w = 1; w < NWAVES; ++w) m = fmaxf(m, wmax[w]);
+    if (m > 0.f)
+      __hip_atomic_fetch_max(reinterpret_cast<unsigned*>(ymax) + (shard % kMaxShards) * kShardStride,
+                             __float_as_uint(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -152,7 +162,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 
   auto load_a = [&](int kt, bool kv, ConvRegs& r) {   // kv false: zeros (a tile past the slice, no traffic)
     if constexpr (STEM) {
-      // taps 8 kt + 2 ac, + 1: three channels each (the fourth is the weights' zero pad)
+      // taps 8 kt + 2 ac, + 1: three channels each (the fourth is the weights' zero pad); a 4-channel input
+      // (Cin 4: pixels padded with a zero fourth channel, mmt_image_normalize4) loads a tap as one float4
+      if (a.Cin == 4) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int tap = kt * 8 + ac * 2 + h;
+          const int ky = tap / a.kw, kx = tap - ky * a.kw;
+          const int iy = iy0 + ky, ix = ix0 + kx;
+          const bool ok = kv && mval && tap < a.kh * a.kw && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+          const uint32_t vo = ok ? (xrow + (uint32_t)((iy * a.W + ix) * 4)) * 4 : kBufOob;
+          (h ? r.a1 : r.a0) = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rX, vo, 0, 0));
+        }
+        return;
+      }
       float v[2][3];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -318,7 +341,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
       for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
     }
   }
-  if (g.ymax) fold_max(g.ymax, ymx, blockIdx.x * 8 + wave);
+  // (the operand stages are free: the K loop ended on a barrier after the last multiply)
+  if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.y * 7 + blockIdx.z * 13, reinterpret_cast<float*>(&sA[0][0][0]));
 }
 
 // split-K: y = sum over the ks slices (in slice order) + bias (+ residual), ReLU, merge; grid (blocks, G), 4 channels
@@ -344,7 +368,8 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvF16Ar
 #pragma unroll
     for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
   }
-  if (g.ymax) fold_max(g.ymax, ymx, blockIdx.x * 4 + (threadIdx.x >> 6));
+  __shared__ float wmax[4];
+  if (g.ymax) fold_max<4>(g.ymax, ymx, blockIdx.x, wmax);
 }
 
 // K slices for a launch of `tiles` output tiles over nk K-tiles, when the tiles alone leave the GPU's 512
@@ -373,7 +398,7 @@ using namespace mmt;
 namespace {
 
 int conv_shape(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pad, int& Ho, int& Wo, int& K) {
-  const bool stem = Cin == 3;
+  const bool stem = Cin == 3 || Cin == 4;   // 4: a 3-channel image padded with a zero channel
   if (N <= 0 || H <= 0 || W <= 0 || Cout <= 0 || Cout % 64 || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 ||
       (!stem && Cin % 32))
     return MMT_E_ARG;
@@ -386,7 +411,7 @@ int conv_shape(int N, int H, int W, int Cin, int Cout, int kh, int kw, int strid
   return MMT_OK;
 }
 
-int conv_bn(int Cin, int Cout) { return Cin == 3 ? 64 : Cout % 128 == 0 ? 128 : 64; }
+int conv_bn(int Cin, int Cout) { return Cin <= 4 ? 64 : Cout % 128 == 0 ? 128 : 64; }
 
 int64_t conv_ks_for(int N, int Ho, int Wo, int Cin, int Cout, int Kp, int G) {
   const int64_t gm = ((int64_t)N * Ho * Wo + 127) / 128;
@@ -437,7 +462,7 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   const int bn = conv_bn(Cin, Cout);
   const dim3 grid(gm, Cout / bn, G * ks);
   const hipStream_t s = (hipStream_t)stream;
-  if (Cin == 3)
+  if (Cin <= 4)
     hipLaunchKernelGGL((conv_f16x3_kernel<64, true>), grid, dim3(512), 0, s, a);
   else if (bn == 128)
     hipLaunchKernelGGL((conv_f16x3_kernel<128, false>), grid, dim3(512), 0, s, a);

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void maxpool4_kernel(const float4* __restrict_
 // (net_wrappers.py:62-72: color and depth halves normalised with the same ImageNet constants)
 __global__ __launch_bounds__(256) void normalize_kernel(const float* __restrict__ im, int N, int C, int H, int W,
                                                         float m0, float m1, float m2, float s0, float s1, float s2,
-                                                        float* __restrict__ outa, float* __restrict__ outb) {
+                                                        float* __restrict__ outa, float* __restrict__ outb, int oc) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t HW = (int64_t)H * W;
   if (i >= (int64_t)N * HW) return;
@@ -279,7 +279,11 @@ __global__ __launch_bounds__(256) void normalize_kernel(const float* __restrict_
     v = v - mean[c % 3];
     v = v / sd[c % 3];
     float* o = c < 3 ? outa : outb;
-    o[(n * HW + p) * 3 + (c % 3)] = v;
+    o[(n * HW + p) * oc + (c % 3)] = v;
+  }
+  if (oc == 4) {   // the zero fourth channel of a padded pixel
+    outa[(n * HW + p) * 4 + 3] = 0.f;
+    if (C == 6) outb[(n * HW + p) * 4 + 3] = 0.f;
   }
 }
 
@@ -553,7 +557,16 @@ int mmt_image_normalize(const float* im, int N, int C, int H, int W, const float
   if (!im || !mean || !std_ || !out_a || N <= 0 || H <= 0 || W <= 0 || (C != 3 && C != 6) || (C == 6 && !out_b))
     return MMT_E_ARG;
   hipLaunchKernelGGL(normalize_kernel, dim3(blocks_for((int64_t)N * H * W)), dim3(256), 0, (hipStream_t)stream, im, N, C,
-                     H, W, mean[0], mean[1], mean[2], std_[0], std_[1], std_[2], out_a, out_b);
+                     H, W, mean[0], mean[1], mean[2], std_[0], std_[1], std_[2], out_a, out_b, 3);
+  return last_err();
+}
+
+int mmt_image_normalize4(const float* im, int N, int C, int H, int W, const float mean[3], const float std_[3],
+                         float* out_a, float* out_b, void* stream) {
+  if (!im || !mean || !std_ || !out_a || N <= 0 || H <= 0 || W <= 0 || (C != 3 && C != 6) || (C == 6 && !out_b))
+    return MMT_E_ARG;
+  hipLaunchKernelGGL(normalize_kernel, dim3(blocks_for((int64_t)N * H * W)), dim3(256), 0, (hipStream_t)stream, im, N, C,
+                     H, W, mean[0], mean[1], mean[2], std_[0], std_[1], std_[2], out_a, out_b, 4);
   return last_err();
 }
 

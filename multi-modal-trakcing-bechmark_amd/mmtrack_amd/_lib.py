@@ -153,6 +153,7 @@ SIGNATURES = {
     "mmt_conv2d_f16x3_groups": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, ctypes.c_size_t, _P]),
     "mmt_maxpool2d_f32": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "mmt_image_normalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "mmt_image_normalize4": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "mmt_instance_l2norm_ws_bytes": (ctypes.c_size_t, [_I, _I, _I]),
     "mmt_instance_l2norm": (_I, [_P, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P]),
     "mmt_prroi_pool": (_I, [_P, _I, _I, _I, _I, _P, _F, _I, _I, _P, _P]),

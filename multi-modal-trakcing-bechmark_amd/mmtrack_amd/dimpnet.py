@@ -115,14 +115,16 @@ class _Conv:
         return out
 
 
-def run_f16x3(lib, conv, groups, N, H, W, ws, stream):
+def run_f16x3(lib, conv, groups, N, H, W, ws, stream, cin=None):
     """One mmt_conv2d_f16x3_groups launch of conv's shape over groups (the twin layers of the two backbones, or
-    one); split-K partials in ws(nbytes) when the library asks for a split."""
+    one); split-K partials in ws(nbytes) when the library asks for a split.  cin=4: the stem over an image
+    padded to 4 channels (mmt_image_normalize4)."""
     G = len(groups)
-    need = lib.mmt_conv2d_f16x3_ws_bytes(N, H, W, conv.cin, conv.cout, conv.kh, conv.kw, conv.stride, conv.pad, G)
+    cin = conv.cin if cin is None else cin
+    need = lib.mmt_conv2d_f16x3_ws_bytes(N, H, W, cin, conv.cout, conv.kh, conv.kw, conv.stride, conv.pad, G)
     buf = ws(need) if (need and ws is not None) else None
     arr = (_lib.MmtConvGroup * G)(*groups)
-    _rc(lib.mmt_conv2d_f16x3_groups(arr, G, N, H, W, conv.cin, conv.kp, conv.cout, conv.kh, conv.kw, conv.stride,
+    _rc(lib.mmt_conv2d_f16x3_groups(arr, G, N, H, W, cin, conv.kp, conv.cout, conv.kh, conv.kw, conv.stride,
                                     conv.pad, _p(buf), need if buf is not None else 0, stream),
         "mmt_conv2d_f16x3_groups")
 
@@ -204,11 +206,12 @@ class DiMPNet:
     def _ws(self, nbytes):
         return self._buf("splitk", (nbytes + 3) // 4)
 
-    def _layer(self, convs, kws, N, H, W, s):
+    def _layer(self, convs, kws, N, H, W, s, cin=None):
         """The same layer of each backbone: f16x3 runs the twins as one grouped launch (unless one merges into
-        the other's output); fp32 runs them in backbone order."""
+        the other's output); fp32 runs them in backbone order.  cin: the f16x3 input's channel count when it
+        differs from the conv's (4: the padded image)."""
         if self.precision == "f16x3" and len(convs) > 1 and not any(kw.get("merge_max") for kw in kws):
-            run_f16x3(self.lib, convs[0], [c.group(**kw) for c, kw in zip(convs, kws)], N, H, W, self._ws, s)
+            run_f16x3(self.lib, convs[0], [c.group(**kw) for c, kw in zip(convs, kws)], N, H, W, self._ws, s, cin)
             return
         for c, kw in zip(convs, kws):
             c(self.lib, kw.pop("x"), N, H, W, kw.pop("out"), s, ws=self._ws, **kw)
@@ -224,8 +227,9 @@ class DiMPNet:
         h, w = stems[0].out_hw(H, W)
         t0 = [self._buf(f"stem{k}", N * h * w * 64) for k in K]
         t0_max = [self._slot() for k in K]
+        f16 = self.precision == "f16x3"   # f16x3: the images come padded to 4 channels
         self._layer(stems, [dict(x=xs[k], out=t0[k], relu=True, x_scale=self.image_scale, y_max=t0_max[k])
-                            for k in K], N, H, W, s)
+                            for k in K], N, H, W, s, cin=4 if f16 else None)
         H2, W2 = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
         cur = [self._buf(f"ping{k}", N * H2 * W2 * 256) for k in K]
         for k in K:
@@ -322,10 +326,12 @@ class DiMPNet:
         im = im.contiguous()
         N, _, H, W = im.shape
         s = self._stream()
-        xa = self._buf("xa", N * H * W * 3)
-        xb = self._buf("xb", N * H * W * 3)
-        _rc(self.lib.mmt_image_normalize(_p(im), N, 6, H, W, self._mean, self._std, _p(xa), _p(xb), s),
-            "mmt_image_normalize")
+        f16 = self.precision == "f16x3"
+        pc = 4 if f16 else 3   # f16x3: pixels padded to 4 channels (one 16-B load per stem tap)
+        xa = self._buf("xa", N * H * W * pc)
+        xb = self._buf("xb", N * H * W * pc)
+        norm = self.lib.mmt_image_normalize4 if f16 else self.lib.mmt_image_normalize
+        _rc(norm(_p(im), N, 6, H, W, self._mean, self._std, _p(xa), _p(xb), s), "mmt_image_normalize")
         Hf, Wf = (H + 15) // 16, (W + 15) // 16
         out = torch.empty(N, Hf, Wf, 1024, dtype=torch.float32, device=self.dev)
         if self._max_words is not None:

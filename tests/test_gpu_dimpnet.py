@@ -123,6 +123,42 @@ def test_conv2d_f16x3_groups_and_splitk(N, C, H, W, Co, k, s, p):
     assert lib.mmt_conv2d_f16x3_groups(bad, 2, N, H, W, C, convs[0].kp, Co, k, k, s, p, None, 0, stream) == -1
 
 
+def test_conv2d_f16x3_stem_padded_input_bitwise():
+    """The f16x3 stem over the image padded to 4 channels (mmt_image_normalize4 layout, one 16-B load per tap)
+    gives the bits of the stem over the 3-channel image (the same K order, the pad channel's weight is 0)."""
+    import ctypes
+    from mmtrack_amd import _lib, dimpnet
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(3, 3, 75, 61, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) / math.sqrt(147)
+    b = torch.randn(64, generator=g) * 0.1
+    conv = dimpnet._Conv(w, bias=b, stride=2, pad=3, dev="cuda", f16x3=True)
+    Ho, Wo = conv.out_hw(75, 61)
+    x3 = x.permute(0, 2, 3, 1).contiguous().cuda()
+    x4 = torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 1)).contiguous().cuda()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for xi, cin in ((x3, 3), (x4, 4)):
+        out = torch.empty(3, Ho, Wo, 64, device="cuda")
+        dimpnet.run_f16x3(lib, conv, [conv.group(xi, out, relu=True, x_scale=dimpnet.range_scale(float(x.abs().max())))],
+                          3, 75, 61, None, stream, cin=cin)
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+    close(outs[0].permute(0, 3, 1, 2), F.relu(F.conv2d(x.double(), w.double(), b.double(), stride=2, padding=3)), 1e-5)
+    # the padded normalisation: the first three channels of each pixel as mmt_image_normalize, the fourth 0
+    im = (torch.rand(2, 6, 20, 24, generator=g) * 255).cuda()
+    mean = (ctypes.c_float * 3)(*dimpnet.MEAN)
+    std = (ctypes.c_float * 3)(*dimpnet.STD)
+    a3, b3 = torch.empty(2, 20, 24, 3, device="cuda"), torch.empty(2, 20, 24, 3, device="cuda")
+    a4, b4 = torch.full((2, 20, 24, 4), 7.0, device="cuda"), torch.full((2, 20, 24, 4), 7.0, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    assert lib.mmt_image_normalize(P(im), 2, 6, 20, 24, mean, std, P(a3), P(b3), stream) == 0
+    assert lib.mmt_image_normalize4(P(im), 2, 6, 20, 24, mean, std, P(a4), P(b4), stream) == 0
+    assert torch.equal(a4[..., :3], a3) and torch.equal(b4[..., :3], b3)
+    assert float(a4[..., 3].abs().max()) == 0.0 and float(b4[..., 3].abs().max()) == 0.0
+
+
 def test_conv2d_stem_w4():
     """The 3-channel stem through MMT_CONV_W4 (weights padded to 4 channels per tap) and through the generic
     per-element path agree with torch and each other (summation orders differ: fp32 rounding)."""
