@@ -22,6 +22,7 @@
 // ends with 4 consecutive output channels of one pixel (16-B NHWC stores).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -377,7 +378,8 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvF16Ar
 // fewest slices), at least 8 K-tiles per slice
 int conv_pick_ks(int64_t tiles, int nk) {
   constexpr int64_t kSlots = 512;
-  if (tiles >= kSlots) return 1;
+  static const bool nosplit = getenv("MMT_CONV_NOSPLIT") != nullptr;   // batch-invariant summation order
+  if (tiles >= kSlots || nosplit) return 1;
   int best = 1;
   double best_eff = 0.0;
   for (int ks = 1; ks <= kMaxSplitK && nk / ks >= 8; ++ks) {

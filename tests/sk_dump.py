@@ -35,6 +35,19 @@ eng = Engine(EngineConfig(max_batch=1, use_graphs=True, precision="fp32"), sd)
 frames, gts = synth.make_frames(21, 5, 360, 480, 6)
 eng.initialize(0, frames[0], list(gts[0]))
 out["boxes"] = np.array([eng.track(0, frames[t])[0] for t in range(1, 5)])
+# device frames whose size and address change between launches that reuse a ring entry (the ring hand-off
+# reads each launch's frame parameters from pinned memory: a stale entry would show against the copy path)
+big, _ = synth.make_frames(22, 6, 360, 480, 6)
+small, _ = synth.make_frames(23, 6, 300, 400, 6)
+seq = []
+for t in range(20):   # > 2 x the ring depth (MMT_PIPELINE_DEPTH = 8)
+    src = big if (t // 3) % 2 == 0 else small
+    f = torch.from_numpy(np.ascontiguousarray(src[1 + t % 5])).cuda()   # a fresh device buffer per launch
+    if t % 4 == 1:
+        f = torch.cat([f, f[:1]]).contiguous()[:-1]                       # another address, same contents
+    seq.append(eng.track(0, f)[0])
+    del f
+out["boxes_device_frames"] = np.array(seq)
 eng.close()
 np.savez(sys.argv[1], **out)
 print("sk_dump ok", sorted(out))

@@ -63,7 +63,8 @@ def test_splitk_combine_bitwise(tmp_path):
     MMT_SK_INLAUNCH=1 write-through, =2 release / acquire) and the default separate reduce launch give the same
     bits: op-level GEMMs and a parity-mode sequence whose few-tile GEMMs split K (tests/sk_dump.py, one child
     process each).  So does the engine with copy launches for the frame parameters and results
-    (MMT_RING_COPY=1) instead of the ring hand-off."""
+    (MMT_RING_COPY=1) instead of the ring hand-off, including device frames whose size and address change
+    between launches that reuse a ring entry."""
     import os
     import subprocess
     import sys
