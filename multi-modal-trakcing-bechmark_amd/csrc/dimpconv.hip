@@ -413,11 +413,18 @@ int conv_shape(int N, int H, int W, int Cin, int Cout, int kh, int kw, int strid
   return MMT_OK;
 }
 
-int conv_bn(int Cin, int Cout) { return Cin <= 4 ? 64 : Cout % 128 == 0 ? 128 : 64; }
+// output channels per tile: 128 where the 128-wide tiles fill the GPU (or everywhere but the stem by default);
+// MMT_CONV_PREFER64 (tuning): 64-wide tiles instead of splitting K when the 128-wide ones leave it under-filled
+int conv_bn(int64_t gm, int Cin, int Cout, int G) {
+  static const bool prefer64 = getenv("MMT_CONV_PREFER64") != nullptr;
+  if (Cin <= 4 || Cout % 128) return 64;
+  if (prefer64 && gm * (Cout / 128) * G < 512) return 64;
+  return 128;
+}
 
 int64_t conv_ks_for(int N, int Ho, int Wo, int Cin, int Cout, int Kp, int G) {
   const int64_t gm = ((int64_t)N * Ho * Wo + 127) / 128;
-  return conv_pick_ks(gm * (Cout / conv_bn(Cin, Cout)) * G, Kp / 32);
+  return conv_pick_ks(gm * (Cout / conv_bn(gm, Cin, Cout, G)) * G, Kp / 32);
 }
 
 }  // namespace
@@ -461,7 +468,7 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   a.ks = ks;
   a.part = static_cast<float*>(ws);
   const unsigned gm = (unsigned)((M + 127) / 128);
-  const int bn = conv_bn(Cin, Cout);
+  const int bn = conv_bn((M + 127) / 128, Cin, Cout, G);
   const dim3 grid(gm, Cout / bn, G * ks);
   const hipStream_t s = (hipStream_t)stream;
   if (Cin <= 4)
