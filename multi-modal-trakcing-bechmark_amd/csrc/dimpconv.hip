@@ -373,11 +373,12 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvF16Ar
   if (g.ymax) fold_max<4>(g.ymax, ymx, blockIdx.x, wmax);
 }
 
-// K slices for a launch of `tiles` output tiles over nk K-tiles, when the tiles alone leave the GPU's 512
-// workgroup slots (256 CUs x 2) under-filled: the split whose last round of workgroups is fullest (ties: the
-// fewest slices), at least 8 K-tiles per slice
+// K slices for a launch of `tiles` output tiles over nk K-tiles, when the tiles alone leave the GPU's 256 CUs
+// under-filled: the split whose last round of workgroups (over kSlots slots) is fullest (ties: the fewest
+// slices), at least 8 K-tiles per slice.  256 slots (one workgroup per CU) measured +1 % over 512 and level
+// with no split at all once the two backbones share a launch (profiles/r03_ab_conv_slots.txt)
 int conv_pick_ks(int64_t tiles, int nk) {
-  constexpr int64_t kSlots = 512;
+  static const int64_t kSlots = getenv("MMT_CONV_SLOTS") ? atoi(getenv("MMT_CONV_SLOTS")) : 256;   // tuning
   static const bool nosplit = getenv("MMT_CONV_NOSPLIT") != nullptr;   // batch-invariant summation order
   if (tiles >= kSlots || nosplit) return 1;
   int best = 1;
