@@ -72,10 +72,11 @@ __device__ unsigned long long* g_gemm_stamps = nullptr;
   } while (0)
 
 
-// fused epilogue for one lane's 4 consecutive outputs C[m][n..n+3]
+// fused epilogue for one lane's 4 consecutive outputs C[m][n..n+3], with the bias bv of those columns and (fp32
+// residual / position epilogues) the residual chunk rr already loaded
 template <int EPI, bool SPLIT>
-__device__ __forceinline__ void store4(const GemmGroup& g, const GemmArgs& args, int m, int n, const f32x4& a) {
-  const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+__device__ __forceinline__ void store4v(const GemmGroup& g, const GemmArgs& args, int m, int n, const f32x4& a,
+                                        const float4& bv, const float4& rr) {
   const float sc = SPLIT ? g.inv : 1.0f;
   float v[4] = {a[0] * sc + bv.x, a[1] * sc + bv.y, a[2] * sc + bv.z, a[3] * sc + bv.w};
   if (EPI == EPI_GELU_BF16)
@@ -105,15 +106,46 @@ __device__ __forceinline__ void store4(const GemmGroup& g, const GemmArgs& args,
     }
   } else {
     float4 o = make_float4(v[0], v[1], v[2], v[3]);
-    if (EPI == EPI_RESID_F32) {
-      const float4 rr = *reinterpret_cast<const float4*>(g.R + (int64_t)m * g.ldr + n);
+    if (EPI == EPI_RESID_F32)
       o = make_float4(rr.x + v[0], rr.y + v[1], rr.z + v[2], rr.w + v[3]);
-    } else if (EPI == EPI_POS_F32) {
-      const float4 rr = *reinterpret_cast<const float4*>(g.R + (int64_t)(m % args.pos_rows) * g.ldr + n);
+    else if (EPI == EPI_POS_F32)
       o = make_float4(v[0] + rr.x, v[1] + rr.y, v[2] + rr.z, v[3] + rr.w);
-    }
     *reinterpret_cast<float4*>(static_cast<float*>(g.C) + off) = o;
   }
+}
+
+constexpr bool epi_has_r(int e) { return e == EPI_RESID_F32 || e == EPI_POS_F32; }
+
+// the same loading its own operands (one fragment: the split-K reduce, sk_combine)
+template <int EPI, bool SPLIT>
+__device__ __forceinline__ void store4(const GemmGroup& g, const GemmArgs& args, int m, int n, const f32x4& a) {
+  const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 rr = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (EPI == EPI_RESID_F32) rr = *reinterpret_cast<const float4*>(g.R + (int64_t)m * g.ldr + n);
+  else if (EPI == EPI_POS_F32) rr = *reinterpret_cast<const float4*>(g.R + (int64_t)(m % args.pos_rows) * g.ldr + n);
+  store4v<EPI, SPLIT>(g, args, m, n, a, bv, rr);
+}
+
+// epilogue operands of a fragment-shaped store pass, requested together before any is used: the bias of a
+// column chunk and the residual / position chunk of (row m, column n) through buffer loads that read zeros for
+// an absent bias or a row past M (a load behind a branch, as in store4, is waited for in place: one dependent
+// round trip per fragment)
+__device__ __forceinline__ float4 epi_bias(const rsrc_t& rB, int n) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rB, (uint32_t)n * 4, 0, 0));
+}
+template <int EPI>
+__device__ __forceinline__ float4 epi_resid(const rsrc_t& rR, const GemmGroup& g, const GemmArgs& args, int m, int n,
+                                            int M) {
+  if constexpr (!epi_has_r(EPI)) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const int row = EPI == EPI_POS_F32 ? m % args.pos_rows : m;
+  const uint32_t off = m < M ? (uint32_t)(((int64_t)row * g.ldr + n) * 4) : kBufOob;
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rR, off, 0, 0));
+}
+template <int EPI>
+__device__ __forceinline__ rsrc_t epi_resid_rsrc(const GemmGroup& g, const GemmArgs& args, int M) {
+  if constexpr (!epi_has_r(EPI)) return make_rsrc(nullptr, 0);
+  const int64_t rows = EPI == EPI_POS_F32 ? args.pos_rows : M;
+  return make_rsrc(g.R, rows * g.ldr * 4);
 }
 
 
@@ -485,13 +517,34 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
     __syncthreads();
     LT::template drain<BM, T::NT, RPRE>(lds, g, args, m0, n0, M, rpre);
   } else {
+    const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)args.N * 4 : 0);
+    const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
+    // (the residual chunks of the 32-fragment tiles -- 256 x 256 tuning configs -- would need 128 more VGPRs:
+    // those keep one fragment's residual at a time)
+    constexpr bool RPRE_ALL = epi_has_r(EPI) && T::FM * T::FN <= 16;
+    float4 bq[T::FN], rq[RPRE_ALL ? T::FM : 1][RPRE_ALL ? T::FN : 1];
+#pragma unroll
+    for (int jj = 0; jj < T::FN; ++jj) bq[jj] = epi_bias(rB, n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4);
+    if constexpr (RPRE_ALL) {
+#pragma unroll
+      for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < T::FN; ++jj)
+          rq[i][jj] = epi_resid<EPI>(rR, g, args, m0 + wm * T::WM + i * 16 + (lane & 15),
+                                     n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4, M);
+    }
 #pragma unroll
     for (int i = 0; i < T::FM; ++i) {
       const int m = m0 + wm * T::WM + i * 16 + (lane & 15);
       if (m >= M) continue;
 #pragma unroll
-      for (int jj = 0; jj < T::FN; ++jj)
-        store4<EPI, SPLIT>(g, args, m, n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4, acc[i][jj]);
+      for (int jj = 0; jj < T::FN; ++jj) {
+        const int n = n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4;
+        if constexpr (RPRE_ALL)
+          store4v<EPI, SPLIT>(g, args, m, n, acc[i][jj], bq[jj], rq[i][jj]);
+        else
+          store4v<EPI, SPLIT>(g, args, m, n, acc[i][jj], bq[jj], epi_resid<EPI>(rR, g, args, m, n, M));
+      }
     }
   }
   GEMM_STAMP(3);
@@ -1241,6 +1294,15 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
   GEMM_STAMP(2);
 
   constexpr int QA[4] = {0, 0, 1, 1}, QB[4] = {0, 1, 1, 0};
+  // the lane's 4 bias chunks (2 column halves x 2) requested together; the residual epilogues (not used by the
+  // path's launches) keep the per-fragment store4
+  const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)args.N * 4 : 0);
+  float4 bq[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) bq[h][jj] = epi_bias(rB, n0 + h * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4);
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int qd = 0; qd < 4; ++qd)
 #pragma unroll
@@ -1249,7 +1311,11 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
       if (m >= M) continue;
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
-        store4<EPI, true>(g, args, m, n0 + QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, acc[qd][i][jj]);
+        if constexpr (epi_has_r(EPI))
+          store4<EPI, true>(g, args, m, n0 + QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, acc[qd][i][jj]);
+        else
+          store4v<EPI, true>(g, args, m, n0 + QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, acc[qd][i][jj],
+                             bq[QB[qd]][jj], zero4);
     }
   GEMM_STAMP(3);
 }
