@@ -254,6 +254,28 @@ __device__ __forceinline__ void sk_combine(const GemmArgs& args, const GemmGroup
   }
 }
 
+// scheduling groups: NR times {one LDS read, K MFMAs}
+template <int NR, int K>
+__device__ __forceinline__ void sched_interleave() {
+  if constexpr (NR > 0) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, K, 0);
+    sched_interleave<NR - 1, K>();
+  }
+}
+// vmcnt(min(n, MAXN)) for a wave-uniform n: a scalar branch to an immediate
+template <int N>
+__device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <int MAXN>
+__device__ __forceinline__ void vm_wait_rt(int n) {   // n wave-uniform; scalar branch to an immediate
+  if constexpr (MAXN > 0) {
+    if (n >= MAXN) return vm_wait_n<MAXN>();
+    return vm_wait_rt<MAXN - 1>(n);
+  } else {
+    vm_wait_n<0>();
+  }
+}
+
 template <int BM, int BN, int WMW, int WNW, int EPI, int AM, bool SPLIT, int STAGES, int BK = 64>
 __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args) {
   static_assert(BK == 64 || (BK == 32 && AM == A_DENSE), "BK 32: dense A only");
@@ -373,66 +395,126 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
 #pragma unroll
     for (int jj = 0; jj < T::FN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int stage) {
+  // fragments of one 32-deep K-step, double-buffered in registers: the next step's ds_reads are in flight
+  // while this step's MFMAs issue (a barrier-separated read-then-multiply step would leave the MFMA pipe idle
+  // for the whole LDS read of every step, all waves phase-locked by the barrier)
+  struct Frags {
+    bf16x8 ah[T::FM], bh[T::FN];
+    bf16x8 al[SPLIT ? T::FM : 1], bl[SPLIT ? T::FN : 1];
+  };
+  auto read = [&](int stage, int s, Frags& f) {
     const bf16_t* S = smem + stage * T::STAGE;
+    const int c = 4 * s + (lane >> 4);
 #pragma unroll
-    for (int s = 0; s < BK / 32; ++s) {
-      const int c = 4 * s + (lane >> 4);
-      bf16x8 ah[T::FM], bh[T::FN];
-      bf16x8 al[SPLIT ? T::FM : 1], bl[SPLIT ? T::FN : 1];
+    for (int i = 0; i < T::FM; ++i) {
+      const int row = wm * T::WM + i * 16 + (lane & 15);
+      f.ah[i] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(row, c));
+      if (SPLIT) f.al[i] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(BM + row, c));
+    }
 #pragma unroll
-      for (int i = 0; i < T::FM; ++i) {
-        const int row = wm * T::WM + i * 16 + (lane & 15);
-        ah[i] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(row, c));
-        if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(BM + row, c));
-      }
-#pragma unroll
-      for (int jj = 0; jj < T::FN; ++jj) {
-        const int row = T::AROWS + wn * T::WN + jj * 16 + (lane & 15);
-        bh[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(row, c));
-        if (SPLIT) bl[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(BN + row, c));
-      }
-#pragma unroll
-      for (int i = 0; i < T::FM; ++i)
-#pragma unroll
-        for (int jj = 0; jj < T::FN; ++jj) {
-          acc[i][jj] = mfma16<SPLIT>(bh[jj], ah[i], acc[i][jj]);
-          if (SPLIT) {
-            acc[i][jj] = mfma16<SPLIT>(bl[jj], ah[i], acc[i][jj]);
-            acc[i][jj] = mfma16<SPLIT>(bh[jj], al[i], acc[i][jj]);
-          }
-        }
+    for (int jj = 0; jj < T::FN; ++jj) {
+      const int row = T::AROWS + wn * T::WN + jj * 16 + (lane & 15);
+      f.bh[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(row, c));
+      if (SPLIT) f.bl[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<BK>(BN + row, c));
     }
   };
+  auto mma = [&](const Frags& f) {
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj) {
+        acc[i][jj] = mfma16<SPLIT>(f.bh[jj], f.ah[i], acc[i][jj]);
+        if (SPLIT) {
+          acc[i][jj] = mfma16<SPLIT>(f.bl[jj], f.ah[i], acc[i][jj]);
+          acc[i][jj] = mfma16<SPLIT>(f.bh[jj], f.al[i], acc[i][jj]);
+        }
+      }
+  };
 
-  // K loop over an LDS ring of NSTAGE buffers: tiles kt+1 .. kt+NSTAGE-1 are in flight while tile kt
-  // is multiplied.  A tile is read only after the issuing waves' counted vmcnt retired it AND a
-  // barrier (raw s_barrier: __syncthreads() would drain every in-flight LDS-DMA with vmcnt(0)).
   // Split-K (EPI_PARTIAL): workgroup row blockIdx.y takes K-tiles [kbeg, kend) and stores raw sums.
   const int nk_all = K / BK;
   const int kbeg = EPI == EPI_PARTIAL ? (int)((int64_t)blockIdx.y * nk_all / args.ksplit) : 0;
   const int kend = EPI == EPI_PARTIAL ? (int)((int64_t)(blockIdx.y + 1) * nk_all / args.ksplit) : nk_all;
   const int nk = kend - kbeg;
-  constexpr int D = T::NSTAGE - 1;   // tiles in flight ahead of the one being multiplied
-  for (int p = 0; p < D; ++p)
-    if (p < nk) issue(kbeg + p, p);
-  if (nk > 1 && D > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  GEMM_STAMP(1);
-  int stage = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = kt + D;
-    if (ahead < nk) issue(kbeg + ahead, ahead % T::NSTAGE);
-    compute(stage);
-    stage = stage + 1 == T::NSTAGE ? 0 : stage + 1;
-    // retire tile kt+1: the loads issued after it (tiles kt+2 .. min(kt+D, nk-1)) may stay in flight
-    const int after = min(kt + D, nk - 1) - (kt + 1);
-    if (D > 1 && after >= D - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  constexpr int NS = T::NSTAGE, SPK = BK / 32;
+  // Register-pipelined loop (DBUF) where the LDS ring already limits the CU to one workgroup (> 80 KB) and a
+  // step has enough MFMAs to cover its reads: the second fragment set (146 VGPRs for the 128 x 128 f16x3 tile,
+  // 98 without) would otherwise halve the workgroups per CU (proj, 2-stage 32-deep: 47 -> 55 us)
+  constexpr int FRAG_REGS = (T::FM + T::FN) * (SPLIT ? 2 : 1) * 4;
+  constexpr bool DBUF = T::NSTAGE * T::STAGE * 2 > 80 * 1024 && T::FM * T::FN >= 4 &&
+                        T::FM * T::FN * 4 + 2 * FRAG_REGS <= 192;
+  if constexpr (DBUF) {
+    // One 32-deep step at a time (BK / 32 steps per K-tile).  At the last step of K-tile kt the wave retires
+    // tile kt + 1's loads (counted vmcnt: younger tiles stay in flight) and its own reads of tile kt
+    // (lgkmcnt), and meets the others at a barrier (raw s_barrier: __syncthreads() would drain every in-flight
+    // LDS-DMA with vmcnt(0)); tile kt's stage is then free and takes tile kt + NSTAGE.  The next step's
+    // fragments are read into the other register set while this step's MFMAs issue.
+    for (int p = 0; p < NS; ++p)
+      if (p < nk) issue(kbeg + p, p);
+    vm_wait_rt<GPW*(NS - 1)>(GPW * (min(NS, nk) - 1));   // tile 0 landed (this wave's part)
     __builtin_amdgcn_s_barrier();
+    GEMM_STAMP(1);
+    const int nsteps = nk * SPK;
+    int stage = 0;   // stage of the K-tile of the current step
+    auto boundary = [&](int kt) {
+      // loads issued after tile kt + 1: tiles kt + 2 .. min(kt + NS - 1, nk - 1)
+      vm_wait_rt<GPW*(NS - 2 > 0 ? NS - 2 : 0)>(GPW * (min(kt + NS - 1, nk - 1) - (kt + 1)));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + NS < nk) issue(kbeg + kt + NS, stage);
+      stage = stage + 1 == NS ? 0 : stage + 1;
+    };
+    Frags f0, f1;
+    if (nk > 0) read(0, 0, f0);
+    // The next fragments are read unconditionally (after the last step: a harmless re-read of the current
+    // stage), so no branch separates them from the MFMAs.  The scheduler is told the order: one MFMA of cur
+    // (its lgkmcnt wait sits before it, while no read of nxt is pending), then each read of nxt followed by a
+    // few more MFMAs -- left alone it sinks the reads below the MFMAs, into cur's registers.
+    auto step = [&](int t, const Frags& cur, Frags& nxt) {
+      const int s = SPK == 1 ? 0 : (t & 1);
+      if (s == SPK - 1 && t + 1 < nsteps) boundary(t / SPK);
+      mma(cur);
+      read(stage, s == SPK - 1 ? 0 : s + 1, nxt);
+      constexpr int NR = (T::FM + T::FN) * (SPLIT ? 2 : 1), NM = T::FM * T::FN * (SPLIT ? 3 : 1);
+      constexpr int KPER = (NM - 1) / NR > 0 ? (NM - 1) / NR : 1;
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      sched_interleave<NR, KPER>();
+    };
+    for (int t = 0; t < nsteps; t += 2) {
+      step(t, f0, f1);
+      if (t + 1 < nsteps) step(t + 1, f1, f0);
+    }
+  } else {
+    // tiles kt+1 .. kt+NSTAGE-1 are in flight while tile kt is read and multiplied; a tile is read only after the
+    // issuing waves' counted vmcnt retired it AND a barrier
+    constexpr int D = NS - 1;
+    for (int p = 0; p < D; ++p)
+      if (p < nk) issue(kbeg + p, p);
+    if (nk > 1 && D > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    GEMM_STAMP(1);
+    int stage = 0;
+    Frags f;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int ahead = kt + D;
+      if (ahead < nk) issue(kbeg + ahead, ahead % NS);
+#pragma unroll
+      for (int s = 0; s < SPK; ++s) {
+        read(stage, s, f);
+        mma(f);
+      }
+      stage = stage + 1 == NS ? 0 : stage + 1;
+      // retire tile kt+1: the loads issued after it (tiles kt+2 .. min(kt+D, nk-1)) may stay in flight
+      const int after = min(kt + D, nk - 1) - (kt + 1);
+      if (D > 1 && after >= D - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
   GEMM_STAMP(2);
   // ---- epilogue: lane owns C[m][n..n+3]
@@ -716,17 +798,6 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_persist_kernel(const GemmA
 // the same number of stores).  vmcnt bookkeeping: a step's wait lets the younger ring loads stay in
 // flight and, within NS - 1 steps after an epilogue, that epilogue's stores and the next tile's bias
 // loads (issued after it) as well.
-template <int N>
-__device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-template <int MAXN>
-__device__ __forceinline__ void vm_wait_rt(int n) {   // n wave-uniform; scalar branch to an immediate
-  if constexpr (MAXN > 0) {
-    if (n >= MAXN) return vm_wait_n<MAXN>();
-    return vm_wait_rt<MAXN - 1>(n);
-  } else {
-    vm_wait_n<0>();
-  }
-}
 
 
 template <int BM, int BN, int WMW, int WNW, int EPI, int NS, int BK>
