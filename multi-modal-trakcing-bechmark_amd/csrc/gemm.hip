@@ -441,7 +441,10 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   // step has enough MFMAs to cover its reads: the second fragment set (146 VGPRs for the 128 x 128 f16x3 tile,
   // 98 without) would otherwise halve the workgroups per CU (proj, 2-stage 32-deep: 47 -> 55 us)
   constexpr int FRAG_REGS = (T::FM + T::FN) * (SPLIT ? 2 : 1) * 4;
-  constexpr bool DBUF = T::NSTAGE * T::STAGE * 2 > 80 * 1024 && T::FM * T::FN >= 4 &&
+#ifndef GEMM_DBUF_ALL
+#define GEMM_DBUF_ALL 0
+#endif
+  constexpr bool DBUF = (T::NSTAGE * T::STAGE * 2 > 80 * 1024 || (GEMM_DBUF_ALL && SPLIT)) && T::FM * T::FN >= 4 &&
                         T::FM * T::FN * 4 + 2 * FRAG_REGS <= 192;
   if constexpr (DBUF) {
     // One 32-deep step at a time (BK / 32 steps per K-tile).  At the last step of K-tile kt the wave retires
@@ -1647,6 +1650,25 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         if (n768 == 3) return launch_cfg<128, 256, 2, 4, true, 2, 32>(a, epi, s);
       }
       if (a.K <= 1024 && a.amode == A_DENSE) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
+      // MMT_SK128 (tuning): a long-K residual GEMM with too few tiles for whole rounds of workgroups (fc2 in the
+      // CE-pruned layers: 114-186 tiles of one 128-KB workgroup per CU) splits K so that rounds x (1 / ks) drops,
+      // the slabs left for the consumer's deferred reduce.  Measured against the two-stream halves (whose other
+      // half fills the tail): up to 8 slices -2.8 %, at most 2 (the 152-token layers only) level (tests/r3_run22.sh)
+      static const int sk128 = getenv("MMT_SK128") ? atoi(getenv("MMT_SK128")) : 0;
+      if (sk128 > 0 && a.ws && a.defer_reduce && epi == EPI_RESID_F32 && a.groups == 1 && a.amode == A_DENSE) {
+        const int tiles = t128 * (a.N / 128), nk = a.K / 64, slots = num_cus();
+        int best = 1;
+        double bcost = (double)((tiles + slots - 1) / slots);
+        for (int ks = 2; ks <= (sk128 > 1 ? sk128 : kMaxDeferKs); ++ks) {
+          if (nk / ks < 8 || (int64_t)ks * a.M * a.N > a.ws_elems - kSkCounters) break;
+          const double cost = (double)((tiles * ks + slots - 1) / slots) / ks;
+          if (cost < 0.9 * bcost) {
+            best = ks;
+            bcost = cost;
+          }
+        }
+        if (best > 1) return launch_splitk<128, 128, 4, 2, A_DENSE, true, 2>(a, epi, best, s);
+      }
       return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);
     }
   }
