@@ -185,6 +185,9 @@ __device__ __forceinline__ float fovea_s8(float a, float cc, const float* st, in
 }
 
 // ------------------------------------------------------------------ LayerNorm (optionally fused CE gather)
+// RR: a pending split-K update may be applied (its up-to-8 slabs take 96 VGPRs: the variant without them keeps
+// more waves per CU)
+template <bool RR>
 __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w, const float* b, bf16_t* ob,
                                                  bf16_t* olo, float oscale, float* of, int rows, int rows_per_seq,
                                                  const int* gather, int in_rows_per_seq, float* xcopy,
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
     src = (int64_t)bs * in_rows_per_seq + gather[r];
   }
   Row12 xv = load_row(x + src * C768, lane);
-  if (rr.ws) {   // the pending split-K update of the residual stream (proj / fc2), then X is current again
+  if (RR && rr.ws) {   // the pending split-K update of the residual stream (proj / fc2), then X is current again
     xv = apply_reduce(xv, rr, src, lane);
     if (!xcopy) store_f32(const_cast<float*>(x) + src * C768, xv, lane);
   }
@@ -211,8 +214,12 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
 void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float out_scale,
                float* out_f32, int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy,
                hipStream_t s, const RowReduce& rr) {
-  hipLaunchKernelGGL(ln_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_scale, out_f32,
-                     rows, rows_per_seq, gather, in_rows_per_seq, xcopy, rr);
+  if (rr.ws)
+    hipLaunchKernelGGL(ln_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_scale,
+                       out_f32, rows, rows_per_seq, gather, in_rows_per_seq, xcopy, rr);
+  else
+    hipLaunchKernelGGL(ln_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_scale,
+                       out_f32, rows, rows_per_seq, gather, in_rows_per_seq, xcopy, rr);
 }
 
 // ------------------------------------------------------------------ prompt block, part 1
@@ -305,10 +312,11 @@ __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) 
 constexpr int TOK_THREADS = 512;   // 8 waves per block share one LDS copy of the weights
 constexpr int TOK_ROWS = TOK_THREADS / 64;
 
+template <bool RR>
 __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const PromptArgs a) {
   __shared__ float fold[FOLD_N];
   __shared__ __attribute__((aligned(16))) float W0[8 * C768];   // conv0_0 (LN_A affine folded in)
-  __shared__ __attribute__((aligned(16))) float va[FOVEA_MAX_TOKENS * 8];
+  extern __shared__ __attribute__((aligned(16))) float va[];   // [L][8] (dynamic: sized by the launch)
   __shared__ float red[64], st[32];
   const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, b = blockIdx.y;
   const FoveaStage fsg = fovea_stage(a.a8p + (int64_t)b * L * 8, L);
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
   if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
   fovea_stats(fsg, a.Lz, a.Lx, a.smooth_p, va, red, st);   // ends with a barrier
   if (!valid) return;
-  if (pos >= 0 && a.rr.ws) {   // the previous block's fc2 update of this slot's residual row, written back
+  if (RR && pos >= 0 && a.rr.ws) {   // the previous block's fc2 update of this slot's residual row, written back
     x = apply_reduce(x, a.rr, xrow, lane);
     store_f32(const_cast<float*>(a.srcA) + xrow * C768, x, lane);
   }
@@ -378,7 +386,13 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
     const int waves = (a.B * L + PR_ROWS - 1) / PR_ROWS;
     hipLaunchKernelGGL(prompt_reduce_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL(prompt_reduce_deep_kernel, dim3((L + TOK_ROWS - 1) / TOK_ROWS, a.B), dim3(TOK_THREADS), 0, s, a);
+    // the sequence's a8 in LDS takes L x 32 B, not the 32-KB maximum: at 320 tokens four blocks fit a CU instead
+    // of two, so the 640 blocks of a 16-sequence half run in one round
+    const dim3 grid((L + TOK_ROWS - 1) / TOK_ROWS, a.B);
+    if (a.rr.ws)
+      hipLaunchKernelGGL(prompt_reduce_deep_kernel<true>, grid, dim3(TOK_THREADS), (size_t)L * 8 * sizeof(float), s, a);
+    else
+      hipLaunchKernelGGL(prompt_reduce_deep_kernel<false>, grid, dim3(TOK_THREADS), (size_t)L * 8 * sizeof(float), s, a);
   }
 }
 
@@ -393,10 +407,15 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
 // then out = LN(X[r]) (norm1 of the block).  One block = 8 compact rows of one sequence, one per wave; the
 // slot, rows and weights are all requested before the statistics and barriers.
 template <int MODE>
-__global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptArgs a) {
+// LNP_WPE (build-time tuning): waves per SIMD the register allocation targets; 6 (80 VGPRs, three blocks per CU)
+// spills 5 VGPRs in mode 2 and measured -0.35 % at 32 sequences against the default (tests/r3_run23.sh)
+#ifndef LNP_WPE
+#define LNP_WPE 1
+#endif
+__global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP_WPE))) void ln_prompt_kernel(const LnPromptArgs a) {
   __shared__ __attribute__((aligned(16))) float W1t[8 * C768];
   __shared__ __attribute__((aligned(16))) float cst[3 * C768];   // conv1x1 bias, norm1 weight, norm1 bias
-  __shared__ __attribute__((aligned(16))) float va[FOVEA_MAX_TOKENS * 8];
+  extern __shared__ __attribute__((aligned(16))) float va[];   // [L][8] (dynamic: sized by the launch)
   __shared__ float red[64], st[32];
   const int lane = threadIdx.x & 63, b = blockIdx.y, L = a.Lz + a.Lx;
   const FoveaStage fsg = fovea_stage(a.a8 + (int64_t)b * L * 8, L);
@@ -472,10 +491,11 @@ __global__ __launch_bounds__(TOK_THREADS) void ln_prompt_kernel(const LnPromptAr
 
 void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s) {
   const dim3 grid((a.rows_per_seq + TOK_ROWS - 1) / TOK_ROWS, a.rows / a.rows_per_seq);
+  const size_t va_bytes = (size_t)(a.Lz + a.Lx) * 8 * sizeof(float);
   if (a.mode == 1)
-    hipLaunchKernelGGL(ln_prompt_kernel<1>, grid, dim3(TOK_THREADS), 0, s, a);
+    hipLaunchKernelGGL(ln_prompt_kernel<1>, grid, dim3(TOK_THREADS), va_bytes, s, a);
   else
-    hipLaunchKernelGGL(ln_prompt_kernel<2>, grid, dim3(TOK_THREADS), 0, s, a);
+    hipLaunchKernelGGL(ln_prompt_kernel<2>, grid, dim3(TOK_THREADS), va_bytes, s, a);
 }
 
 // ------------------------------------------------------------------ candidate elimination
