@@ -21,6 +21,7 @@ namespace mmt {
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4* lds_bf16x4_t;
+typedef __attribute__((address_space(3))) void* lds_void_t;
 
 constexpr int KB = 64;         // keys per LDS tile
 constexpr int CE_MAX = 1024;   // max tokens for the exported CE row
@@ -41,7 +42,8 @@ __device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (
 // few (sequence, head) pairs (one sequence: 12), where a lone wave per row block would load every K / V tile
 // by itself
 template <int WAVES, bool SPLIT, int RB = 1, bool KSPLIT = false>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVES < 4 || KSPLIT ? 1 : (SPLIT ? ATTN_WPE_SPLIT : ATTN_WPE)))) void attn_kernel(const AttnArgs a) {
+// (the 8-wave f16x3 kernel is held to 128 VGPRs: two workgroups per CU)
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVES < 4 || KSPLIT ? 1 : (SPLIT ? (WAVES >= 8 ? 4 : ATTN_WPE_SPLIT) : ATTN_WPE)))) void attn_kernel(const AttnArgs a) {
   // SPLIT (fp32-faithful f16x3, common.h): every operand is an (hi, lo) fp16 pair of a range-scaled
   // value and each product is hi*hi + lo*hi + hi*lo; the LDS images of K and V^T hold both halves.
   // RB: 16-query row blocks per wave, multiplied together against each K / V fragment (fragment
@@ -51,7 +53,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
   constexpr int NH = SPLIT ? 2 : 1;
   constexpr int QW = 16 * RB;   // queries per wave
   constexpr int QWAVES = KSPLIT ? 1 : WAVES;   // waves with distinct queries
-  constexpr int KW = KSPLIT ? WAVES : 1;       // K / V staging slots
+  // DMA: K / V tiles go HBM -> LDS by buffer_load ... lds (no VGPRs, no LDS writes by the waves) into a ring of two
+  // stages, one barrier per tile.  The key split, and the f16x3 kernels of fewer than 8 waves (whose 68-KB ring
+  // would cost them workgroups per CU), stage through registers into one slot per wave / per workgroup.
+  constexpr bool DMA = !KSPLIT && (WAVES >= 8 || !SPLIT);
+  constexpr int KW = KSPLIT ? WAVES : (DMA ? 2 : 1);   // K / V staging slots (per wave, ring stages, or one)
   __shared__ __attribute__((aligned(16))) bf16_t KsAll[KW][NH][KB * 64];
   __shared__ __attribute__((aligned(16))) bf16_t VsAll[KW][NH][KB * 64];
   __shared__ float ce_row[CE_MAX];
@@ -65,9 +71,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
   const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + jx;
   const int qt = lid % nqt, bh = lid / nqt;
   const int b = bh / a.heads, h = bh - b * a.heads;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  bf16_t(&Ks)[NH][KB * 64] = KsAll[KSPLIT ? wave : 0];
-  bf16_t(&Vs)[NH][KB * 64] = VsAll[KSPLIT ? wave : 0];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
   const int N = a.N, Cd = 64 * a.heads, C3 = 3 * Cd;
   const bf16_t* base = a.qkv + (int64_t)b * N * C3;
   const int q0 = qt * (QW * QWAVES) + (KSPLIT ? 0 : wave * QW);
@@ -124,6 +129,25 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
     if constexpr (KSPLIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     else __syncthreads();
   };
+  // LDS-DMA pieces: one wave-instruction fills 8 key rows x 128 B of one image (K or V, hi or lo); lane l lands at
+  // byte 16 l of the piece = row l >> 3, chunk position l & 7, so it loads the source chunk (l & 7) ^ (l >> 3) that
+  // tile_off puts there.  Keys past N read zeros (offset past the resource).
+  constexpr int NPIECE = 2 * NH * 8, PPW = NPIECE / WAVES;
+  static_assert(!DMA || NPIECE % WAVES == 0, "pieces must divide over the waves");
+  const rsrc_t rq = make_rsrc(base, (int64_t)N * C3 * 2);
+  const rsrc_t rql = SPLIT ? make_rsrc(base_lo, (int64_t)N * C3 * 2) : rq;
+  auto issue = [&](int kb, int st) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int p = wave * PPW + j;                        // wave-uniform
+      const int kv = p / (8 * NH), hl = (p / 8) % NH, rb = p % 8;
+      const int key = kb + rb * 8 + (lane >> 3), c = (lane & 7) ^ (lane >> 3);
+      const uint32_t vo = key < N ? (uint32_t)(((int64_t)key * C3 + (kv ? 2 * Cd : Cd) + h * 64 + c * 8) * 2) : kBufOob;
+      bf16_t* img = kv ? &VsAll[st][hl][0] : &KsAll[st][hl][0];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(hl ? rql : rq, (lds_void_t)(img + rb * 8 * 64), 16, vo, 0, 0, 0);
+    }
+  };
+
   uint4 kreg[NCHT], vreg[NCHT];
   auto fetch = [&](int kb) {
 #pragma unroll
@@ -143,20 +167,36 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
   };
   const int kb0 = KSPLIT ? wave * KB : 0;
   constexpr int KSTEP = KSPLIT ? WAVES * KB : KB;
-  if (kb0 < N) fetch(kb0);
+  if constexpr (DMA) {
+    if (kb0 < N) issue(kb0, 0);
+  } else {
+    if (kb0 < N) fetch(kb0);
+  }
+  int stage = 0;
   for (int kb = kb0; kb < N; kb += KSTEP) {
-    tile_sync();
+    if constexpr (DMA) {
+      // this tile's pieces landed (the only loads in flight) and every wave is past the previous tile, whose
+      // stage then takes the next tile
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kb + KSTEP < N) issue(kb + KSTEP, stage ^ 1);
+    } else {
+      tile_sync();
 #pragma unroll
-    for (int i = 0; i < NCHT; ++i) {
-      const int q = ltid + i * LT;
-      if (!CH_EXACT && q >= NCHUNK) break;
-      const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
-      const int r = qq >> 3, c = qq & 7;
-      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Ks[hl]) + tile_off(r, c)) = kreg[i];
-      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(Vs[hl]) + tile_off(r, c)) = vreg[i];
+      for (int i = 0; i < NCHT; ++i) {
+        const int q = ltid + i * LT;
+        if (!CH_EXACT && q >= NCHUNK) break;
+        const int hl = q / (KB * 8), qq = q - hl * (KB * 8);
+        const int r = qq >> 3, c = qq & 7;
+        *reinterpret_cast<uint4*>(reinterpret_cast<char*>(KsAll[KSPLIT ? wave : 0][hl]) + tile_off(r, c)) = kreg[i];
+        *reinterpret_cast<uint4*>(reinterpret_cast<char*>(VsAll[KSPLIT ? wave : 0][hl]) + tile_off(r, c)) = vreg[i];
+      }
+      tile_sync();
+      if (kb + KSTEP < N) fetch(kb + KSTEP);
     }
-    tile_sync();
-    if (kb + KSTEP < N) fetch(kb + KSTEP);
+    bf16_t(&Ks)[NH][KB * 64] = KsAll[DMA ? stage : (KSPLIT ? wave : 0)];
+    bf16_t(&Vs)[NH][KB * 64] = VsAll[DMA ? stage : (KSPLIT ? wave : 0)];
+    stage ^= 1;
 
     f32x4 sc[RB][4];
 #pragma unroll
