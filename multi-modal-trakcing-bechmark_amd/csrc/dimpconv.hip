@@ -346,6 +346,141 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.y * 7 + blockIdx.z * 13, reinterpret_cast<float*>(&sA[0][0][0]));
 }
 
+// The stem (kh x kw / stride on a 4-channel image -- 3 channels padded with a zero one, mmt_image_normalize4 --
+// and 64 output channels) as 2-D tiles of 8 x 16 output pixels: the tile's input patch ((8 - 1) s + kh rows x
+// (16 - 1) s + kw columns, zeros outside the image) is loaded ONCE, split into fp16 hi / lo into LDS, and every
+// K-tile's A fragments are read from it (a tap is 4 channels, 8 B per half); the weights of all K-tiles arrive
+// by LDS-DMA alongside.  One dependent round trip per workgroup instead of one per K-tile
+// (conv_f16x3_kernel<64, true>: 7 K-tiles of register-staged gathers), with the same products in the same
+// order, so the output is that kernel's bit for bit.
+// TH: tile rows (8 or 16; 16 halves the weight re-fetch per output pixel, 79 KB of LDS: still two workgroups per CU)
+constexpr int kStemTW = 16, kStemMaxKt = 7;
+template <int TH>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_stem_f16x3_kernel(const ConvF16Args a) {
+  constexpr int kStemTH = TH, kStemMaxP = ((TH - 1) * 2 + 7) * ((kStemTW - 1) * 2 + 7), NPL = (kStemMaxP + 511) / 512;
+  constexpr int BN = 64, BK = 32, WN = BN / 2, FM = TH / 4, FN = WN / 16;
+  __shared__ __attribute__((aligned(16))) uint16_t sP[2][(kStemMaxP + 1) * 4];   // [hi, lo][pixel][4 ch]; + a zero pixel
+  __shared__ __attribute__((aligned(16))) uint16_t sW[kStemMaxKt][2][BN * BK];
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int grp = blockIdx.z;
+  const ConvGroupArgs g = pick_group(a, grp);
+  const int tiles_x = (a.Wo + kStemTW - 1) / kStemTW, tiles_y = (a.Ho + kStemTH - 1) / kStemTH;
+  const int img = blockIdx.x / (tiles_x * tiles_y), trem = blockIdx.x - img * (tiles_x * tiles_y);
+  const int ty = trem / tiles_x, tx = trem - ty * tiles_x;
+  const int oy0 = ty * kStemTH, ox0 = tx * kStemTW;
+  const int PW = (kStemTW - 1) * a.stride + a.kw, NP = ((kStemTH - 1) * a.stride + a.kh) * PW;
+  const int iy0 = oy0 * a.stride - a.pad, ix0 = ox0 * a.stride - a.pad;
+  const int nk = a.Kp / BK, taps = a.kh * a.kw;
+
+  float sa = g.xscale;
+  if (g.xmax) {
+    const float mx = wave_max(g.xmax[lane * kShardStride]);
+    sa = mx > 0.f ? pow2_scale(mx) : 1.0f;
+  }
+  const float inv = g.inv_w / sa;
+
+  // the weights of every K-tile: one 16-row x 64-B piece per wave and K-tile (conv_f16x3_kernel's load_w, BN = 64)
+  const u32x4 qWh = make_rsrc_words(g.wh, (int64_t)a.Cout * a.Kp * 2);
+  const u32x4 qWl = make_rsrc_words(g.wl, (int64_t)a.Cout * a.Kp * 2);
+  {
+    const int wimg = wave / (BN / 16), rb = wave % (BN / 16);
+    const int row = rb * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 2);
+    const uint32_t vo = (uint32_t)((row * a.Kp + c * 8) * 2);
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lptr_t)(&sW[kt][wimg][rb * 16 * BK]));
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(kt * BK * 2));
+      if (wimg)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWl), "s"(so), "{m0}"(dst) : "memory");
+      else
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWh), "s"(so), "{m0}"(dst) : "memory");
+    }
+  }
+  // the input patch: pixel q = t + 512 k of the patch, one float4 (4 channels) each
+  const rsrc_t rX = make_rsrc(g.x, (int64_t)a.N * a.H * a.W * 16);
+  float4 pv[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int q = t + 512 * k, py = q / PW, px = q - py * PW;
+    const int iy = iy0 + py, ix = ix0 + px;
+    const bool ok = q < NP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    const uint32_t vo = ok ? (uint32_t)(((img * a.H + iy) * a.W + ix) * 16) : kBufOob;
+    pv[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rX, vo, 0, 0));
+  }
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int q = t + 512 * k;
+    if (q < NP) {
+      uint16_t h[4], l[4];
+      split_h(pv[k].x * sa, h[0], l[0]);
+      split_h(pv[k].y * sa, h[1], l[1]);
+      split_h(pv[k].z * sa, h[2], l[2]);
+      split_h(pv[k].w * sa, h[3], l[3]);
+      *reinterpret_cast<uint2*>(&sP[0][q * 4]) = make_uint2(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16);
+      *reinterpret_cast<uint2*>(&sP[1][q * 4]) = make_uint2(l[0] | (uint32_t)l[1] << 16, l[2] | (uint32_t)l[3] << 16);
+    }
+  }
+  if (t < 2) *reinterpret_cast<uint2*>(&sP[t][kStemMaxP * 4]) = make_uint2(0u, 0u);   // the zero taps' pixel
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fragment row = local pixel wm * 16 FM + i * 16 + (lane & 15): tile row wm * FM + i, column lane & 15; K chunk
+  // lane >> 4 = taps 8 kt + 2 (lane >> 4) + (0, 1), 4 channels each (conv_f16x3_kernel's STEM K order)
+  const int c = lane >> 4, col = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    bf16x8 ah[FM], al[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int r = wm * FM + i;
+      uint2 hv[2], lv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int tap = kt * 8 + 2 * c + h, ky = tap / a.kw, kx = tap - ky * a.kw;
+        const int pix = tap < taps ? (r * a.stride + ky) * PW + col * a.stride + kx : kStemMaxP;
+        hv[h] = *reinterpret_cast<const uint2*>(&sP[0][pix * 4]);
+        lv[h] = *reinterpret_cast<const uint2*>(&sP[1][pix * 4]);
+      }
+      ah[i] = __builtin_bit_cast(bf16x8, make_uint4(hv[0].x, hv[0].y, hv[1].x, hv[1].y));
+      al[i] = __builtin_bit_cast(bf16x8, make_uint4(lv[0].x, lv[0].y, lv[1].x, lv[1].y));
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * WN + j * 16 + (lane & 15);
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(&sW[kt][0][cswz(row, c)]);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&sW[kt][1][cswz(row, c)]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        acc[i][j] = mfma16<true>(bh, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bl, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bh, al[i], acc[i][j]);
+      }
+    }
+  }
+
+  const int lk = lane >> 4;
+  float ymx = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int oy = oy0 + wm * FM + i, ox = ox0 + col;
+    if (oy >= a.Ho || ox >= a.Wo) continue;
+    const int64_t mo = ((int64_t)img * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int no = wn * WN + j * 16 + 4 * lk;
+      const f32x4 v = conv_out(g, acc[i][j] * inv, mo, no, a.Cout);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
+    }
+  }
+  __syncthreads();   // the patch is free for the max fold
+  if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.z * 13, reinterpret_cast<float*>(&sP[0][0]));
+}
+
 // split-K: y = sum over the ks slices (in slice order) + bias (+ residual), ReLU, merge; grid (blocks, G), 4 channels
 // per thread
 __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvF16Args a) {
@@ -472,7 +607,17 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   const int bn = conv_bn((M + 127) / 128, Cin, Cout, G);
   const dim3 grid(gm, Cout / bn, G * ks);
   const hipStream_t s = (hipStream_t)stream;
-  if (Cin <= 4)
+  // the stem on a 4-channel image: 2-D tiles from an LDS input patch (MMT_CONV_STEM_OLD: the gather kernel, tuning)
+  static const bool stem_old = getenv("MMT_CONV_STEM_OLD") != nullptr;
+  static const int stem_th = getenv("MMT_CONV_STEM_TH") ? atoi(getenv("MMT_CONV_STEM_TH")) : 16;   // tuning: 8
+  if (!stem_old && Cin == 4 && Cout == 64 && ks == 1 && kh <= 7 && kw <= 7 && stride <= 2 && Kp / 32 <= kStemMaxKt) {
+    const int th = stem_th == 8 ? 8 : 16;
+    const unsigned tiles = (unsigned)(((Ho + th - 1) / th) * ((Wo + kStemTW - 1) / kStemTW) * N);
+    if (th == 8)
+      hipLaunchKernelGGL(conv_stem_f16x3_kernel<8>, dim3(tiles, 1, G), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL(conv_stem_f16x3_kernel<16>, dim3(tiles, 1, G), dim3(512), 0, s, a);
+  } else if (Cin <= 4)
     hipLaunchKernelGGL((conv_f16x3_kernel<64, true>), grid, dim3(512), 0, s, a);
   else if (bn == 128)
     hipLaunchKernelGGL((conv_f16x3_kernel<128, false>), grid, dim3(512), 0, s, a);
