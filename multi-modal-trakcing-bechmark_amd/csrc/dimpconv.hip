@@ -513,7 +513,11 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvF16Ar
 // slices), at least 8 K-tiles per slice.  256 slots (one workgroup per CU) measured +1 % over 512 and level
 // with no split at all once the two backbones share a launch (profiles/r03_ab_conv_slots.txt)
 int conv_pick_ks(int64_t tiles, int nk) {
-  static const int64_t kSlots = getenv("MMT_CONV_SLOTS") ? atoi(getenv("MMT_CONV_SLOTS")) : 256;   // tuning
+  // slots: 256 (one workgroup per CU); long-K layers (>= 72 K-tiles: layer3's 3 x 3 convs, the 3 x 3 clf conv
+  // over 1 024 channels) count two per CU -- the clf conv 466 -> 410 us, layer3 conv2 117 -> 113 us, while the
+  // short-K layers lose with it (layer3 conv1 58 -> 70 us; tests/bench_conv_f16x3.py, r3_run30.sh)
+  static const int64_t kSlotsEnv = getenv("MMT_CONV_SLOTS") ? atoi(getenv("MMT_CONV_SLOTS")) : 0;   // tuning
+  const int64_t kSlots = kSlotsEnv > 0 ? kSlotsEnv : (nk >= 72 ? 512 : 256);
   static const bool nosplit = getenv("MMT_CONV_NOSPLIT") != nullptr;   // batch-invariant summation order
   if (tiles >= kSlots || nosplit) return 1;
   int best = 1;
