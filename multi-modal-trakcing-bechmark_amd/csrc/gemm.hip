@@ -1649,7 +1649,12 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         if (n768 == 2) return launch_cfg<256, 128, 4, 2, true, 2, 32>(a, epi, s);
         if (n768 == 3) return launch_cfg<128, 256, 2, 4, true, 2, 32>(a, epi, s);
       }
-      if (a.K <= 1024 && a.amode == A_DENSE) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
+      // (the N = 768 GEMMs -- proj, patch -- take the register-pipelined 64-deep tile since it exists: proj at one
+      // half's rows 31 -> 25 us (5 120 rows) .. 27 -> 22 us (2 432), tests/r3_run33.sh; the wide qkv / fc1 fallbacks
+      // keep the 32-deep ring, level or better there)
+      static const bool k32_all = getenv("MMT_SPLIT_K32") != nullptr;   // tuning: the 32-deep tile for N = 768 too
+      if (a.K <= 1024 && a.amode == A_DENSE && (k32_all || a.N > 768))
+        return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
       // MMT_SK128 (tuning): a long-K residual GEMM with too few tiles for whole rounds of workgroups (fc2 in the
       // CE-pruned layers: 114-186 tiles of one 128-KB workgroup per CU) splits K so that rounds x (1 / ks) drops,
       // the slabs left for the consumer's deferred reduce.  Measured against the two-stream halves (whose other
