@@ -140,6 +140,10 @@ int mmt_timing_read(mmt_engine* e, int* launches, double* total_ms, double* flop
 /* out[b][0][y][x] = scale * sum_c,i,j x[b][c][y+i][x+j] * z[b][c][i][j] + bias  (valid)        */
 int mmt_xcorr(const float* z, const float* x, float* out, int B, int C, int hz, int wz, int hx, int wx,
               float scale, float bias, void* hip_stream);
+/* the same over NHWC maps (the HIP AlexNet's layout): z [hz][wz][C] at z + b * z_batch_stride floats (0: one
+ * exemplar for all B), x [B][hx][wx][C]; hz * wz * C <= 16384; 16-B aligned maps when C % 4 == 0         */
+int mmt_xcorr_nhwc(const float* z, int64_t z_batch_stride, const float* x, float* out, int B, int C, int hz, int wz,
+                   int hx, int wx, float scale, float bias, void* hip_stream);
 
 /* SiamFC per-frame steps around the correlation (TrackerSiamFC.init/update, published SiamFC; the
  * reference's RGBE/models/siamfc is an empty submodule):
@@ -150,6 +154,9 @@ int mmt_xcorr(const float* z, const float* x, float* out, int B, int C, int hz, 
  *     result (device) [4] = scale id, row, col, value; scratch: n*up*up floats (device).           */
 int mmt_siamfc_crop(const uint8_t* frame, int H, int W, int C, int64_t row_stride, int n, const int* y0,
                     const int* x0, const int* size, const int pad[3], int out_sz, float* out, void* hip_stream);
+/* mmt_siamfc_crop writing out [n][out_sz][out_sz][3] (NHWC, the HIP AlexNet's input)                */
+int mmt_siamfc_crop_nhwc(const uint8_t* frame, int H, int W, int C, int64_t row_stride, int n, const int* y0,
+                         const int* x0, const int* size, const int pad[3], int out_sz, float* out, void* hip_stream);
 int mmt_siamfc_response(const float* resp, int n, int r, int up, float scale_penalty, double window_influence,
                         const double* hann1d, double hann_sum, float* scratch, float* result, void* hip_stream);
 
@@ -180,6 +187,12 @@ int mmt_rgbx_merge(const uint8_t* rgb, int64_t rgb_stride, const uint8_t* aux, i
 /* nn.Conv2d (+ folded BN, + residual, ReLU): y [N*Ho*Wo][Cout] = conv(x [N][H][W][Cin]); Cout % 64 == 0 */
 int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w, const float* bias, int Cout, int kh,
                    int kw, int stride, int pad, const float* resid, float* y, int flags, void* hip_stream);
+/* the same with channel pitches: x pixels ldx floats apart (>= Cin), y / resid pixels ldy apart (>= Cout,
+ * % 4 == 0), so one group of a grouped nn.Conv2d (groups = g) is a call at x + i*Cin, w_i, bias + i*Cout,
+ * y + i*Cout (SiamFC's AlexNet, RGBE/models/siamfc); y, bias, resid 16-B aligned                     */
+int mmt_conv2d_f32_ld(const float* x, int N, int H, int W, int Cin, int ldx, const float* w, const float* bias,
+                      int Cout, int kh, int kw, int stride, int pad, const float* resid, float* y, int ldy, int flags,
+                      void* hip_stream);
 /* the same convolution on the fp16 matrix cores at fp32-faithful precision ("f16x3", csrc/dimpconv.hip):
  * w_hi / w_lo: fp16 halves of w * w_scale (w_scale a power of two with max|w| w_scale <= 2^14), layout
  * [Cout][Kp], K = kh*kw*Cin (Cin = 3: kh*kw*4, each tap padded to 4 channels), zero-padded to Kp =

@@ -34,6 +34,7 @@ struct ConvArgs {
   const float* resid;   // [M][Cout] or null
   float* y;             // [M][Cout], M = N * Ho * Wo
   int N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, flags;
+  int ldx, ldy;         // channel pitch of x / of y and resid (Cin / Cout; wider for one group of a grouped conv)
 };
 
 // ---------------------------------------------------------------------------------------------------
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
     ox = r - oy * a.Wo;
   }
   const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
-  const float* xb = a.x + (int64_t)nimg * a.H * a.W * a.Cin;
+  const float* xb = a.x + (int64_t)nimg * a.H * a.W * a.ldx;
   const float* wrow = a.w + (int64_t)(n0 + lr) * K;
   const int nk = (K + BK - 1) / BK;
   const int cpt = FAST ? a.Cin / BK : 1;   // K-tiles per tap
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
       const int ky = tap / a.kw, kx = tap - ky * a.kw;
       const int iy = iy0 + ky, ix = ix0 + kx;
       const bool ok = mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      const float* src = xb + ((int64_t)iy * a.W + ix) * a.Cin + c0;
+      const float* src = xb + ((int64_t)iy * a.W + ix) * a.ldx + c0;
 #pragma unroll
       for (int v = 0; v < VPT / 4; ++v) {
         ra[v] = ok ? *reinterpret_cast<const f32x4v*>(src + 4 * v) : f32x4v{0.f, 0.f, 0.f, 0.f};
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
       const int ky = tap / a.kw, kx = tap - ky * a.kw;
       const int iy = iy0 + ky, ix = ix0 + kx;
       const bool ok = tv && mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      const float* src = xb + ((int64_t)iy * a.W + ix) * 3;
+      const float* src = xb + ((int64_t)iy * a.W + ix) * a.ldx;
       ra[0] = ok ? f32x4v{src[0], src[1], src[2], 0.f} : f32x4v{0.f, 0.f, 0.f, 0.f};
       rb[0] = tv ? *reinterpret_cast<const f32x4v*>(wrow + tap * 4) : f32x4v{0.f, 0.f, 0.f, 0.f};
     } else {
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
           const int tap = k / a.Cin, c = k - tap * a.Cin;
           const int ky = tap / a.kw, kx = tap - ky * a.kw;
           const int iy = iy0 + ky, ix = ix0 + kx;
-          if (mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) va = xb[((int64_t)iy * a.W + ix) * a.Cin + c];
+          if (mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) va = xb[((int64_t)iy * a.W + ix) * a.ldx + c];
           vb = wrow[k];
         }
         ra[j / 4][j % 4] = va;
@@ -195,11 +196,11 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
       const int no = n0 + wc * 32 + c * 16 + 4 * lk;
       f32x4v v = acc[p][c];
       if (a.bias) v += *reinterpret_cast<const f32x4v*>(a.bias + no);
-      if (a.resid) v += *reinterpret_cast<const f32x4v*>(a.resid + (int64_t)mo * a.Cout + no);
+      if (a.resid) v += *reinterpret_cast<const f32x4v*>(a.resid + (int64_t)mo * a.ldy + no);
       if (a.flags & MMT_CONV_RELU)
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-      f32x4v* dst = reinterpret_cast<f32x4v*>(a.y + (int64_t)mo * a.Cout + no);
+      f32x4v* dst = reinterpret_cast<f32x4v*>(a.y + (int64_t)mo * a.ldy + no);
       if (a.flags & MMT_CONV_MAX) {
         const f32x4v o = *dst;
 #pragma unroll
@@ -511,30 +512,38 @@ static inline int last_err() { return hipGetLastError() == hipSuccess ? MMT_OK :
 
 extern "C" {
 
-int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w, const float* bias, int Cout, int kh,
-                   int kw, int stride, int pad, const float* resid, float* y, int flags, void* stream) {
-  if (!x || !w || !y || N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || Cout % 64 || kh <= 0 || kw <= 0 ||
-      stride <= 0 || pad < 0 || (flags & ~(MMT_CONV_RELU | MMT_CONV_MAX | MMT_CONV_W4)) ||
-      ((flags & MMT_CONV_W4) && Cin != 3))
+int mmt_conv2d_f32_ld(const float* x, int N, int H, int W, int Cin, int ldx, const float* w, const float* bias, int Cout,
+                      int kh, int kw, int stride, int pad, const float* resid, float* y, int ldy, int flags, void* stream) {
+  if (!x || !w || !y || N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || ldx < Cin || Cout <= 0 || Cout % 64 || ldy < Cout ||
+      ldy % 4 || (reinterpret_cast<uintptr_t>(y) & 15) || (resid && (reinterpret_cast<uintptr_t>(resid) & 15)) ||
+      (bias && (reinterpret_cast<uintptr_t>(bias) & 15)) || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 ||
+      (flags & ~(MMT_CONV_RELU | MMT_CONV_MAX | MMT_CONV_W4)) || ((flags & MMT_CONV_W4) && Cin != 3))
     return MMT_E_ARG;
-  ConvArgs a{x, w, bias, resid, y, N, H, W, Cin, Cout, kh, kw, stride, pad, 0, 0, flags};
+  ConvArgs a{x, w, bias, resid, y, N, H, W, Cin, Cout, kh, kw, stride, pad, 0, 0, flags, ldx, ldy};
   a.Ho = (H + 2 * pad - kh) / stride + 1;
   a.Wo = (W + 2 * pad - kw) / stride + 1;
   if (a.Ho <= 0 || a.Wo <= 0) return MMT_E_ARG;
   const int64_t M = (int64_t)N * a.Ho * a.Wo;
   if (M > (int64_t)1 << 30 || (int64_t)Cout * kh * kw * Cin > (int64_t)1 << 30) return MMT_E_ARG;
   const dim3 grid(blocks_for(M, 64), Cout / 64);
+  // the float4 operand loads of the FAST kernels need 16-B aligned pixel rows (a group's channel offset included)
+  const bool vec = ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   // 32-deep K-tiles (half the barriers per MFMA) where a tile stays inside one tap; 16 for Cin = 48 / 16
   static const int bk = getenv("MMT_CONV_BK") ? atoi(getenv("MMT_CONV_BK")) : 32;
   if (flags & MMT_CONV_W4)
     hipLaunchKernelGGL((conv_f32_kernel<false, 16, true>), grid, dim3(256), 0, (hipStream_t)stream, a);
-  else if (Cin % 32 == 0 && bk == 32)
+  else if (vec && Cin % 32 == 0 && bk == 32)
     hipLaunchKernelGGL((conv_f32_kernel<true, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
-  else if (Cin % 16 == 0)
+  else if (vec && Cin % 16 == 0)
     hipLaunchKernelGGL((conv_f32_kernel<true, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL((conv_f32_kernel<false, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);
   return last_err();
+}
+
+int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w, const float* bias, int Cout, int kh,
+                   int kw, int stride, int pad, const float* resid, float* y, int flags, void* stream) {
+  return mmt_conv2d_f32_ld(x, N, H, W, Cin, Cin, w, bias, Cout, kh, kw, stride, pad, resid, y, Cout, flags, stream);
 }
 
 int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y, void* stream) {

@@ -1580,8 +1580,19 @@ int mmt_xcorr(const float* z, const float* x, float* out, int B, int Cc, int hz,
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 
-int mmt_siamfc_crop(const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride, int n, const int* y0,
-                    const int* x0, const int* size, const int pad[3], int out_sz, float* out, void* stream) {
+int mmt_xcorr_nhwc(const float* z, int64_t z_batch_stride, const float* x, float* out, int B, int Cc, int hz, int wz,
+                   int hx, int wx, float scale, float bias, void* stream) {
+  if (!z || !x || !out || B <= 0 || Cc <= 0 || hz <= 0 || wz <= 0 || hx < hz || wx < wz || z_batch_stride < 0 ||
+      (int64_t)hz * wz * Cc > 16384 || ((Cc & 3) == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(z) |
+                                                           (uintptr_t)z_batch_stride * 4) & 15)))
+    return MMT_E_ARG;
+  xcorr_nhwc(z, z_batch_stride, x, out, B, Cc, hz, wz, hx, wx, scale, bias, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+static int siamfc_crop_impl(const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride, int n, const int* y0,
+                            const int* x0, const int* size, const int pad[3], int out_sz, float* out, int nhwc,
+                            void* stream) {
   if (!frame || !out || !y0 || !x0 || !size || !pad || n <= 0 || n > 8 || Hh <= 0 || Ww <= 0 || Cc < 3 ||
       row_stride < (int64_t)Ww * Cc || out_sz <= 0)
     return MMT_E_ARG;
@@ -1601,8 +1612,19 @@ int mmt_siamfc_crop(const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_st
   }
   for (int c = 0; c < 3; ++c) a.pad[c] = std::min(std::max(pad[c], 0), 255);
   a.out = out;
+  a.nhwc = nhwc;
   siamfc_crop(a, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_siamfc_crop(const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride, int n, const int* y0,
+                    const int* x0, const int* size, const int pad[3], int out_sz, float* out, void* stream) {
+  return siamfc_crop_impl(frame, Hh, Ww, Cc, row_stride, n, y0, x0, size, pad, out_sz, out, 0, stream);
+}
+
+int mmt_siamfc_crop_nhwc(const uint8_t* frame, int Hh, int Ww, int Cc, int64_t row_stride, int n, const int* y0,
+                         const int* x0, const int* size, const int pad[3], int out_sz, float* out, void* stream) {
+  return siamfc_crop_impl(frame, Hh, Ww, Cc, row_stride, n, y0, x0, size, pad, out_sz, out, 1, stream);
 }
 
 int mmt_siamfc_response(const float* resp, int n, int r, int up, float scale_penalty, double window_influence,

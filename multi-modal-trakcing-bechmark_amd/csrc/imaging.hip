@@ -273,4 +273,51 @@ void xcorr(const float* Z, const float* X, float* out, int B, int C, int hz, int
                      C, hz, wz, hx, wx, scale, bias);
 }
 
+// NHWC correlation: one wave per output pixel, lanes over channels (float4 when C % 4 == 0), the exemplar in
+// LDS, the wave's partial sums combined in a fixed butterfly order (same bits on every run)
+__global__ __launch_bounds__(256) void xcorr_nhwc_kernel(const float* __restrict__ Z, int64_t z_bstride,
+                                                         const float* __restrict__ X, float* __restrict__ out, int C,
+                                                         int hz, int wz, int hx, int wx, float scale, float bias) {
+  extern __shared__ __attribute__((aligned(16))) float zsh[];
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int ho = hx - hz + 1, wo = wx - wz + 1;
+  const int n = hz * wz * C;
+  const float* zb = Z + b * z_bstride;
+  for (int i = threadIdx.x; i < n; i += 256) zsh[i] = zb[i];
+  __syncthreads();
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= ho * wo) return;
+  const int y = p / wo, x = p - y * wo;
+  const float* xb = X + (int64_t)b * hx * wx * C;
+  float acc = 0.f;
+  if ((C & 3) == 0) {
+    const int c4 = C >> 2;
+    for (int i = 0; i < hz; ++i)
+      for (int j = 0; j < wz; ++j) {
+        const float4* xr = reinterpret_cast<const float4*>(xb + ((int64_t)(y + i) * wx + x + j) * C);
+        const float4* zr = reinterpret_cast<const float4*>(zsh + (i * wz + j) * C);
+        for (int c = lane; c < c4; c += 64) {
+          const float4 u = xr[c], v = zr[c];
+          acc += u.x * v.x + u.y * v.y + u.z * v.z + u.w * v.w;
+        }
+      }
+  } else {
+    for (int i = 0; i < hz; ++i)
+      for (int j = 0; j < wz; ++j) {
+        const float* xr = xb + ((int64_t)(y + i) * wx + x + j) * C;
+        const float* zr = zsh + (i * wz + j) * C;
+        for (int c = lane; c < C; c += 64) acc += xr[c] * zr[c];
+      }
+  }
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) out[(int64_t)b * ho * wo + p] = acc * scale + bias;
+}
+
+void xcorr_nhwc(const float* Z, int64_t z_bstride, const float* X, float* out, int B, int C, int hz, int wz, int hx,
+                int wx, float scale, float bias, hipStream_t s) {
+  const int n = (hx - hz + 1) * (wx - wz + 1);
+  hipLaunchKernelGGL(xcorr_nhwc_kernel, dim3((n + 3) / 4, B), dim3(256), (size_t)hz * wz * C * sizeof(float), s, Z,
+                     z_bstride, X, out, C, hz, wz, hx, wx, scale, bias);
+}
+
 }  // namespace mmt

@@ -248,6 +248,10 @@ void decode(const DecodeArgs& a, hipStream_t s);
 // out[b][y][x] = scale * sum_{c,i,j} X[b][c][y+i][x+j] * Z[b][c][i][j] + bias   (valid, fp32)
 void xcorr(const float* Z, const float* X, float* out, int B, int C, int hz, int wz, int hx, int wx, float scale,
            float bias, hipStream_t s);
+// the same over NHWC feature maps (the layout of the HIP AlexNet backbone): z [hz][wz][C] per batch entry at
+// z + b * z_bstride (0: one exemplar for every entry), x [B][hx][wx][C]
+void xcorr_nhwc(const float* Z, int64_t z_bstride, const float* X, float* out, int B, int C, int hz, int wz, int hx,
+                int wx, float scale, float bias, hipStream_t s);
 
 // ---- SiamFC (siamfc.hip)
 struct SiamCropArgs {
@@ -257,7 +261,8 @@ struct SiamCropArgs {
   int n, out_sz;                   // crops, output side
   int y0[8], x0[8], size[8];       // window corner (may lie outside the frame) and side, per crop
   int pad[3];                      // border colour (cv2 Scalar -> uint8)
-  float* out;                      // [n][3][out_sz][out_sz]
+  float* out;                      // [n][3][out_sz][out_sz], or [n][out_sz][out_sz][3] when nhwc
+  int nhwc;
 };
 void siamfc_crop(const SiamCropArgs& a, hipStream_t s);
 

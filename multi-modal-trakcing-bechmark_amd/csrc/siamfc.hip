@@ -3,7 +3,7 @@
 //  * siamfc_crop: crop_and_resize for the exemplar / the 3-scale instance pyramid straight from the
 //    HBM-resident H x W x C uint8 frame: square window of side round(size) at round(center - (size-1)/2),
 //    constant border = the frame's mean colour (cv2.copyMakeBorder BORDER_CONSTANT), cv2 INTER_LINEAR
-//    resize, written as float NCHW (raw 0..255, what the AlexNet backbone consumes);
+//    resize, written as float NCHW or NHWC (raw 0..255, what the AlexNet backbone consumes);
 //  * siamfc_response: the post-correlation step of TrackerSiamFC.update -- INTER_CUBIC x16 upsampling
 //    of every scale's 17x17 response, scale penalty, first-max scale selection, min/sum normalisation,
 //    cosine-window blend in double, first-occurrence argmax.
@@ -26,6 +26,12 @@ __global__ __launch_bounds__(256) void siamfc_crop_kernel(const SiamCropArgs a) 
   };
   int u8[3];
   cv_linear_u8(px, S, O, oy, ox, 3, u8);
+  if (a.nhwc) {   // [n][O][O][3]: the HIP AlexNet's input layout
+    float* o = a.out + ((int64_t)n * O * O + idx) * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = (float)u8[c];
+    return;
+  }
   float* o = a.out + (int64_t)n * 3 * O * O + idx;
 #pragma unroll
   for (int c = 0; c < 3; ++c) o[(int64_t)c * O * O] = (float)u8[c];

@@ -141,12 +141,15 @@ SIGNATURES = {
     "mmt_timing_read": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_D), ctypes.POINTER(_D), ctypes.POINTER(_D)]),
     "mmt_xcorr": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P]),
     "mmt_siamfc_crop": (_I, [_P, _I, _I, _I, ctypes.c_int64, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "mmt_siamfc_crop_nhwc": (_I, [_P, _I, _I, _I, ctypes.c_int64, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "mmt_xcorr_nhwc": (_I, [_P, ctypes.c_int64, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _P]),
     "mmt_siamfc_response": (_I, [_P, _I, _I, _I, ctypes.c_float, ctypes.c_double, _P, ctypes.c_double, _P, _P, _P]),
     "mmt_rgbd_workspace_bytes": (ctypes.c_size_t, []),
     "mmt_rgbd_assemble": (_I, [_P, ctypes.c_int64, _P, ctypes.c_int64, _I, _I, _I, _P, _P, ctypes.c_int64, _P,
                                ctypes.c_size_t, _P]),
     "mmt_set_frame_stream": (_I, [_P, _P]),
     "mmt_conv2d_f32": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "mmt_conv2d_f32_ld": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _P]),
     "mmt_conv_max_words": (ctypes.c_size_t, []),
     "mmt_conv2d_f16x3": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _I, _P]),
     "mmt_conv2d_f16x3_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),

@@ -13,7 +13,7 @@ the CPU restatement (oracle/) timed on the same inputs on the host cores (a repo
        (scores, filter gradient, J g) = 3 x I x S x C x H x W x 4 B.
 * A18  ``mmt_xcorr``           SiamFC correlation of 3 scales (AlexNet-5 [256, 6, 6] exemplar over
        [256, 22, 22] instances -> 3 x 17 x 17): 2 C hz wz ho wo FLOP per scale; plus the whole
-       SiamFC update (HIP crop, MIOpen AlexNet, HIP xcorr, HIP cubic response) in frames/s.
+       SiamFC update (HIP crop, HIP AlexNet, HIP xcorr, HIP cubic response) in frames/s.
 
 usage: python tests/bench_rows.py [--rows f1,A19,A18] [--cpu-seconds 4]
 """
@@ -132,6 +132,12 @@ def row_siamfc(cpu_seconds):
                                            ctypes.c_float(0.001), ctypes.c_float(0.0), s()), n=200)
     ref = osf.xcorr(z, x)
     err = float((out.cpu() - ref).abs().max())
+    # the NHWC correlation the tracker runs since the backbone is on the HIP conv (one exemplar for 3 scales)
+    zn, xn = z[0].permute(1, 2, 0).contiguous().cuda(), x.permute(0, 2, 3, 1).contiguous().cuda()
+    out2 = torch.empty(n, 1, ho, ho, device="cuda")
+    us_nhwc = gpu_time_us(lambda: lib.mmt_xcorr_nhwc(zn.data_ptr(), 0, xn.data_ptr(), out2.data_ptr(), n, C, hz, hz,
+                                                     hx, hx, ctypes.c_float(0.001), ctypes.c_float(0.0), s()), n=200)
+    err_nhwc = float((out2.cpu() - ref).abs().max())
     flops = 2.0 * n * C * hz * hz * ho * ho
     tfs = flops / us / 1e6
     # the whole SiamFC update step (C1 config, here on the GPU)
@@ -152,6 +158,7 @@ def row_siamfc(cpu_seconds):
     ct, cn = cpu_time_s(lambda: osf.xcorr(z, x), cpu_seconds)
     return {"row": "A18", "op": "mmt_xcorr", "shape": f"{n} x [{C},{hz},{hz}] * [{C},{hx},{hx}] -> {n}x{ho}x{ho}",
             "us_per_call": round(us, 2), "max_abs_err_vs_oracle": err,
+            "nhwc_us_per_call": round(us_nhwc, 2), "nhwc_max_abs_err_vs_oracle": err_nhwc,
             "siamfc_update_frames_per_s": round(upd, 1),
             "roofline": {"bound": "fp32 VALU (latency-bound at this size)", "achieved": round(tfs, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tfs / PEAK_FP32_TFLOPS, 5),

@@ -1,6 +1,8 @@
 """SiamFC on the HIP path vs the CPU restatement (oracle/siamfc.py) -- parity unpinned (the
 reference's SiamFC source is absent). Crops are bit-exact; response selection exact in scale and
-location; the tracker's boxes agree to IoU >= 0.999 over a 30-frame synthetic sequence."""
+location; the HIP AlexNet backbone (fp32-MFMA grouped convs, max-pools) and the NHWC correlation match
+fp64 torch within fp32 rounding; the tracker's boxes agree to IoU >= 0.999 over a 30-frame synthetic
+sequence."""
 import numpy as np
 import pytest
 import torch
@@ -39,6 +41,113 @@ def test_crop_bitexact(tracker, center, size, out):
     got = tracker._crop(torch.from_numpy(img).cuda(), [size], out, buf)[0].permute(1, 2, 0).cpu().numpy()
     ref = osf.crop_and_resize(img[..., :3], np.array(center, dtype=np.float32), size, out, avg)
     np.testing.assert_array_equal(got.astype(np.uint8), ref)
+
+
+def _torch_alexnet(sd, x_nchw):
+    """AlexNetV1 (BN eps 1e-6, eval) in fp64 torch on the device: the fp32-rounding yardstick of the HIP backbone"""
+    import torch.nn.functional as F
+    from mmtrack_amd.siamfc import AlexNetV1
+    x = x_nchw.double()
+    for name, stride, groups, bn, pool in AlexNetV1.LAYERS:
+        x = F.conv2d(x, sd[f"backbone.{name}.0.weight"].double().cuda(), sd[f"backbone.{name}.0.bias"].double().cuda(),
+                     stride=stride, groups=groups)
+        if bn:
+            p = f"backbone.{name}.1."
+            x = F.batch_norm(x, sd[p + "running_mean"].double().cuda(), sd[p + "running_var"].double().cuda(),
+                             sd[p + "weight"].double().cuda(), sd[p + "bias"].double().cuda(), False, 0.0, 1e-6)
+            x = F.relu(x)
+        if pool:
+            x = F.max_pool2d(x, 3, 2)
+    return x
+
+
+@pytest.mark.parametrize("n,side", [(1, 127), (3, 255)])
+def test_backbone_vs_torch(tracker, n, side):
+    """The HIP AlexNet (grouped convs as channel-pitched calls of mmt_conv2d_f32_ld, conv1 padded to 128 channels)
+    on crop-like inputs (0..255) against fp64 torch: max |d| <= 1e-5 of the output's max magnitude."""
+    from mmtrack_amd import synth
+    g = torch.Generator().manual_seed(side)
+    x = (torch.rand(n, side, side, 3, generator=g) * 255).round().cuda()
+    got = tracker.backbone(x, tracker._stream())
+    torch.cuda.synchronize()
+    ref = _torch_alexnet(synth.make_siamfc_state_dict(0), x.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    err = (got.double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), (err, ref.abs().max().item())
+
+
+def test_conv2d_ld_grouped_vs_torch():
+    """mmt_conv2d_f32_ld: a groups = 2 conv as two channel-pitched calls (stride 2, padding 1, a 48-channel group
+    on the 16-deep K-tiles, a 64-channel group on the 32-deep ones, residual + ReLU) vs fp64 torch"""
+    import torch.nn.functional as F
+    from mmtrack_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(3)
+    for cin_g, cout_g, k, stride, pad in [(48, 64, 5, 1, 0), (64, 128, 3, 2, 1), (5, 64, 3, 1, 1)]:
+        N, H, W = 2, 21, 19
+        x = torch.randn(N, 2 * cin_g, H, W, generator=g)
+        w = torch.randn(2 * cout_g, cin_g, k, k, generator=g) * 0.1
+        b = torch.randn(2 * cout_g, generator=g)
+        ref = F.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=pad, groups=2)
+        Ho, Wo = ref.shape[2:]
+        res = torch.randn(N, Ho, Wo, 2 * cout_g, generator=g)
+        ref = torch.relu(ref.permute(0, 2, 3, 1) + res.double())
+        xd = x.permute(0, 2, 3, 1).contiguous().cuda()
+        rd = res.cuda()
+        y = torch.full((N, Ho, Wo, 2 * cout_g), float("nan"), device="cuda")
+        for gi in range(2):
+            wg = w[gi * cout_g:(gi + 1) * cout_g].permute(0, 2, 3, 1).contiguous().cuda()
+            bg = b[gi * cout_g:(gi + 1) * cout_g].contiguous().cuda()
+            rc = lib.mmt_conv2d_f32_ld(xd.data_ptr() + 4 * gi * cin_g, N, H, W, cin_g, 2 * cin_g, wg.data_ptr(),
+                                       bg.data_ptr(), cout_g, k, k, stride, pad, rd.data_ptr() + 4 * gi * cout_g,
+                                       y.data_ptr() + 4 * gi * cout_g, 2 * cout_g, 1, None)
+            assert rc == 0
+        torch.cuda.synchronize()
+        err = (y.cpu().double() - ref).abs().max().item()
+        assert err <= 1e-5 * ref.abs().max().item(), (cin_g, cout_g, err)
+    # argument checks: Cout not a multiple of 64, a pitch below the channel count, a misaligned output
+    d = torch.zeros(4096, device="cuda")
+    assert lib.mmt_conv2d_f32_ld(d.data_ptr(), 1, 4, 4, 8, 8, d.data_ptr(), None, 96, 1, 1, 1, 0, None, d.data_ptr(),
+                                 96, 0, None) != 0
+    assert lib.mmt_conv2d_f32_ld(d.data_ptr(), 1, 4, 4, 8, 4, d.data_ptr(), None, 64, 1, 1, 1, 0, None, d.data_ptr(),
+                                 64, 0, None) != 0
+    assert lib.mmt_conv2d_f32_ld(d.data_ptr(), 1, 4, 4, 8, 8, d.data_ptr(), None, 64, 1, 1, 1, 0, None,
+                                 d.data_ptr() + 4, 64, 0, None) != 0
+
+
+def test_crop_nhwc_and_xcorr_nhwc(tracker):
+    """mmt_siamfc_crop_nhwc == mmt_siamfc_crop transposed (bit-exact); mmt_xcorr_nhwc (shared exemplar, and
+    one exemplar per entry; C % 4 == 0 and not) vs fp64 torch conv2d(groups = B)"""
+    import torch.nn.functional as F
+    from mmtrack_amd import synth
+    fr, _ = synth.make_frames(5, 1, 240, 320, 6)
+    img = torch.from_numpy(fr[0]).cuda()
+    tracker.center = np.array((118.0, 161.0), dtype=np.float32)
+    tracker.pad = [90, 100, 110]
+    sizes = [240.0, 250.0, 260.0]
+    a = tracker._crop(img, sizes, 255, torch.empty(3, 3, 255, 255, device="cuda"))
+    b = tracker._crop(img, sizes, 255, torch.empty(3, 255, 255, 3, device="cuda"))
+    assert torch.equal(a.permute(0, 2, 3, 1), b)
+    g = torch.Generator().manual_seed(9)
+    for C, shared in [(256, True), (256, False), (7, False)]:
+        B, hz, hx = 3, 6, 22
+        z = torch.randn(1 if shared else B, hz, hz, C, generator=g)
+        x = torch.randn(B, hx, hx, C, generator=g)
+        out = torch.empty(B, 17, 17, device="cuda")
+        zd, xd = z.cuda(), x.cuda()
+        rc = tracker.lib.mmt_xcorr_nhwc(zd.data_ptr(), 0 if shared else hz * hz * C, xd.data_ptr(), out.data_ptr(), B,
+                                        C, hz, hz, hx, hx, ctypes_float(0.001), ctypes_float(0.5), None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        zz = z.expand(B, hz, hz, C) if shared else z
+        ref = F.conv2d(x.double().permute(0, 3, 1, 2).reshape(1, B * C, hx, hx),
+                       zz.double().permute(0, 3, 1, 2).contiguous(), groups=B).view(B, 17, 17) * 0.001 + 0.5
+        assert (out.cpu().double() - ref).abs().max().item() < 1e-5
+
+
+def ctypes_float(v):
+    import ctypes
+    return ctypes.c_float(v)
 
 
 def test_response_select(tracker):
@@ -98,7 +207,7 @@ def test_c1_benchmark_dispatch_100_frames(tmp_path):
     tracker had after frame t-1 and tracks frame t; its box must match the GPU's (IoU >= 0.999), unless the
     GPU's choice is a tie at fp32 resolution in the oracle's own windowed response (its value within 1e-5
     relative of the oracle's maximum: the 272 x 272 bicubic upsampling makes neighbouring pixels near-equal,
-    and the MIOpen AlexNet sums in another order than the CPU).  A free run of the oracle is reported beside."""
+    and the HIP AlexNet sums in another order than the CPU).  A free run of the oracle is reported beside."""
     import os
     import subprocess
     import sys
