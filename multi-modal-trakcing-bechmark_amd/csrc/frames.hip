@@ -9,8 +9,8 @@
 //   merge        cv2.merge((rgb, colormap)) -> H x W x 6 uint8 = R G B | B' G' R'
 // Parity is unpinned at the OpenCV boundary (no cv2 in this image): the JET table is the published
 // piecewise-linear definition unless the caller passes OpenCV's own table.
-// Three launches: histogram + min/max (atomics on exact integers, deterministic), one workgroup to
-// find the median and the normalisation constants, then the per-pixel map.
+// Three launches: histogram + min/max (LDS-private per workgroup, then exact integer atomics: deterministic),
+// one workgroup to find the median and the normalisation constants, then the per-pixel map.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,57 +38,93 @@ __global__ void stats_init_kernel(FrameStats* st) {
   st->dmax = 0;
 }
 
-__global__ __launch_bounds__(256) void depth_hist_kernel(const uint16_t* dp, int64_t stride, int H, int W,
-                                                         FrameStats* st, int want_hist) {
+// One pass over the depth map: each workgroup counts its pixels into a private 65 536-bin histogram in the LDS
+// (two 16-bit counters per word: a workgroup sees at most kHistPix pixels, fewer than 65 536, so a counter never
+// carries into its neighbour), then adds its non-zero bins to the global histogram -- one global atomic per
+// (workgroup, distinct depth value) instead of one per pixel, exact integer counts in any order.
+constexpr int kHistPix = 65535;
+template <bool HIST>
+__global__ __launch_bounds__(1024) void depth_hist_kernel(const uint16_t* dp, int64_t stride, int H, int W,
+                                                          FrameStats* st) {
+  constexpr bool want_hist = HIST;
+  __shared__ unsigned int lh[HIST ? 32768 : 1];   // packed counters (128 KB)
   __shared__ unsigned int smin, smax;
-  if (threadIdx.x == 0) { smin = 0xffffffffu; smax = 0; }
+  const int t = threadIdx.x;
+  if (t == 0) { smin = 0xffffffffu; smax = 0; }
+  if constexpr (want_hist)
+    for (int i = t; i < 32768; i += 1024) lh[i] = 0;
   __syncthreads();
   unsigned int lmin = 0xffffffffu, lmax = 0;
   const int64_t n = (int64_t)H * W;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;   // <= kHistPix (checked at launch)
+  const int64_t i0 = (int64_t)blockIdx.x * per, i1 = i0 + per < n ? i0 + per : n;
+  for (int64_t i = i0 + t; i < i1; i += 1024) {
     const int y = (int)(i / W), x = (int)(i - (int64_t)y * W);
     const unsigned int v = dp[(int64_t)y * stride + x];
     lmin = min(lmin, v);
     lmax = max(lmax, v);
-    if (want_hist) atomicAdd(&st->hist[v], 1u);
+    if constexpr (want_hist) atomicAdd(&lh[v >> 1], 1u << ((v & 1) * 16));
   }
   atomicMin(&smin, lmin);
   atomicMax(&smax, lmax);
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     atomicMin(&st->dmin, smin);
     atomicMax(&st->dmax, smax);
   }
+  if constexpr (want_hist)
+    for (int i = t; i < 32768; i += 1024) {
+      const unsigned int w = lh[i];
+      if (w & 0xffffu) atomicAdd(&st->hist[2 * i], w & 0xffffu);
+      if (w >> 16) atomicAdd(&st->hist[2 * i + 1], w >> 16);
+    }
 }
 
-// median (np.median: mean of the two middle order statistics for an even count), clip and scale
-__global__ __launch_bounds__(256) void depth_stats_kernel(FrameStats* st, int64_t n, int depth_clip) {
-  __shared__ unsigned int part[256];
-  __shared__ int64_t base[257];
+// median (np.median: mean of the two middle order statistics for an even count), clip and scale.  1 024 threads,
+// 64 bins each held in registers (16-B loads): per-thread sums, an inclusive scan of them in the LDS, then the
+// thread whose range holds an order statistic walks its own 64 bins
+__global__ __launch_bounds__(1024) void depth_stats_kernel(FrameStats* st, int64_t n, int depth_clip) {
+  __shared__ unsigned int scan[2][1024];
   __shared__ int kv[2];
   const int t = threadIdx.x;
   unsigned int lo = st->dmin, hi = st->dmax;
   unsigned int clip = 65535u;
   if (depth_clip) {
-    unsigned int s = 0;
-    for (int b = t * 256; b < t * 256 + 256; ++b) s += st->hist[b];
-    part[t] = s;
+    uint4 h[16];
+    const uint4* src = reinterpret_cast<const uint4*>(st->hist) + t * 16;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) h[q] = src[q];
+    unsigned int sum = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sum += h[q].x + h[q].y + h[q].z + h[q].w;
+    // inclusive Hillis-Steele scan over the 1 024 sums (exact integers, n < 2^31)
+    int cur = 0;
+    scan[0][t] = sum;
     __syncthreads();
-    if (t == 0) {
-      int64_t acc = 0;
-      for (int i = 0; i < 256; ++i) { base[i] = acc; acc += part[i]; }
-      base[256] = acc;
+    for (int off = 1; off < 1024; off <<= 1) {
+      const unsigned int v = scan[cur][t] + (t >= off ? scan[cur][t - off] : 0u);
+      scan[cur ^ 1][t] = v;
+      cur ^= 1;
+      __syncthreads();
     }
-    __syncthreads();
+    const int64_t end = scan[cur][t], base = end - sum;
     // order statistics k1 = (n-1)/2, k2 = n/2 (0-based)
     const int64_t k[2] = {(n - 1) / 2, n / 2};
+#pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if (k[j] >= base[t] && k[j] < base[t + 1]) {
-        int64_t c = base[t];
-        for (int b = t * 256; b < t * 256 + 256; ++b) {
-          c += st->hist[b];
-          if (k[j] < c) { kv[j] = b; break; }
+      if (k[j] >= base && k[j] < end) {
+        int64_t c = base;
+        int found = t * 64 + 63;
+        for (int q = 0; q < 16; ++q) {
+          const unsigned int w[4] = {h[q].x, h[q].y, h[q].z, h[q].w};
+          bool done = false;
+          for (int e = 0; e < 4; ++e) {
+            c += w[e];
+            if (k[j] < c) { found = t * 64 + q * 4 + e; done = true; break; }
+          }
+          if (done) break;
         }
+        kv[j] = found;
       }
     }
     __syncthreads();
@@ -182,9 +218,14 @@ int mmt_rgbd_assemble(const uint8_t* rgb, int64_t rgb_stride, const uint16_t* de
   hipLaunchKernelGGL(stats_init_kernel, dim3(1), dim3(1), 0, s, st);
   if (depth_clip && hipMemsetAsync(st->hist, 0, sizeof(st->hist), s) != hipSuccess) return MMT_E_HIP;
   const int64_t n = (int64_t)H * W;
-  const int blocks = (int)((n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024);
-  hipLaunchKernelGGL(depth_hist_kernel, dim3(blocks), dim3(256), 0, s, depth, depth_stride, H, W, st, depth_clip);
-  hipLaunchKernelGGL(depth_stats_kernel, dim3(1), dim3(256), 0, s, st, n, depth_clip);
+  // 1 024-thread workgroups over 4 096 pixels each (at most kHistPix: the 16-bit LDS counters)
+  int blocks = (int)((n + 4095) / 4096);
+  if (blocks < (int)((n + kHistPix - 1) / kHistPix)) blocks = (int)((n + kHistPix - 1) / kHistPix);
+  if (depth_clip)
+    hipLaunchKernelGGL(depth_hist_kernel<true>, dim3(blocks), dim3(1024), 0, s, depth, depth_stride, H, W, st);
+  else
+    hipLaunchKernelGGL(depth_hist_kernel<false>, dim3(blocks), dim3(1024), 0, s, depth, depth_stride, H, W, st);
+  hipLaunchKernelGGL(depth_stats_kernel, dim3(1), dim3(1024), 0, s, st, n, depth_clip);
   hipLaunchKernelGGL(rgbd_map_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rgb, rgb_stride, depth,
                      depth_stride, H, W, st, lut_bgr, out, out_stride);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;

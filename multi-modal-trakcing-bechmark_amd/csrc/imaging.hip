@@ -239,38 +239,49 @@ void decode(const DecodeArgs& a, hipStream_t s) {
 
 // ------------------------------------------------------------------ cross-correlation
 // One thread per output pixel, channel loop with the exemplar staged in LDS per 16-channel slab.
-__global__ __launch_bounds__(256) void xcorr_kernel(const float* Z, const float* X, float* out, int C, int hz,
-                                                    int wz, int hx, int wx, float scale, float bias) {
-  extern __shared__ float zs[];
-  const int b = blockIdx.y;
-  const int ho = hx - hz + 1, wo = wx - wz + 1;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  const int y = idx / wo, x = idx - (idx / wo) * wo;
-  const bool live = idx < ho * wo;
+// NCHW correlation: a workgroup takes 16 output pixels of one batch entry; its 256 threads are 16 pixels x 16
+// channel slices (slice s sums channels s, s + 16, ...; 16 neighbouring pixels read neighbouring x), the exemplar
+// staged in the LDS a chunk of channels at a time, the 16 slice sums of a pixel added in slice order (same bits
+// on every run)
+constexpr int kXcLds = 16384;   // floats of exemplar per chunk
+__global__ __launch_bounds__(256) void xcorr_kernel(const float* __restrict__ Z, const float* __restrict__ X,
+                                                    float* __restrict__ out, int C, int hz, int wz, int hx, int wx,
+                                                    float scale, float bias) {
+  __shared__ float zs[kXcLds];
+  __shared__ float part[16][17];
+  const int b = blockIdx.y, t = threadIdx.x, o = t & 15, sl = t >> 4;
+  const int ho = hx - hz + 1, wo = wx - wz + 1, zsz = hz * wz;
+  const int p = blockIdx.x * 16 + o;
+  const bool live = p < ho * wo;
+  const int y = live ? p / wo : 0, x = live ? p - (p / wo) * wo : 0;
+  const int cc = (kXcLds / zsz) & ~15;   // channels per chunk (a multiple of the 16 slices; zsz <= 1024)
   float acc = 0.f;
-  const int zsz = hz * wz;
-  for (int c0 = 0; c0 < C; c0 += 16) {
-    const int cn = min(16, C - c0);
+  for (int c0 = 0; c0 < C; c0 += cc) {
+    const int cn = min(cc, C - c0);
     __syncthreads();
-    for (int i = threadIdx.x; i < cn * zsz; i += 256) zs[i] = Z[((int64_t)b * C + c0) * zsz + i];
+    for (int i = t; i < cn * zsz; i += 256) zs[i] = Z[((int64_t)b * C + c0) * zsz + i];
     __syncthreads();
-    if (live) {
-      for (int c = 0; c < cn; ++c) {
+    if (live)
+      for (int c = sl; c < cn; c += 16) {
         const float* xp = X + (((int64_t)b * C + c0 + c) * hx + y) * wx + x;
         const float* zp = zs + c * zsz;
         for (int i = 0; i < hz; ++i)
           for (int j = 0; j < wz; ++j) acc += xp[i * wx + j] * zp[i * wz + j];
       }
-    }
   }
-  if (live) out[((int64_t)b * ho + y) * wo + x] = acc * scale + bias;
+  part[sl][o] = acc;
+  __syncthreads();
+  if (t < 16 && live) {
+    float sum = part[0][t];
+    for (int k = 1; k < 16; ++k) sum += part[k][t];
+    out[(int64_t)b * ho * wo + p] = sum * scale + bias;
+  }
 }
 
 void xcorr(const float* Z, const float* X, float* out, int B, int C, int hz, int wz, int hx, int wx, float scale,
            float bias, hipStream_t s) {
   const int n = (hx - hz + 1) * (wx - wz + 1);
-  hipLaunchKernelGGL(xcorr_kernel, dim3((n + 255) / 256, B), dim3(256), 16 * hz * wz * sizeof(float), s, Z, X, out,
-                     C, hz, wz, hx, wx, scale, bias);
+  hipLaunchKernelGGL(xcorr_kernel, dim3((n + 15) / 16, B), dim3(256), 0, s, Z, X, out, C, hz, wz, hx, wx, scale, bias);
 }
 
 // NHWC correlation: one wave per output pixel, lanes over channels (float4 when C % 4 == 0), the exemplar in

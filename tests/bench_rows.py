@@ -11,7 +11,7 @@ the CPU restatement (oracle/) timed on the same inputs on the host cores (a repo
        update shapes (sample memory 50, 8 sequences, 512 x 18 x 18 features, 4 x 4 filter,
        net_opt_update_iter 2): per Gauss-Newton iteration the features are read three times
        (scores, filter gradient, J g) = 3 x I x S x C x H x W x 4 B.
-* A18  ``mmt_xcorr``           SiamFC correlation of 3 scales (AlexNet-5 [256, 6, 6] exemplar over
+* A18  ``mmt_xcorr_nhwc``      SiamFC correlation of 3 scales (AlexNet-5 [256, 6, 6] exemplar over
        [256, 22, 22] instances -> 3 x 17 x 17): 2 C hz wz ho wo FLOP per scale; plus the whole
        SiamFC update (HIP crop, HIP AlexNet, HIP xcorr, HIP cubic response) in frames/s.
 
@@ -139,7 +139,7 @@ def row_siamfc(cpu_seconds):
                                                      hx, hx, ctypes.c_float(0.001), ctypes.c_float(0.0), s()), n=200)
     err_nhwc = float((out2.cpu() - ref).abs().max())
     flops = 2.0 * n * C * hz * hz * ho * ho
-    tfs = flops / us / 1e6
+    tfs = flops / us_nhwc / 1e6   # the roofline line is the NHWC kernel the tracker runs
     # the whole SiamFC update step (C1 config, here on the GPU)
     frames, gt = synth.make_frames(7, 12, 360, 640, 3, box=(300.0, 160.0, 40.0, 30.0))
     tr = TrackerSiamFC(state_dict=synth.make_siamfc_state_dict(0))
@@ -156,9 +156,10 @@ def row_siamfc(cpu_seconds):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     ct, cn = cpu_time_s(lambda: osf.xcorr(z, x), cpu_seconds)
-    return {"row": "A18", "op": "mmt_xcorr", "shape": f"{n} x [{C},{hz},{hz}] * [{C},{hx},{hx}] -> {n}x{ho}x{ho}",
-            "us_per_call": round(us, 2), "max_abs_err_vs_oracle": err,
-            "nhwc_us_per_call": round(us_nhwc, 2), "nhwc_max_abs_err_vs_oracle": err_nhwc,
+    return {"row": "A18", "op": "mmt_xcorr_nhwc (the tracker's; NCHW mmt_xcorr beside it)",
+            "shape": f"{n} x [{C},{hz},{hz}] * [{C},{hx},{hx}] -> {n}x{ho}x{ho}",
+            "us_per_call": round(us_nhwc, 2), "max_abs_err_vs_oracle": err_nhwc,
+            "nchw_us_per_call": round(us, 2), "nchw_max_abs_err_vs_oracle": err,
             "siamfc_update_frames_per_s": round(upd, 1),
             "roofline": {"bound": "fp32 VALU (latency-bound at this size)", "achieved": round(tfs, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tfs / PEAK_FP32_TFLOPS, 5),
