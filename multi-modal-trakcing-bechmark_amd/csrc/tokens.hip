@@ -312,7 +312,8 @@ __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) 
 constexpr int TOK_THREADS = 512;   // 8 waves per block share one LDS copy of the weights
 constexpr int TOK_ROWS = TOK_THREADS / 64;
 
-template <bool RR>
+// R: slots per wave (the block's weight fill and fovea statistics shared by R x 8 slots; 2 at large batches)
+template <bool RR, int R>
 __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const PromptArgs a) {
   __shared__ float fold[FOLD_N];
   __shared__ __attribute__((aligned(16))) float W0[8 * C768];   // conv0_0 (LN_A affine folded in)
@@ -320,13 +321,22 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
   __shared__ float red[64], st[32];
   const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, b = blockIdx.y;
   const FoveaStage fsg = fovea_stage(a.a8p + (int64_t)b * L * 8, L);
-  const int s = blockIdx.x * TOK_ROWS + (threadIdx.x >> 6);   // slot of this wave
-  const bool valid = s < L;
-  const int pos = !valid ? -1 : s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];   // wave-uniform
-  const int64_t xrow = (int64_t)b * a.srcA_rows + max(pos, 0);
-  Row12 x = load_row(a.srcA + xrow * C768, lane);
-  const int64_t srow = ((int64_t)b * L + min(s, L - 1)) * 8;
-  const float ap = lane < 8 ? a.a8p[srow + lane] : 0.f, cp = lane < 8 ? a.c8p[srow + lane] : 0.f;
+  int sv[R], posv[R];
+  int64_t xrowv[R];
+  Row12 xv[R];
+  float apv[R], cpv[R];
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+    const int s = (blockIdx.x * R + rr) * TOK_ROWS + (threadIdx.x >> 6);   // slot of this wave
+    const int pos = s >= L ? -1 : s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];   // wave-uniform
+    sv[rr] = s;
+    posv[rr] = pos;
+    xrowv[rr] = (int64_t)b * a.srcA_rows + max(pos, 0);
+    xv[rr] = load_row(a.srcA + xrowv[rr] * C768, lane);
+    const int64_t srow = ((int64_t)b * L + min(s, L - 1)) * 8;
+    apv[rr] = lane < 8 ? a.a8p[srow + lane] : 0.f;
+    cpv[rr] = lane < 8 ? a.c8p[srow + lane] : 0.f;
+  }
   constexpr int WV = 8 * C768 / 4 / TOK_THREADS;
   float4 wst[WV];
 #pragma unroll
@@ -337,7 +347,13 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
   for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[threadIdx.x + TOK_THREADS * k] = wst[k];
   if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
   fovea_stats(fsg, a.Lz, a.Lx, a.smooth_p, va, red, st);   // ends with a barrier
-  if (!valid) return;
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+  const int s = sv[rr], pos = posv[rr];
+  const int64_t xrow = xrowv[rr];
+  Row12 x = xv[rr];
+  const float ap = apv[rr], cp = cpv[rr];
+  if (s >= L) break;   // wave-uniform; later slots of the wave lie further out
   if (RR && pos >= 0 && a.rr.ws) {   // the previous block's fc2 update of this slot's residual row, written back
     x = apply_reduce(x, a.rr, xrow, lane);
     store_f32(const_cast<float*>(a.srcA) + xrow * C768, x, lane);
@@ -378,6 +394,15 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
     a.a8[row * 8 + lane] = ra + ba;
     a.c8[row * 8 + lane] = rb;
   }
+  }
+}
+
+// slots per wave of the deep prompt / LN1 kernels: 2 from 8 sequences up (the weight fill and fovea statistics of a
+// block amortised over 16 rows), 1 below (a sequence's rows spread over more blocks); MMT_TOK_R (tuning) forces it
+static int tok_rows_per_wave(int B) {
+  static const int forced = getenv("MMT_TOK_R") ? atoi(getenv("MMT_TOK_R")) : 0;
+  if (forced == 1 || forced == 2) return forced;
+  return B >= 8 ? 2 : 1;
 }
 
 void prompt_reduce(const PromptArgs& a, hipStream_t s) {
@@ -388,11 +413,15 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
   } else {
     // the sequence's a8 in LDS takes L x 32 B, not the 32-KB maximum: at 320 tokens four blocks fit a CU instead
     // of two, so the 640 blocks of a 16-sequence half run in one round
-    const dim3 grid((L + TOK_ROWS - 1) / TOK_ROWS, a.B);
+    const int R = a.rr.ws ? 1 : tok_rows_per_wave(a.B);   // the slab-holding variant keeps one slot per wave
+    const dim3 grid((L + TOK_ROWS * R - 1) / (TOK_ROWS * R), a.B);
+    const size_t va_bytes = (size_t)L * 8 * sizeof(float);
     if (a.rr.ws)
-      hipLaunchKernelGGL(prompt_reduce_deep_kernel<true>, grid, dim3(TOK_THREADS), (size_t)L * 8 * sizeof(float), s, a);
+      hipLaunchKernelGGL((prompt_reduce_deep_kernel<true, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
+    else if (R == 2)
+      hipLaunchKernelGGL((prompt_reduce_deep_kernel<false, 2>), grid, dim3(TOK_THREADS), va_bytes, s, a);
     else
-      hipLaunchKernelGGL(prompt_reduce_deep_kernel<false>, grid, dim3(TOK_THREADS), (size_t)L * 8 * sizeof(float), s, a);
+      hipLaunchKernelGGL((prompt_reduce_deep_kernel<false, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
   }
 }
 
@@ -406,7 +435,7 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
 //                    (candidate_elimination_prompt + x_ori add, attn_blocks.py:9-18, vit_ce_prompt.py:310)
 // then out = LN(X[r]) (norm1 of the block).  One block = 8 compact rows of one sequence, one per wave; the
 // slot, rows and weights are all requested before the statistics and barriers.
-template <int MODE>
+template <int MODE, int R>
 // LNP_WPE (build-time tuning): waves per SIMD the register allocation targets; 6 (80 VGPRs, three blocks per CU)
 // spills 5 VGPRs in mode 2 and measured -0.35 % at 32 sequences against the default (tests/r3_run23.sh)
 #ifndef LNP_WPE
@@ -419,20 +448,29 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
   __shared__ float red[64], st[32];
   const int lane = threadIdx.x & 63, b = blockIdx.y, L = a.Lz + a.Lx;
   const FoveaStage fsg = fovea_stage(a.a8 + (int64_t)b * L * 8, L);
-  const int t = blockIdx.x * TOK_ROWS + (threadIdx.x >> 6);
-  const bool valid = t < a.rows_per_seq;
-  const int tc = min(t, a.rows_per_seq - 1);
-  const int64_t r = (int64_t)b * a.rows_per_seq + tc;
-  const int slot = (MODE == 1 || tc < a.Lz) ? tc : a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (tc - a.Lz)];
-  Row12 xv, q;
-  if (MODE == 1) {
-    xv = load_row(a.tok_rgb + r * C768, lane);
-    q = load_row(a.pos + (int64_t)tc * C768, lane);
-  } else {
-    xv = load_row(a.X + r * C768, lane);
+  int tv[R], slotv[R];
+  int64_t rv[R];
+  Row12 xvv[R], qv[R];
+  float avv[R], cvv[R];
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+    const int t = (blockIdx.x * R + rr) * TOK_ROWS + (threadIdx.x >> 6);
+    const int tc = min(t, a.rows_per_seq - 1);
+    const int64_t r = (int64_t)b * a.rows_per_seq + tc;
+    const int slot = (MODE == 1 || tc < a.Lz) ? tc : a.Lz + a.gidx[b * (a.rows_per_seq - a.Lz) + (tc - a.Lz)];
+    tv[rr] = t;
+    rv[rr] = r;
+    slotv[rr] = slot;
+    if (MODE == 1) {
+      xvv[rr] = load_row(a.tok_rgb + r * C768, lane);
+      qv[rr] = load_row(a.pos + (int64_t)tc * C768, lane);
+    } else {
+      xvv[rr] = load_row(a.X + r * C768, lane);
+    }
+    const int64_t srow = ((int64_t)b * L + slot) * 8;
+    avv[rr] = lane < 8 ? a.a8[srow + lane] : 0.f;
+    cvv[rr] = lane < 8 ? a.c8[srow + lane] : 0.f;
   }
-  const int64_t srow = ((int64_t)b * L + slot) * 8;
-  const float av = lane < 8 ? a.a8[srow + lane] : 0.f, cv = lane < 8 ? a.c8[srow + lane] : 0.f;
   constexpr int WE = 8 * C768 / 4 / TOK_THREADS;   // 3 float4 of conv1x1 (channel-major, a.w1 = W1t) per thread
   float4 wst[WE];
 #pragma unroll
@@ -451,7 +489,13 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
     if (e < 3 * C768) cst[e] = cs[k];
   }
   fovea_stats(fsg, a.Lz, a.Lx, a.smooth, va, red, st);   // ends with a barrier
-  if (!valid) return;
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+  if (tv[rr] >= a.rows_per_seq) break;   // wave-uniform; later rows of the wave lie further out
+  const int slot = slotv[rr];
+  const int64_t r = rv[rr];
+  const Row12 xv = xvv[rr], q = qv[rr];
+  const float av = avv[rr], cv = cvv[rr];
   const float s8v = lane < 8 ? fovea_s8(av, cv, st, slot < a.Lz ? 0 : 1, lane, a.smooth) : 0.f;
   float f[8];
 #pragma unroll
@@ -487,15 +531,21 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
   }
   if (a.out_lo) store_split(a.out + r * C768, a.out_lo + r * C768, y, a.out_scale, lane);
   else store_bf16(a.out + r * C768, y, lane);
+  }
 }
 
 void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s) {
-  const dim3 grid((a.rows_per_seq + TOK_ROWS - 1) / TOK_ROWS, a.rows / a.rows_per_seq);
+  const int B = a.rows / a.rows_per_seq, R = tok_rows_per_wave(B);
+  const dim3 grid((a.rows_per_seq + TOK_ROWS * R - 1) / (TOK_ROWS * R), B);
   const size_t va_bytes = (size_t)(a.Lz + a.Lx) * 8 * sizeof(float);
-  if (a.mode == 1)
-    hipLaunchKernelGGL(ln_prompt_kernel<1>, grid, dim3(TOK_THREADS), va_bytes, s, a);
+  if (a.mode == 1 && R == 2)
+    hipLaunchKernelGGL((ln_prompt_kernel<1, 2>), grid, dim3(TOK_THREADS), va_bytes, s, a);
+  else if (a.mode == 1)
+    hipLaunchKernelGGL((ln_prompt_kernel<1, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
+  else if (R == 2)
+    hipLaunchKernelGGL((ln_prompt_kernel<2, 2>), grid, dim3(TOK_THREADS), va_bytes, s, a);
   else
-    hipLaunchKernelGGL(ln_prompt_kernel<2>, grid, dim3(TOK_THREADS), va_bytes, s, a);
+    hipLaunchKernelGGL((ln_prompt_kernel<2, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
 }
 
 // ------------------------------------------------------------------ candidate elimination
