@@ -401,7 +401,7 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
 // block amortised over 16 rows), 1 below (a sequence's rows spread over more blocks); MMT_TOK_R (tuning) forces it
 static int tok_rows_per_wave(int B) {
   static const int forced = getenv("MMT_TOK_R") ? atoi(getenv("MMT_TOK_R")) : 0;
-  if (forced == 1 || forced == 2) return forced;
+  if (forced == 1 || forced == 2 || forced == 4) return forced;
   return B >= 8 ? 2 : 1;
 }
 
@@ -418,6 +418,8 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
     const size_t va_bytes = (size_t)L * 8 * sizeof(float);
     if (a.rr.ws)
       hipLaunchKernelGGL((prompt_reduce_deep_kernel<true, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
+    else if (R == 4)
+      hipLaunchKernelGGL((prompt_reduce_deep_kernel<false, 4>), grid, dim3(TOK_THREADS), va_bytes, s, a);
     else if (R == 2)
       hipLaunchKernelGGL((prompt_reduce_deep_kernel<false, 2>), grid, dim3(TOK_THREADS), va_bytes, s, a);
     else
@@ -535,10 +537,12 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
 }
 
 void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s) {
-  const int B = a.rows / a.rows_per_seq, R = tok_rows_per_wave(B);
+  const int B = a.rows / a.rows_per_seq, R = a.mode == 1 ? std::min(tok_rows_per_wave(B), 2) : tok_rows_per_wave(B);
   const dim3 grid((a.rows_per_seq + TOK_ROWS * R - 1) / (TOK_ROWS * R), B);
   const size_t va_bytes = (size_t)(a.Lz + a.Lx) * 8 * sizeof(float);
-  if (a.mode == 1 && R == 2)
+  if (a.mode == 2 && R == 4)
+    hipLaunchKernelGGL((ln_prompt_kernel<2, 4>), grid, dim3(TOK_THREADS), va_bytes, s, a);
+  else if (a.mode == 1 && R == 2)
     hipLaunchKernelGGL((ln_prompt_kernel<1, 2>), grid, dim3(TOK_THREADS), va_bytes, s, a);
   else if (a.mode == 1)
     hipLaunchKernelGGL((ln_prompt_kernel<1, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
