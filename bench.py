@@ -117,7 +117,7 @@ def cpu_baseline(workload, frames_np, gts, seconds=4.0):
 
 def pmc_traffic(cls, precision, path=None):
     """HBM bytes per launch of the probed kernel class from the committed PMC summary
-    (tests/pmc_bench.sh + tests/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes)."""
+    (tools/pmc_bench.sh + tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes)."""
     import glob
     pat = f"*pmc_traffic_{precision}*.json"
     files = [path] if path else sorted(glob.glob(os.path.join(REPO, "profiles", pat)))

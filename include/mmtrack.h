@@ -354,7 +354,8 @@ int mmt_dimp_track_optimize(const mmt_dimp_state* states, int n, const mmt_dimp_
                             int C, int H, int W, float* filters, int fh, int fw, const mmt_dimp_params* p,
                             int max_iter, void* workspace, size_t ws_bytes, void* hip_stream);
 /* mmt_dimp_optimize with the boxes and sample weights (or NULL) in device memory: no host staging and no
- * synchronisation (losses are not returned).  Strides in floats, 0 = the contiguous [I][S] layout: sample i
+ * synchronisation (losses are not returned).  Strides in floats, -1 = the contiguous [I][S] layout (0 is a
+ * real stride: one operand broadcast): sample i
  * of sequence s is feat + i * feat_img_stride + s * feat_seq_stride ([C][H][W]), its box bb_dev + i *
  * bb_img_stride + s * bb_seq_stride (4 floats), its weight sample_weight_dev[i * sw_img_stride + s * sw_seq_stride] --
  * so S sequences' memories in a pool of device states ([slot][MMT_DIMP_MEMORY] samples, mmt_dimp_state's

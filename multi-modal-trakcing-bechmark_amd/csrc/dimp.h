@@ -3,9 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-namespace mmt {
-
 #include "../../include/mmtrack.h"
+
+namespace mmt {
 
 constexpr int kDimpStage = 24;   // staged floats per thread per chunk (6144 per workgroup and LDS buffer)
 

@@ -206,8 +206,8 @@ int mmt_dimp_optimize_dev(const float* feat, int64_t feat_img_stride, int64_t fe
                           int64_t sw_seq_stride, const mmt_dimp_params* p, int num_iter, void* workspace,
                           size_t ws_bytes, void* stream_) {
   if (!feat || !weights || !bb_dev || !p || !workspace || num_iter < 0 || bad_dims(I, S, C, H, W, fh, fw) ||
-      p->num_dist_bins <= 0 || p->num_dist_bins > 128 || feat_img_stride < 0 || feat_seq_stride < 0 ||
-      bb_img_stride < 0 || bb_seq_stride < 0 || sw_img_stride < 0 || sw_seq_stride < 0)
+      p->num_dist_bins <= 0 || p->num_dist_bins > 128 || feat_img_stride < -1 || feat_seq_stride < -1 ||
+      bb_img_stride < -1 || bb_seq_stride < -1 || sw_img_stride < -1 || sw_seq_stride < -1)
     return MMT_E_ARG;
   const WsLayout L = layout(I, S, C, H, W, fh, fw, num_iter);
   if (ws_bytes < L.total) return MMT_E_ARG;
@@ -215,13 +215,13 @@ int mmt_dimp_optimize_dev(const float* feat, int64_t feat_img_stride, int64_t fe
   char* ws = static_cast<char*>(workspace);
   auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
   const int64_t chw = (int64_t)C * H * W;
-  // strides 0: the contiguous [I][S] layouts
-  if (!feat_seq_stride) feat_seq_stride = chw;
-  if (!feat_img_stride) feat_img_stride = S * feat_seq_stride;
-  if (!bb_seq_stride) bb_seq_stride = 4;
-  if (!bb_img_stride) bb_img_stride = S * bb_seq_stride;
-  if (!sw_seq_stride) sw_seq_stride = 1;
-  if (!sw_img_stride) sw_img_stride = S * sw_seq_stride;
+  // strides -1: the contiguous [I][S] layouts (0 is a real stride: one sample broadcast over the sequences)
+  if (feat_seq_stride < 0) feat_seq_stride = chw;
+  if (feat_img_stride < 0) feat_img_stride = S * feat_seq_stride;
+  if (bb_seq_stride < 0) bb_seq_stride = 4;
+  if (bb_img_stride < 0) bb_img_stride = S * bb_seq_stride;
+  if (sw_seq_stride < 0) sw_seq_stride = 1;
+  if (sw_img_stride < 0) sw_img_stride = S * sw_seq_stride;
   DimpPrep pp{bb_dev, sample_weight_dev, bb_img_stride, bb_seq_stride, sw_img_stride, sw_seq_stride, I * S, I, S,
               p->feat_stride, (float)(fh % 2) / 2.0f, (float)(fw % 2) / 2.0f, F(L.centers), F(L.sqrtsw)};
   dimp_prep(pp, st);

@@ -190,7 +190,8 @@ __device__ int update_sample_weights(float* sw, int num_samp, int num_init, int 
   if (init_w) {
     float init_sum = 0.f;
     for (int k = 0; k < num_init; ++k) init_sum += sw[k];
-    if ((double)init_sum < p.init_samples_minimum_weight) {
+    // sw[:num_init].sum() < init_samp_weight: a float32 tensor against a Python float, compared in float32
+    if (init_sum < pyf(p.init_samples_minimum_weight)) {
       float rest = 0.f;
       for (int k = num_init; k < kMem; ++k) rest += sw[k];
       const float d = pyf(p.init_samples_minimum_weight) + rest;
@@ -316,7 +317,9 @@ __global__ __launch_bounds__(256) void dimp_localize_kernel(mmt_dimp_state* stat
       } else {
         flag = F_UNCERTAIN;
       }
-    } else if (ms2 > pyf(p.hard_negative_threshold) * ms1 && (double)ms2 > p.target_not_found_threshold) {
+    } else if (ms2 > pyf(p.hard_negative_threshold) * ms1 && ms2 > pyf(p.target_not_found_threshold)) {
+      // both tensor-vs-Python-float comparisons (dimp.py:298), so in float32; the max_score1.item() tests above
+      // compare Python floats, in double
       flag = F_HARD_NEGATIVE;
     } else {
       flag = F_NORMAL;

@@ -136,11 +136,11 @@ class DiMPSteepestDescentGN:
             losses.append(torch.tensor(lbuf[0]))
         return w, iterates, losses
 
-    def optimize_dev(self, weights, feat, bb_ptr, sw_ptr, num_iter, bb_strides=(0, 0), sw_strides=(0, 0)):
+    def optimize_dev(self, weights, feat, bb_ptr, sw_ptr, num_iter, bb_strides=(-1, -1), sw_strides=(-1, -1)):
         """num_iter steps in place on ``weights`` (a contiguous [S, C, fh, fw] CUDA tensor) over ``feat``
         [I, S, C, H, W] -- any strides on the first two dims, e.g. a DimpPool's memory[a:b, :I].transpose(0, 1)
         -- with the boxes and sample weights at device addresses (the device tracker state), strides in floats
-        as (sample, sequence), 0: contiguous [I][S]; no host staging, no synchronisation (mmt_dimp_optimize_dev)."""
+        as (sample, sequence), -1: contiguous [I][S] (0 is a real stride: a broadcast operand); no host staging, no synchronisation (mmt_dimp_optimize_dev)."""
         lib = _lib.load()
         if not (isinstance(feat, torch.Tensor) and feat.is_cuda and feat.dtype == torch.float32 and feat.dim() == 5):
             raise ValueError("feat must be a 5-dim float32 CUDA tensor")

@@ -364,8 +364,14 @@ class DimpPool:
         if p.sample_memory_size != _lib.MMT_DIMP_MEMORY:
             raise ValueError(f"sample_memory_size must be {_lib.MMT_DIMP_MEMORY}")
         self.tparams = p
-        self.frames_host = (_lib.MmtDimpFrame * capacity)()
-        self.frames = torch.empty(capacity * ctypes.sizeof(_lib.MmtDimpFrame), dtype=torch.uint8, device=self.dev)
+        # frame descriptors: one pinned host copy per record parity, copied to the device without a stream sync;
+        # a parity's pinned rows (descriptors and staged host frames) are rewritten only after the copies of its
+        # previous launch have run (its event, normally long complete when the host is one frame behind)
+        fb = ctypes.sizeof(_lib.MmtDimpFrame)
+        self.desc_host = [torch.zeros(capacity * fb, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self.frames = torch.empty(capacity * fb, dtype=torch.uint8, device=self.dev)
+        self._stage = {}      # (slot, parity) -> pinned host staging of a numpy frame
+        self._copy_ev = {}    # (first slot, parity) -> event after the launch's host-to-device copies
         # two pinned record buffers: frame k + 1 may be launched (its records copied) before frame k's are read
         self.res_host = [torch.empty(capacity * self.rbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
         self._parity = {}   # per first slot: the record buffer its next launch uses
@@ -410,13 +416,21 @@ class DimpPool:
         """Sample, network, classifier and the device state update for trackers in slots [first, first + n);
         the result records go to pinned host memory behind the returned event."""
         lib, n, net = self.lib, len(trackers), self.net
-        fr = [t._frame(f) for t, f in zip(trackers, frames)]
-        for i, f in enumerate(fr):
-            d = self.frames_host[first + i]
-            d.data, d.stride, d.H, d.W, d.C = f.data_ptr(), f.stride(0), f.shape[0], f.shape[1], f.shape[2]
+        buf = self._parity.get(first, 0)
+        prev = self._copy_ev.get((first, buf))
+        if prev is not None:
+            prev.synchronize()   # this parity's pinned rows are still being read by the launch two frames back
+        fr = [self._device_frame(first + i, buf, f) for i, f in enumerate(frames)]
         fb = ctypes.sizeof(_lib.MmtDimpFrame)
-        host = torch.frombuffer(bytearray(bytes(self.frames_host)[first * fb:(first + n) * fb]), dtype=torch.uint8)
-        self.frames[first * fb:(first + n) * fb].copy_(host)
+        desc = (_lib.MmtDimpFrame * n).from_address(self.desc_host[buf].data_ptr() + first * fb)
+        for i, f in enumerate(fr):
+            d = desc[i]
+            d.data, d.stride, d.H, d.W, d.C = f.data_ptr(), f.stride(0), f.shape[0], f.shape[1], f.shape[2]
+        self.frames[first * fb:(first + n) * fb].copy_(self.desc_host[buf][first * fb:(first + n) * fb],
+                                                        non_blocking=True)
+        cev = torch.cuda.Event()
+        cev.record()
+        self._copy_ev[(first, buf)] = cev
         sz = [int(v) for v in self.tparams.img_sample_sz]
         C = fr[0].shape[2]
         patches = torch.empty(n, C, sz[0], sz[1], dtype=torch.float32, device=self.dev)
@@ -455,13 +469,25 @@ class DimpPool:
                                              ctypes.c_void_p(self._opt_ws.data_ptr()), nbytes, stream)
             if rc != 0:
                 raise RuntimeError(f"mmt_dimp_track_optimize failed ({rc})")
-        buf = self._parity.get(first, 0)
         self._parity[first] = buf ^ 1
         self.res_host[buf][first * self.rbytes:(first + n) * self.rbytes].copy_(
             self.results[first * self.rbytes:(first + n) * self.rbytes], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return ev, buf
+
+    def _device_frame(self, slot, buf, image):
+        """A frame on the device without a blocking copy: device tensors as they are, host frames through a
+        pinned staging buffer of (slot, parity) and an asynchronous copy."""
+        if isinstance(image, torch.Tensor) and image.is_cuda:
+            return image.to(self.dev).contiguous()
+        src = image if isinstance(image, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(image))
+        st = self._stage.get((slot, buf))
+        if st is None or st.shape != src.shape or st.dtype != src.dtype:
+            st = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+            self._stage[(slot, buf)] = st
+        st.copy_(src)
+        return st.to(self.dev, non_blocking=True)
 
     def finish(self, trackers, first, ticket):
         """Wait for a launch's records (its filter updates are already queued on the device) and return the

@@ -260,8 +260,25 @@ def synth_hann(sz):
     return hann2d(torch.tensor([sz, sz]).long(), centered=True)
 
 
-def tracker_fixture(name, yaml_name, sd, n_frames, seq_seed, H, W, C, init_box):
-    """Run the reference ViPTTrack (lib/test/tracker/vipt.py) on a synthetic sequence."""
+def _track_loop(tracker, frames, gts, init_box, steps):
+    """Free-running (the tracker's own previous box) or, with steps, teacher-forced: before frame t the state is
+    set to the sequence's ground-truth box of frame t - 1 (ViPTTrack keeps no other per-frame state, vipt.py:
+    64-110), so every frame is a discriminating one-step check whose crop holds the target."""
+    boxes, scores, states = [list(init_box)], [1.0], [list(init_box)]
+    tracker.initialize(frames[0], {"init_bbox": list(init_box)})
+    for t in range(1, len(frames)):
+        if steps:
+            tracker.state = [float(v) for v in gts[t - 1]]
+        states.append(list(tracker.state))
+        o = tracker.track(frames[t])
+        boxes.append([float(v) for v in o["target_bbox"]])
+        scores.append(float(o["best_score"]))
+    return boxes, scores, states
+
+
+def tracker_fixture(name, yaml_name, sd, n_frames, seq_seed, H, W, C, init_box, steps=False):
+    """Run the reference ViPTTrack (lib/test/tracker/vipt.py) on a synthetic sequence (steps: teacher-forced
+    one-step checks from the ground-truth boxes, tracker_steps_<name>.npz)."""
     import lib.test.tracker.vipt as tv
     # the reference tracker hard-codes .cuda() (vipt.py:23,30; data_utils.py:17-18,22): run it on the CPU
     torch.Tensor.cuda = lambda self, *a, **k: self
@@ -281,20 +298,16 @@ def tracker_fixture(name, yaml_name, sd, n_frames, seq_seed, H, W, C, init_box):
     params.checkpoint = ckpt
     tracker = tv.ViPTTrack(params)
     frames, gts = synth.make_frames(seq_seed, n_frames, H, W, C, box=init_box)
-    boxes = [list(init_box)]
-    scores = [1.0]
-    tracker.initialize(frames[0], {"init_bbox": list(init_box)})
-    for t in range(1, n_frames):
-        o = tracker.track(frames[t])
-        boxes.append([float(v) for v in o["target_bbox"]])
-        scores.append(float(o["best_score"]))
+    boxes, scores, states = _track_loop(tracker, frames, gts, init_box, steps)
     os.remove(ckpt)
-    np.savez_compressed(os.path.join(HERE, f"tracker_{name}.npz"), boxes=np.array(boxes), scores=np.array(scores),
-                        meta=np.array([seq_seed, n_frames, H, W, C]), init_box=np.array(init_box, dtype=np.float64))
+    extra = dict(states=np.array(states)) if steps else {}
+    np.savez_compressed(os.path.join(HERE, f"tracker_{'steps_' if steps else ''}{name}.npz"), boxes=np.array(boxes),
+                        scores=np.array(scores), meta=np.array([seq_seed, n_frames, H, W, C]),
+                        init_box=np.array(init_box, dtype=np.float64), **extra)
     print("wrote tracker", name, np.round(np.array(boxes), 1).tolist(), "gt", np.round(gts, 1).tolist())
 
 
-def ostrack_tracker_fixture(sd, n_frames, seq_seed, H, W, init_box):
+def ostrack_tracker_fixture(sd, n_frames, seq_seed, H, W, init_box, steps=False):
     """OSTrack-384 (C4) through the reference ViPTTrack state machine at its search factor 5.0.
 
     The reference's own OSTrack tracker does not run as shipped (lib/test/tracker/ostrack.py:56, 79 call
@@ -330,15 +343,12 @@ def ostrack_tracker_fixture(sd, n_frames, seq_seed, H, W, init_box):
     tracker.output_window = hann2d(torch.tensor([tracker.feat_sz, tracker.feat_sz]).long(), centered=True)
     tracker.use_visdom, tracker.debug, tracker.frame_id, tracker.save_all_boxes = False, 0, 0, False
     frames, gts = synth.make_frames(seq_seed, n_frames, H, W, 3, box=init_box)
-    boxes, scores = [list(init_box)], [1.0]
-    tracker.initialize(frames[0], {"init_bbox": list(init_box)})
-    for t in range(1, n_frames):
-        o = tracker.track(frames[t])
-        boxes.append([float(v) for v in o["target_bbox"]])
-        scores.append(float(o["best_score"]))
-    np.savez_compressed(os.path.join(HERE, "tracker_ostrack384.npz"), boxes=np.array(boxes), scores=np.array(scores),
-                        meta=np.array([seq_seed, n_frames, H, W, 3]), init_box=np.array(init_box, dtype=np.float64),
-                        search_factor=np.array([params.search_factor]))
+    boxes, scores, states = _track_loop(tracker, frames, gts, init_box, steps)
+    extra = dict(states=np.array(states)) if steps else {}
+    np.savez_compressed(os.path.join(HERE, f"tracker_{'steps_' if steps else ''}ostrack384.npz"), boxes=np.array(boxes),
+                        scores=np.array(scores), meta=np.array([seq_seed, n_frames, H, W, 3]),
+                        init_box=np.array(init_box, dtype=np.float64), search_factor=np.array([params.search_factor]),
+                        **extra)
     print("wrote tracker ostrack384", np.round(np.array(boxes), 1).tolist(), "gt", np.round(gts, 1).tolist())
 
 
@@ -392,6 +402,13 @@ def main():
     torch.set_num_threads(8)
     from lib.models.vipt import build_viptrack, build_ostrack
     install_ce_recorder()
+    if "--steps" in sys.argv:   # round 4: teacher-forced one-step tracker checks (the rest is unchanged)
+        sd = synth.make_state_dict(0, kind="vipt", prompt_type="vipt_deep")
+        tracker_fixture("deep_rgbt", "deep_rgbt", sd, 24, 31, 480, 640, 6, (300.0, 200.0, 40.0, 30.0), steps=True)
+        tracker_fixture("deep_rgbd", "deep_rgbd", sd, 24, 47, 360, 640, 6, (220.0, 140.0, 52.0, 44.0), steps=True)
+        ostrack_tracker_fixture(synth.make_state_dict(0, kind="ostrack", search_size=384, template_size=192), 16, 53,
+                                480, 640, (300.0, 220.0, 14.0, 12.0), steps=True)
+        return
     if "--only-ostrack-tracker" in sys.argv:   # round 3: the C4 tracker sequence alone (the rest is unchanged)
         ostrack_tracker_fixture(synth.make_state_dict(0, kind="ostrack", search_size=384, template_size=192), 12, 53,
                                 480, 640, (300.0, 220.0, 14.0, 12.0))

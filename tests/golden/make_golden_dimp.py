@@ -13,9 +13,19 @@ Build container only (needs /root/reference).  No bytecode is written into the r
 * ``cv2.warpAffine`` (Rotate init augmentation): oracle/dimpnet.py's restatement of OpenCV -- unpinned.
 The tracker runs with use_iou_net = False (IoU-Net refinement is not on the MI355X path) and
 torch.manual_seed(SEED) right before initialize, so the init shifts / dropout masks are reproducible.
-Usage:  python tests/golden/make_golden_dimp.py
+
+tracker_dimp_branches.npz drives the same reference tracker through every decision branch of
+localize_advanced / update_classifier (dimp.py:94-176, 239-302, 432-487, 607-650) on sequences with a full
+occlusion, a pasted distractor near and far from the target, and DeT parameters with the optional thresholds
+(uncertain_threshold, hard_sample_threshold, low_score_opt_threshold) set, plus a 52-frame sequence that
+fills the 50-sample memory and replaces samples.  Per frame it records the flag, box, confidence and the
+masked second maximum (max_score2, NaN where the branch returns before computing it); per sequence the filter
+after the first hard-negative update and at the end, and the memory bookkeeping (sample weights, boxes,
+num_stored, previous replace index).
+Usage:  python tests/golden/make_golden_dimp.py [net] [tracker] [branches]   (default: all three)
 """
 import importlib
+import json
 import os
 import sys
 import types
@@ -146,14 +156,89 @@ def tracker_fixture(wnet):
     print("wrote tracker_dimp", np.round(np.array(boxes), 2).tolist(), flags, np.round(conf, 4).tolist())
 
 
+# name -> (frame events for synth.make_frames, DeT parameter overrides, number of frames); frames, seed and box
+# otherwise those of SEQ.  The flags each one reaches are listed in the fixture (see branch_fixture's print).
+BRANCH_SEQS = {
+    "occlusion": (dict(occlude=(8, 14)), {}, 24),                           # not_found x 6, recovery
+    "distractor": (dict(distractor=(10, 30, -60, 20)), {}, 24),            # uncertain, hard_negative (2nd peak)
+    "distractor_far": (dict(distractor=(10, 30, -85, -50)), {}, 27),       # hard_negative by displacement
+    "distractor_branch": (dict(distractor=(10, 30, -60, 20)), {"distractor_threshold": 0.5}, 24),  # uncertain
+    "uncertain_threshold": ({}, {"uncertain_threshold": 0.33}, 24),
+    "hard_sample_threshold": ({}, {"hard_sample_threshold": 0.34}, 24),
+    "low_score": ({}, {"low_score_opt_threshold": 0.36, "net_opt_low_iter": 1}, 24),
+    "long": ({}, {}, 52),                                                  # memory full at ~36, replacements
+}
+
+
+def branch_fixture(wnet):
+    from pytracking.parameter.dimp import DeT_DiMP50_Max as P
+    from pytracking.tracker.dimp import dimp as dm
+    seen = []
+    max2d = dm.dcf.max2d
+
+    def rec_max2d(x):   # localize_advanced's two maxima (scores, then the masked scores)
+        r = max2d(x)
+        seen.append(float(r[0].max()))
+        return r
+    dm.dcf.max2d = rec_max2d
+    out = {"names": np.array(list(BRANCH_SEQS))}
+    try:
+        for name, (events, over, n) in BRANCH_SEQS.items():
+            params = P.parameters()
+            params.use_gpu, params.device, params.use_iou_net, params.net = False, "cpu", False, wnet
+            for k, v in over.items():
+                setattr(params, k, v)
+            tr = dm.DiMP(params)
+            tr.features_initialized = True
+            frames, _ = synth.make_frames(SEQ["seed"], n, SEQ["H"], SEQ["W"], SEQ["C"], box=SEQ["box"], **events)
+            torch.manual_seed(TRACK_SEED)
+            tr.initialize(frames[0], {"init_bbox": list(SEQ["box"])})
+            boxes, conf, ms2, flags = [list(SEQ["box"])], [1.0], [np.nan], ["init"]
+            hn_filter = None
+            for t in range(1, n):
+                seen.clear()
+                o = tr.track(frames[t])
+                boxes.append([float(v) for v in o["target_bbox"]])
+                conf.append(float(o["confidence"]))
+                flags.append(tr.debug_info["flag"])
+                ms2.append(seen[1] if len(seen) > 1 else np.nan)
+                if flags[-1] == "hard_negative" and hn_filter is None:
+                    hn_filter = (t, tr.target_filter.clone())
+            p = f"{name}/"
+            out[p + "boxes"], out[p + "confidence"], out[p + "flags"] = np.array(boxes), np.array(conf), np.array(flags)
+            out[p + "max_score2"] = np.array(ms2)
+            out[p + "events"] = np.array(json.dumps(events))
+            out[p + "params"] = np.array(json.dumps(over))
+            out[p + "final_filter"] = tr.target_filter.numpy()
+            if hn_filter is not None:
+                out[p + "hn_frame"], out[p + "hn_filter"] = np.array(hn_filter[0]), hn_filter[1].numpy()
+            out[p + "sample_weights"] = tr.sample_weights[0].numpy()
+            out[p + "target_boxes"] = tr.target_boxes.numpy()
+            out[p + "num_stored"] = np.array(int(tr.num_stored_samples[0]))
+            prev = tr.previous_replace_ind[0]
+            out[p + "prev_replace"] = np.array(-1 if prev is None else int(prev))
+            counts = {f: flags.count(f) for f in ("normal", "not_found", "uncertain", "hard_negative")}
+            print(f"{name}: {counts} num_stored {int(tr.num_stored_samples[0])} prev_replace {prev}")
+    finally:
+        dm.dcf.max2d = max2d
+    meta = np.array([SEQ["seed"], SEQ["H"], SEQ["W"], SEQ["C"], TRACK_SEED])
+    np.savez_compressed(os.path.join(HERE, "tracker_dimp_branches.npz"), meta=meta, init_box=np.array(SEQ["box"]),
+                        **out)
+
+
 def main():
+    what = set(sys.argv[1:]) or {"net", "tracker", "branches"}
     install()
     torch.set_num_threads(8)
     sd = synth.make_dimp_state_dict(0)
     net = build_net(sd)
     wnet = wrap(net)
-    net_fixture(net, wnet)
-    tracker_fixture(wnet)
+    if "net" in what:
+        net_fixture(net, wnet)
+    if "tracker" in what:
+        tracker_fixture(wnet)
+    if "branches" in what:
+        branch_fixture(wnet)
 
 
 if __name__ == "__main__":

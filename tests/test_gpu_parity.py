@@ -185,20 +185,63 @@ def test_bf16_mode_teacher_forced(engines):
         assert d < 3e-2
 
 
+def spans_frame(box, H, W, tol=0.5):
+    """A box touching two opposite frame edges (the free-running random-weight trackers grow their boxes until
+    clip_box pins them to the frame): an IoU check on it says little, so such frames are reported, not asserted."""
+    x, y, w, h = box
+    return (x <= tol and x + w >= W - tol) or (y <= tol and y + h >= H - tol)
+
+
 @pytest.mark.parametrize("seq", ["deep_rgbt", "deep_rgbd"])
 def test_tracker_sequence_matches_reference(engines, seq):
-    """Sequences of the reference ViPTTrack (golden: 10 frames 640x480, 20 frames 640x360) vs the engine."""
+    """Free-running sequences of the reference ViPTTrack (golden: 10 frames 640x480, 20 frames 640x360) vs the
+    engine: IoU >= 0.999 on every frame whose reference box does not span the frame (those are listed)."""
     g = np.load(os.path.join(GOLDEN, f"tracker_{seq}.npz"))
     seed, n, H, W, C = [int(v) for v in g["meta"]]
     frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
     eng = engines("deep_rgbt", "fp32")
     eng.initialize(0, frames[0], list(g["init_box"]))
-    ious = []
+    ious, spanning = [], []
     for t in range(1, n):
         box, score = eng.track(0, frames[t])
-        ious.append(iou(box, g["boxes"][t]))
-    print("per-frame IoU vs reference:", np.round(ious, 5))
-    assert min(ious) >= 0.999
+        if spans_frame(g["boxes"][t], H, W):
+            spanning.append((t, round(iou(box, g["boxes"][t]), 5)))
+        else:
+            ious.append(iou(box, g["boxes"][t]))
+    print("per-frame IoU vs reference:", np.round(ious, 5), "frame-spanning (not asserted):", spanning)
+    assert len(ious) >= 8 and min(ious) >= 0.999
+
+
+@pytest.mark.parametrize("seq", ["deep_rgbt", "deep_rgbd", "ostrack384"])
+def test_tracker_steps_match_reference(engines, seq):
+    """Teacher-forced one-step checks (tracker_steps_<seq>.npz, make_golden.py --steps): before frame t the
+    reference ViPTTrack's state was set to the ground-truth box of frame t - 1, so every frame's crop holds the
+    target and no frame saturates; the engine, given the same state through set_state (vipt.py:84-88, 112-118),
+    gives the reference's box (IoU >= 0.999) and best score (within 1e-3) on every frame."""
+    g = np.load(os.path.join(GOLDEN, f"tracker_steps_{seq}.npz"))
+    seed, n, H, W, C = [int(v) for v in g["meta"]]
+    frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
+    if seq == "ostrack384":
+        cfg = EngineConfig(model="ostrack", prompt_type="none", in_chans=3, template_size=192, search_size=384,
+                           search_factor=float(g["search_factor"][0]))
+        eng = Engine(cfg, synth.make_state_dict(0, **SHAPES["ostrack384"]))
+    else:
+        eng = engines("deep_rgbt", "fp32")
+    try:
+        eng.initialize(0, frames[0], list(g["init_box"]))
+        ious, dsc = [], []
+        for t in range(1, n):
+            assert not spans_frame(g["boxes"][t], H, W)
+            eng.set_state(0, g["states"][t])
+            box, score = eng.track(0, frames[t])
+            ious.append(iou(box, g["boxes"][t]))
+            dsc.append(abs(score - g["scores"][t]))
+        print(f"{seq} teacher-forced per-step IoU vs reference:", np.round(ious, 5), "max|dscore|", max(dsc))
+        assert min(ious) >= 0.999
+        assert max(dsc) < 1e-3
+    finally:
+        if seq == "ostrack384":
+            eng.close()
 
 
 def test_crop_kernel_bit_exact_vs_oracle(engines):
@@ -352,13 +395,17 @@ def test_ostrack384_tracker_sequence_matches_reference():
     eng = Engine(cfg, synth.make_state_dict(0, **SHAPES["ostrack384"]))
     try:
         eng.initialize(0, frames[0], list(g["init_box"]))
-        ious, dsc = [], []
+        ious, dsc, spanning = [], [], []
         for t in range(1, n):
             box, score = eng.track(0, frames[t])
+            if spans_frame(g["boxes"][t], H, W):
+                spanning.append((t, round(iou(box, g["boxes"][t]), 5)))
+                continue
             ious.append(iou(box, g["boxes"][t]))
             dsc.append(abs(score - g["scores"][t]))
-        print("OSTrack-384 per-frame IoU vs reference:", np.round(ious, 5), "max|dscore|", max(dsc))
-        assert min(ious) >= 0.999
+        print("OSTrack-384 per-frame IoU vs reference:", np.round(ious, 5), "max|dscore|", max(dsc),
+              "frame-spanning (not asserted):", spanning)
+        assert len(ious) >= 8 and min(ious) >= 0.999
         assert max(dsc) < 1e-3
     finally:
         eng.close()

@@ -92,6 +92,47 @@ def test_oracle_ostrack384_tracker_matches_reference():
     np.testing.assert_allclose(scores, g["scores"], rtol=1e-3, atol=1e-5)
 
 
+@pytest.mark.parametrize("name", ["deep_rgbd", "ostrack384"])
+def test_oracle_tracker_steps_match_reference(name):
+    """The oracle tracker on the teacher-forced one-step goldens (make_golden.py --steps: the reference's state
+    set to the ground-truth box of frame t - 1 before frame t), every third frame to keep the CPU suite short."""
+    g = np.load(os.path.join(GOLDEN, f"tracker_steps_{name}.npz"))
+    seed, n, H, W, C = [int(v) for v in g["meta"]]
+    frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(g["init_box"]))
+    if name == "ostrack384":
+        sd = synth.make_state_dict(0, kind="ostrack", search_size=384, template_size=192)
+        tr = otracker.OracleTracker(sd, ov.NetCfg(kind="ostrack", search_size=384, template_size=192),
+                                    search_factor=float(g["search_factor"][0]))
+    else:
+        tr = otracker.OracleTracker(synth.make_state_dict(0, kind="vipt", prompt_type="vipt_deep"), ov.NetCfg())
+    tr.initialize(frames[0], {"init_bbox": list(g["init_box"])})
+    for t in range(1, n, 3):
+        tr.state = [float(v) for v in g["states"][t]]
+        o = tr.track(frames[t])
+        np.testing.assert_allclose(o["target_bbox"], g["boxes"][t], rtol=1e-4, atol=2e-2)
+        np.testing.assert_allclose(o["best_score"], g["scores"][t], rtol=1e-3, atol=1e-5)
+
+
+def test_dimp_branch_golden_covers_every_flag():
+    """tracker_dimp_branches.npz (make_golden_dimp.py branch_fixture) reaches every localize_advanced outcome,
+    a hard-negative filter update, and a full sample memory with replacements; its frames are the plain
+    sequence's wherever no event is active (synth.make_frames draws the same numbers with events)."""
+    import json
+    g = np.load(os.path.join(GOLDEN, "tracker_dimp_branches.npz"))
+    flags = set()
+    for name in g["names"]:
+        flags |= set(str(f) for f in g[f"{name}/flags"][1:])
+    assert flags == {"normal", "not_found", "uncertain", "hard_negative"}
+    assert any(f"{n}/hn_filter" in g.files for n in g["names"])
+    assert int(g["long/num_stored"]) > 50 and int(g["long/prev_replace"]) >= 17
+    seed, H, W, C, _ = [int(v) for v in g["meta"]]
+    plain, _ = synth.make_frames(seed, 12, H, W, C, box=tuple(g["init_box"]))
+    ev, _ = synth.make_frames(seed, 12, H, W, C, box=tuple(g["init_box"]),
+                              **json.loads(str(g["occlusion/events"])))
+    np.testing.assert_array_equal(ev[:8], plain[:8])
+    assert not np.array_equal(ev[8], plain[8])
+
+
 def test_cv2_resize_restatement_properties():
     """Unpinned piece: self-consistency of the INTER_LINEAR restatement."""
     rng = np.random.Generator(np.random.PCG64(3))
