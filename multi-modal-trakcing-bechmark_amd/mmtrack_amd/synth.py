@@ -232,8 +232,8 @@ def make_frames(seed: int, n: int, H: int = 480, W: int = 640, C: int = 6,
     Optional events (the same random draws as without them, so a sequence with events shares its background,
     texture and noise with the plain one):
     * ``occlude=(t0, t1)``: the target is not drawn in frames t0 <= t < t1 (full occlusion);
-    * ``distractor=(t0, t1, dx, dy)``: a second blob of the target's colour and size at the target's centre
-      + (dx, dy) in frames t0 <= t < t1.
+    * ``distractor=(t0, t1, dx, dy[, alpha])``: a second blob of the target's colour and size at the target's
+      centre + (dx, dy) in frames t0 <= t < t1, blended over the background with weight alpha (default 1).
 
     Returns (frames uint8 [n,H,W,C], gt boxes float64 [n,4] in x,y,w,h)."""
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -264,7 +264,8 @@ def make_frames(seed: int, n: int, H: int = 480, W: int = 640, C: int = 6,
             m = np.zeros_like(m)
         if distractor is not None and distractor[0] <= t < distractor[1]:
             dx_, dy_ = cx + distractor[2], cy + distractor[3]
-            m = np.maximum(m, np.exp(-(((xx - dx_) / (0.5 * w)) ** 4 + ((yy - dy_) / (0.5 * h)) ** 4))[..., None])
+            alpha = distractor[4] if len(distractor) > 4 else 1.0
+            m = np.maximum(m, alpha * np.exp(-(((xx - dx_) / (0.5 * w)) ** 4 + ((yy - dy_) / (0.5 * h)) ** 4))[..., None])
         noise = rng.integers(-6, 7, size=(H, W, C)).astype(np.float32)
         img = bg * (1 - m) + target_col * m + tex + noise
         frames[t] = np.clip(img, 0, 255).astype(np.uint8)

@@ -26,6 +26,7 @@ Usage:  python tests/golden/make_golden_dimp.py [net] [tracker] [branches]   (de
 """
 import importlib
 import json
+import math
 import os
 import sys
 import types
@@ -157,20 +158,63 @@ def tracker_fixture(wnet):
 
 
 # name -> (frame events for synth.make_frames, DeT parameter overrides, number of frames); frames, seed and box
-# otherwise those of SEQ.  The flags each one reaches are listed in the fixture (see branch_fixture's print).
+# otherwise those of SEQ.  Distractors are blended at alpha < 1: an identical copy of the target ties with it on
+# the score map, and an argmax decided by fp32 summation order pins nothing.
 BRANCH_SEQS = {
-    "occlusion": (dict(occlude=(8, 14)), {}, 24),                           # not_found x 6, recovery
-    "distractor": (dict(distractor=(10, 30, -60, 20)), {}, 24),            # uncertain, hard_negative (2nd peak)
-    "distractor_far": (dict(distractor=(10, 30, -85, -50)), {}, 27),       # hard_negative by displacement
+    "occlusion": (dict(occlude=(8, 14)), {}, 24),                              # not_found x 6, recovery
+    "distractor": (dict(distractor=(10, 30, -60, 20)), {}, 24),               # uncertain, hard_negative (2nd peak)
+    "distractor_far": (dict(distractor=(10, 30, -85, -50)), {}, 27),          # hard_negative by displacement
     "distractor_branch": (dict(distractor=(10, 30, -60, 20)), {"distractor_threshold": 0.5}, 24),  # uncertain
+    "distractor_97": (dict(distractor=(10, 30, -60, 20, 0.97)), {}, 24),       # hard_negative (2nd peak)
+    "distractor_above": (dict(distractor=(10, 30, 0, -55)), {}, 24),          # hard_negative, uncertain
     "uncertain_threshold": ({}, {"uncertain_threshold": 0.33}, 24),
     "hard_sample_threshold": ({}, {"hard_sample_threshold": 0.34}, 24),
     "low_score": ({}, {"low_score_opt_threshold": 0.36, "net_opt_low_iter": 1}, 24),
-    "long": ({}, {}, 52),                                                  # memory full at ~36, replacements
+    "long": ({}, {}, 52),                                                     # memory full at ~36, replacements
 }
 
 
-def branch_fixture(wnet):
+def _margin(ms1, ms2, disp, params):
+    """Smallest relative distance of one of localize_advanced's threshold tests (dimp.py:260-301) from flipping
+    on this frame, counting only the tests that decide the outcome: ms1 against the not-found / uncertain /
+    hard-sample thresholds, then the distractor ratio, then (no distractor) the hard-negative pair, or (distractor)
+    the two displacement tests against their threshold."""
+    g = params.get
+    m = [abs(ms1 - g("target_not_found_threshold")) / g("target_not_found_threshold")]
+    for k in ("uncertain_threshold", "hard_sample_threshold"):
+        if g(k, None) is not None:
+            m.append(abs(ms1 - g(k)) / g(k))
+    if ms2 is None or ms1 < max(g("target_not_found_threshold"), g("uncertain_threshold", -1), g("hard_sample_threshold", -1)):
+        return min(m)
+    r = ms2 / ms1
+    m.append(abs(r - g("distractor_threshold")) / g("distractor_threshold"))
+    if r > g("distractor_threshold"):
+        n1, n2, thr = disp
+        m.extend([abs(n1 - thr) / thr, abs(n2 - thr) / thr])
+    else:
+        a = (r - g("hard_negative_threshold")) / g("hard_negative_threshold")
+        b = (ms2 - g("target_not_found_threshold")) / g("target_not_found_threshold")
+        m.append(min(abs(a), abs(b)) if (a > 0 and b > 0) else (max(abs(a), abs(b)) if (a <= 0 and b <= 0)
+                                                                else abs(a if a <= 0 else b)))
+    return min(m)
+
+
+def _runner_up(s):
+    """The score map's best value outside the 3 x 3 cells around its maximum, relative to the maximum: how near
+    the argmax is to jumping to another peak."""
+    s = s.reshape(s.shape[-2], s.shape[-1]).clone()
+    r, c = divmod(int(s.argmax()), s.shape[1])
+    m1 = float(s[r, c])
+    s[max(r - 1, 0):r + 2, max(c - 1, 0):c + 2] = -1
+    return float(s.max()) / m1
+
+
+def branch_fixture(wnet, seqs=None, path=None):
+    """Per sequence: the end-to-end record (flags, boxes, confidences, filters, memory) and, per frame, the
+    decision record -- the tracker state before track() (position, size, scale, frame number, sample memory
+    bookkeeping), the sample coordinates and the raw score map it localised on, and the state after it, with
+    the Gauss-Newton iteration count update_classifier chose -- so the device state machine can be run on the
+    reference's own score maps, independent of the network's arithmetic."""
     from pytracking.parameter.dimp import DeT_DiMP50_Max as P
     from pytracking.tracker.dimp import dimp as dm
     seen = []
@@ -181,32 +225,103 @@ def branch_fixture(wnet):
         seen.append(float(r[0].max()))
         return r
     dm.dcf.max2d = rec_max2d
-    out = {"names": np.array(list(BRANCH_SEQS))}
+    seqs = BRANCH_SEQS if seqs is None else seqs
+    out = {"names": np.array(list(seqs))}
     try:
-        for name, (events, over, n) in BRANCH_SEQS.items():
+        for name, (events, over, n) in seqs.items():
             params = P.parameters()
             params.use_gpu, params.device, params.use_iou_net, params.net = False, "cpu", False, wnet
             for k, v in over.items():
                 setattr(params, k, v)
             tr = dm.DiMP(params)
             tr.features_initialized = True
+            cap = {}
+            ebf, ct = tr.extract_backbone_features, tr.classify_target
+
+            def extract(*a, **k):
+                r = ebf(*a, **k)
+                cap["coords"] = r[1][0].float().clone()
+                return r
+
+            def classify(x):
+                r = ct(x)
+                cap["scores"] = r[0, 0].clone()
+                return r
+            tr.extract_backbone_features, tr.classify_target = extract, classify
+            opt = wnet.net.classifier.filter_optimizer
+            opt_fwd = opt.forward
+
+            def opt_forward(*a, **k):
+                cap["num_iter"] = k.get("num_iter")
+                return opt_fwd(*a, **k)
             frames, _ = synth.make_frames(SEQ["seed"], n, SEQ["H"], SEQ["W"], SEQ["C"], box=SEQ["box"], **events)
             torch.manual_seed(TRACK_SEED)
             tr.initialize(frames[0], {"init_bbox": list(SEQ["box"])})
-            boxes, conf, ms2, flags = [list(SEQ["box"])], [1.0], [np.nan], ["init"]
+            opt.forward = opt_forward
+            boxes, conf, ms2, flags, margin, runner = [list(SEQ["box"])], [1.0], [np.nan], ["init"], [np.nan], [np.nan]
+            dec = {k: [] for k in ("pre_pos", "pre_sz", "pre_scale", "pre_frame", "pre_nstored", "pre_prev", "pre_sw",
+                                   "pre_tb", "coords", "scores", "post_pos", "post_sz", "post_scale", "post_sw",
+                                   "post_tb", "post_nstored", "post_prev", "num_iter")}
+
+            def snap(pre):
+                p = "pre_" if pre else "post_"
+                dec[p + "pos"].append(tr.pos.numpy().copy())
+                dec[p + "sz"].append(tr.target_sz.numpy().copy())
+                dec[p + "scale"].append(float(tr.target_scale))
+                dec[p + "sw"].append(tr.sample_weights[0].numpy().copy())
+                dec[p + "tb"].append(tr.target_boxes.numpy().copy())
+                dec[p + "nstored"].append(int(tr.num_stored_samples[0]))
+                prev = tr.previous_replace_ind[0]
+                dec[p + "prev"].append(-1 if prev is None else int(prev))
             hn_filter = None
             for t in range(1, n):
                 seen.clear()
+                cap.clear()
+                snap(True)
+                dec["pre_frame"].append(tr.frame_num)
+                pos_before = tr.pos.clone()
                 o = tr.track(frames[t])
+                snap(False)
+                dec["coords"].append(cap["coords"].numpy())
+                dec["scores"].append(cap["scores"].numpy())
+                dec["num_iter"].append(int(cap.get("num_iter") or 0))
                 boxes.append([float(v) for v in o["target_bbox"]])
                 conf.append(float(o["confidence"]))
                 flags.append(tr.debug_info["flag"])
                 ms2.append(seen[1] if len(seen) > 1 else np.nan)
+                # the displacement test's operands (dimp.py:280-292), for the margin
+                sc = cap["coords"]
+                spos = 0.5 * (sc[:2] + sc[2:] - 1)
+                sscale = ((sc[2:] - sc[:2]) / tr.img_sample_sz).prod().sqrt()
+                sz = torch.Tensor(list(cap["scores"].shape))
+                osz = sz - (tr.kernel_size + 1) % 2
+                ctr = (sz - 1) / 2
+                s = cap["scores"]
+                d1 = torch.Tensor(divmod(int(s.argmax()), s.shape[1])) - ctr
+                prev_vec = (pos_before - spos) / ((tr.img_support_sz / osz) * sscale)
+                n1 = float(torch.sqrt(((d1 - prev_vec) ** 2).sum()))
+                thr = params.dispalcement_scale * math.sqrt(sz[0] * sz[1]) / 2
+                n2 = np.nan
+                if len(seen) > 1:
+                    # the masked second peak's position: recompute as localize_advanced does
+                    tns = params.target_neighborhood_scale * (tr.target_sz / sscale) * (osz / tr.img_support_sz)
+                    md = d1 + ctr
+                    t0 = max(round(md[0].item() - tns[0].item() / 2), 0)
+                    t1 = min(round(md[0].item() + tns[0].item() / 2 + 1), int(sz[0]))
+                    l0 = max(round(md[1].item() - tns[1].item() / 2), 0)
+                    l1 = min(round(md[1].item() + tns[1].item() / 2 + 1), int(sz[1]))
+                    sm = s.clone()
+                    sm[t0:t1, l0:l1] = 0
+                    d2 = torch.Tensor(divmod(int(sm.argmax()), sm.shape[1])) - ctr
+                    n2 = float(torch.sqrt(((d2 - prev_vec) ** 2).sum()))
+                margin.append(_margin(seen[0], seen[1] if len(seen) > 1 else None, (n1, n2, thr), params))
+                runner.append(_runner_up(s))
                 if flags[-1] == "hard_negative" and hn_filter is None:
                     hn_filter = (t, tr.target_filter.clone())
+            opt.forward = opt_fwd
             p = f"{name}/"
             out[p + "boxes"], out[p + "confidence"], out[p + "flags"] = np.array(boxes), np.array(conf), np.array(flags)
-            out[p + "max_score2"] = np.array(ms2)
+            out[p + "max_score2"], out[p + "margin"], out[p + "runner_up"] = np.array(ms2), np.array(margin), np.array(runner)
             out[p + "events"] = np.array(json.dumps(events))
             out[p + "params"] = np.array(json.dumps(over))
             out[p + "final_filter"] = tr.target_filter.numpy()
@@ -217,13 +332,18 @@ def branch_fixture(wnet):
             out[p + "num_stored"] = np.array(int(tr.num_stored_samples[0]))
             prev = tr.previous_replace_ind[0]
             out[p + "prev_replace"] = np.array(-1 if prev is None else int(prev))
+            for k, v in dec.items():
+                out[p + "dec_" + k] = np.array(v)
+            out[p + "const"] = np.array([*tr.base_target_sz.tolist(), *tr.image_sz.tolist(), float(tr.min_scale_factor),
+                                         float(tr.max_scale_factor), int(tr.num_init_samples[0])], dtype=np.float64)
             counts = {f: flags.count(f) for f in ("normal", "not_found", "uncertain", "hard_negative")}
-            print(f"{name}: {counts} num_stored {int(tr.num_stored_samples[0])} prev_replace {prev}")
+            print(f"{name}: {counts} num_stored {int(tr.num_stored_samples[0])} prev_replace {prev} "
+                  f"min decision margin {np.nanmin(margin):.4f} max runner-up {np.nanmax(runner):.3f}")
     finally:
         dm.dcf.max2d = max2d
     meta = np.array([SEQ["seed"], SEQ["H"], SEQ["W"], SEQ["C"], TRACK_SEED])
-    np.savez_compressed(os.path.join(HERE, "tracker_dimp_branches.npz"), meta=meta, init_box=np.array(SEQ["box"]),
-                        **out)
+    np.savez_compressed(path or os.path.join(HERE, "tracker_dimp_branches.npz"), meta=meta,
+                        init_box=np.array(SEQ["box"]), **out)
 
 
 def main():
