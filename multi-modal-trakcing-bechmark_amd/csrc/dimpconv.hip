@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "../../include/mmtrack.h"
@@ -232,11 +233,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     l = lx | (uint32_t)ly << 16;
   };
   auto stash = [&](const ConvRegs& r, int st) {
+#if defined(CONV_EXP_NOSTASH)   // tuning experiment only: no A split / LDS write (wrong results)
+    if (r.a0.x == 12345.f) *reinterpret_cast<float*>(&sA[st][0][0]) = r.a0.y + r.a1.z;
+    return;
+#endif
     uint4 hv, lv;
+#if defined(CONV_EXP_HIONLY)    // tuning experiment only: hi halves, lo = 0 (wrong results)
+    hv.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(r.a0.x * sa, r.a0.y * sa));
+    hv.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(r.a0.z * sa, r.a0.w * sa));
+    hv.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(r.a1.x * sa, r.a1.y * sa));
+    hv.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(r.a1.z * sa, r.a1.w * sa));
+    lv = make_uint4(0, 0, 0, 0);
+#else
     pack2(r.a0.x, r.a0.y, hv.x, lv.x);
     pack2(r.a0.z, r.a0.w, hv.y, lv.y);
     pack2(r.a1.x, r.a1.y, hv.z, lv.z);
     pack2(r.a1.z, r.a1.w, hv.w, lv.w);
+#endif
     *reinterpret_cast<uint4*>(&sA[st][0][cswz(ar, ac)]) = hv;
     *reinterpret_cast<uint4*>(&sA[st][1][cswz(ar, ac)]) = lv;
   };
@@ -267,8 +280,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         acc[i][j] = mfma16<true>(bh, ah[i], acc[i][j]);
+#if !defined(CONV_EXP_ONEMFMA)  // tuning experiment only: one MFMA per product (wrong results)
         acc[i][j] = mfma16<true>(bl, ah[i], acc[i][j]);
         acc[i][j] = mfma16<true>(bh, al[i], acc[i][j]);
+#endif
       }
     }
   };
@@ -481,6 +496,222 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.z * 13, reinterpret_cast<float*>(&sP[0][0]));
 }
 
+// 3 x 3 / stride 1 / pad 1 convolutions with the input PATCH staged once per 32-channel chunk.  The generic kernel
+// above gathers, splits and stashes a K-tile of activations for every (tap, chunk) K-tile, so each input element is
+// loaded, split into fp16 hi / lo and written to the LDS nine times.  Here a workgroup's tile is 128 consecutive output
+// pixels of one image (raster order) and, per chunk of 32 input channels, the rows of the input those pixels' nine taps
+// read -- (rows + 2) x (W + 2) pixels, zeros outside the image -- are loaded and split ONCE into an LDS patch; the nine
+// taps then read their A fragments from it at pixel offsets (dy, dx), and only the weights (one 32-deep K-tile per tap,
+// LDS-DMA into a two-stage ring) move per tap.  Patch layout: pixel P = 64 B per half (32 channels), 16-B chunk q of
+// P at q ^ (((P >> 2) & 1) << 1): the fragment reads (16 consecutive pixels x 4 chunks per ds_read_b128 lane group)
+// are bank-conflict-free for any start pixel (exhaustive check over start offsets; a tile row that wraps to the next
+// image row costs at most one 2-way conflict).  K order: chunk-major, tap-minor (the weights' K-tile tap * Cin / 32 +
+// chunk); split-K slices take ranges of chunks.  Same products as conv_f16x3_kernel, summed in a different fp32 order.
+constexpr int kPatchMaxPx = 384, kPatchNPL = 6;   // patch pixels (48 KB of fp16 halves), float4 loads per thread
+template <int BN>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv3x3_patch_f16x3_kernel(
+    const ConvF16Args a, int tiles_per_img, int patch_px) {
+  constexpr int BM = 128, BK = 32;
+  constexpr int WN = BN / 2, FM = 2, FN = WN / 16, NW = BN / 64;
+  extern __shared__ __attribute__((aligned(16))) uint16_t dynlds[];
+  // fixed offsets (immediate fields of the LDS instructions), sized for the largest patch
+  uint16_t* const sPh = dynlds;                          // [kPatchMaxPx][32] hi
+  uint16_t* const sPl = dynlds + kPatchMaxPx * 32;       // lo
+  uint16_t* const sWb = dynlds + 2 * kPatchMaxPx * 32;   // [2 stages][hi, lo][BN * BK]
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int grp = blockIdx.z / a.ks, slice = blockIdx.z - grp * a.ks;
+  const ConvGroupArgs g = pick_group(a, grp);
+  const int HW = a.Ho * a.Wo, Wd = a.W, PW = a.W + 2;
+  const int img = blockIdx.x / tiles_per_img, tile = blockIdx.x - img * tiles_per_img;
+  const int o0 = tile * BM, o_end = min(o0 + BM, HW);
+  const int y_first = o0 / Wd;
+  const int npx = ((o_end - 1) / Wd - y_first + 3) * PW;   // patch pixels of this tile
+  const int n0 = blockIdx.y * BN;
+
+  float sa = g.xscale;
+  if (g.xmax) {
+    const float mx = wave_max(g.xmax[lane * kShardStride]);
+    sa = mx > 0.f ? pow2_scale(mx) : 1.0f;
+  }
+  const float inv = g.inv_w / sa;
+
+  const int nc = a.Cin / BK;                              // 32-channel chunks
+  const int c0 = (int)((int64_t)slice * nc / a.ks), c1 = (int)((int64_t)(slice + 1) * nc / a.ks);
+
+  // the patch: float4 f = t + 512 j is channels 4 (f & 7) .. + 3 of patch pixel f >> 3
+  const rsrc_t rX = make_rsrc(g.x, (int64_t)a.N * a.H * a.W * a.Cin * 4);
+  float4 pv[kPatchNPL];
+  auto load_patch = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < kPatchNPL; ++j) {
+      const int f = t + 512 * j, px = f >> 3, part = f & 7;
+      const int pr = px / PW, pc = px - pr * PW;
+      const int iy = y_first - 1 + pr, ix = pc - 1;
+      const bool ok = px < npx && iy >= 0 && iy < a.H && ix >= 0 && ix < Wd;
+      const uint32_t vo = ok ? (uint32_t)((((img * a.H + iy) * Wd + ix) * a.Cin + c * BK + 4 * part) * 4) : kBufOob;
+      pv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rX, vo, 0, 0));
+    }
+  };
+  auto stash_patch = [&]() {
+    // the thread id made opaque here, so the stash addresses are formed at each stash rather than hoisted out of
+    // the chunk loop (they would take 12 VGPRs across it, and spill)
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+#pragma unroll
+    for (int j = 0; j < kPatchNPL; ++j) {
+      const int f = tt + 512 * j, px = f >> 3, part = f & 7;
+      if (px < npx) {
+        uint16_t h[4], l[4];
+        split_h(pv[j].x * sa, h[0], l[0]);
+        split_h(pv[j].y * sa, h[1], l[1]);
+        split_h(pv[j].z * sa, h[2], l[2]);
+        split_h(pv[j].w * sa, h[3], l[3]);
+        const int off = px * 32 + (((part >> 1) ^ (((px >> 2) & 1) << 1)) << 3) + ((part & 1) << 2);
+        *reinterpret_cast<uint2*>(sPh + off) = make_uint2(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16);
+        *reinterpret_cast<uint2*>(sPl + off) = make_uint2(l[0] | (uint32_t)l[1] << 16, l[2] | (uint32_t)l[3] << 16);
+      }
+    }
+  };
+  // weights: conv_f16x3_kernel's LDS-DMA pieces, K-tile (tap, chunk) = tap * nc + chunk
+  const u32x4 qWh = make_rsrc_words(g.wh, (int64_t)a.Cout * a.Kp * 2);
+  const u32x4 qWl = make_rsrc_words(g.wl, (int64_t)a.Cout * a.Kp * 2);
+  auto load_w = [&](int kt, bool kv, int st) {
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int p = wave * NW + j, im = p / (BN / 16), rb = p % (BN / 16);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(lptr_t)(sWb + (st * 2 + im) * BN * BK + rb * 16 * BK));
+      const int row = rb * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 2);
+      const uint32_t vo = kv ? (uint32_t)(((n0 + row) * a.Kp + c * 8) * 2) : kBufOob;
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(kt * BK * 2));
+      if (im)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWl), "s"(so), "{m0}"(dst) : "memory");
+      else
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWh), "s"(so), "{m0}"(dst) : "memory");
+    }
+  };
+
+  // this lane's fragment rows: patch pixel of tap (0, 0) for output pixel o0 + 32 wm + 16 i + (lane & 15) (rows past
+  // the tile's end read the tile's last pixel; their outputs are dropped)
+  int pbase[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int o = min(o0 + wm * 32 + i * 16 + (lane & 15), o_end - 1);
+    const int y = o / Wd, x = o - y * Wd;
+    pbase[i] = (y - y_first) * PW + x;
+  }
+  const int q = lane >> 4;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int tap, int st) {
+    const int dy = tap / 3, dx = tap - dy * 3;
+    bf16x8 ah[FM], al[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int P = pbase[i] + dy * PW + dx;
+      const int off = P * 32 + ((q ^ (((P >> 2) & 1) << 1)) << 3);
+      ah[i] = *reinterpret_cast<const bf16x8*>(sPh + off);
+      al[i] = *reinterpret_cast<const bf16x8*>(sPl + off);
+    }
+    const uint16_t* wh = sWb + (st * 2) * BN * BK;
+    const uint16_t* wl = sWb + (st * 2 + 1) * BN * BK;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * WN + j * 16 + (lane & 15);
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(wh + cswz(row, q));
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(wl + cswz(row, q));
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        acc[i][j] = mfma16<true>(bh, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bl, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bh, al[i], acc[i][j]);
+      }
+    }
+  };
+
+  // prologue: the first chunk's patch and tap-0 weights
+  load_patch(c0);
+  load_w(c0, true, 0);
+  stash_patch();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int st = 0;
+  for (int c = c0; c < c1; ++c) {
+    const bool more = c + 1 < c1;
+    // tap 0 (its weights and patch were waited for at the chunk boundary): the next tap's weights, then the next
+    // chunk's patch behind them
+    load_w(nc + c, true, st ^ 1);
+    if (more) load_patch(c + 1);
+    compute(0, st);
+    st ^= 1;
+    for (int tap = 1; tap < 9; ++tap) {
+      // tap's weights landed (issued one tap ago; at tap 1 the next chunk's patch loads, issued after them, may stay
+      // in flight) and every wave is past the previous tap, whose stage takes the next weights
+      if (tap == 1 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPatchNPL) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // the next tap's weights, or the next chunk's tap 0 (zeros past the slice: nobody reads them)
+      load_w(tap < 8 ? (tap + 1) * nc + c : c + 1, tap < 8 || more, st ^ 1);
+      compute(tap, st);
+      st ^= 1;
+    }
+    if (more) {
+      // every wave is past its last read of this chunk's patch before it is overwritten
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      stash_patch();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int li = lane & 15, lk = lane >> 4;
+  if (a.ks > 1) {
+    const int G = gridDim.z / a.ks;
+    const int M = a.N * HW;
+    float* pb = a.part + ((int64_t)slice * G + grp) * M * a.Cout;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int o = o0 + wm * 32 + i * 16 + li;
+      if (o >= o_end) continue;
+      const int64_t mo = (int64_t)img * HW + o;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int no = n0 + wn * WN + j * 16 + 4 * lk;
+        const f32x4 v = acc[i][j] * inv;
+        *reinterpret_cast<float4*>(pb + mo * a.Cout + no) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    return;
+  }
+  float ymx = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int o = o0 + wm * 32 + i * 16 + li;
+    if (o >= o_end) continue;
+    const int64_t mo = (int64_t)img * HW + o;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int no = n0 + wn * WN + j * 16 + 4 * lk;
+      const f32x4 v = conv_out(g, acc[i][j] * inv, mo, no, a.Cout);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
+    }
+  }
+  __syncthreads();   // the LDS is free for the max fold
+  if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.y * 7 + blockIdx.z * 13, reinterpret_cast<float*>(dynlds));
+}
+
 // split-K: y = sum over the ks slices (in slice order) + bias (+ residual), ReLU, merge; grid (blocks, G), 4 channels
 // per thread
 __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvF16Args a) {
@@ -562,9 +793,31 @@ int conv_bn(int64_t gm, int Cin, int Cout, int G) {
   return 128;
 }
 
-int64_t conv_ks_for(int N, int Ho, int Wo, int Cin, int Cout, int Kp, int G) {
+// the 3 x 3 / stride-1 patch kernel's geometry: tiles per image (128 raster pixels each) and the largest tile's
+// patch (pixels); 0 when the shape is not one it runs
+int patch_plan(int H, int W, int Cin, int kh, int kw, int stride, int pad, int* tiles_per_img) {
+  static const bool off = getenv("MMT_CONV_NOPATCH") != nullptr;   // tuning A/B: the generic kernel
+  if (off || kh != 3 || kw != 3 || stride != 1 || pad != 1 || Cin % 32 || Cin < 32) return 0;
+  const int HW = H * W, tiles = (HW + 127) / 128;
+  int px = 0;
+  for (int tl = 0; tl < tiles; ++tl) {
+    const int o0 = tl * 128, o1 = std::min(o0 + 128, HW);
+    px = std::max(px, ((o1 - 1) / W - o0 / W + 3) * (W + 2));
+  }
+  if (px > kPatchMaxPx) return 0;
+  *tiles_per_img = tiles;
+  return px;
+}
+
+// M tiles of a launch (the patch kernel tiles each image separately) and its K split
+int64_t conv_ks_for(int N, int H, int W, int Ho, int Wo, int Cin, int Cout, int kh, int kw, int stride, int pad, int Kp,
+                    int G) {
   const int64_t gm = ((int64_t)N * Ho * Wo + 127) / 128;
-  return conv_pick_ks(gm * (Cout / conv_bn(gm, Cin, Cout, G)) * G, Kp / 32);
+  const int bn = conv_bn(gm, Cin, Cout, G);
+  int tpi = 0;
+  if (patch_plan(H, W, Cin, kh, kw, stride, pad, &tpi))
+    return std::min<int64_t>(conv_pick_ks((int64_t)N * tpi * (Cout / bn) * G, Kp / 32), Cin / 32);
+  return conv_pick_ks(gm * (Cout / bn) * G, Kp / 32);
 }
 
 }  // namespace
@@ -579,7 +832,7 @@ size_t mmt_conv2d_f16x3_ws_bytes(int N, int H, int W, int Cin, int Cout, int kh,
   if (groups < 1 || groups > kMaxGroups || conv_shape(N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, K) != MMT_OK)
     return 0;
   const int Kp = (K + 31) / 32 * 32;
-  const int64_t ks = conv_ks_for(N, Ho, Wo, Cin, Cout, Kp, groups);
+  const int64_t ks = conv_ks_for(N, H, W, Ho, Wo, Cin, Cout, kh, kw, stride, pad, Kp, groups);
   return ks > 1 ? (size_t)(ks * groups * N * Ho * Wo * (int64_t)Cout * 4) : 0;
 }
 
@@ -603,7 +856,7 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad;
   a.Ho = Ho; a.Wo = Wo; a.Kp = Kp;
   const int64_t M = (int64_t)N * Ho * Wo;
-  int ks = (int)conv_ks_for(N, Ho, Wo, Cin, Cout, Kp, G);
+  int ks = (int)conv_ks_for(N, H, W, Ho, Wo, Cin, Cout, kh, kw, stride, pad, Kp, G);
   if (ks > 1 && (!ws || ws_bytes < (size_t)(ks * G * M * (int64_t)Cout * 4))) ks = 1;
   a.ks = ks;
   a.part = static_cast<float*>(ws);
@@ -614,7 +867,16 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   // the stem on a 4-channel image: 2-D tiles from an LDS input patch (MMT_CONV_STEM_OLD: the gather kernel, tuning)
   static const bool stem_old = getenv("MMT_CONV_STEM_OLD") != nullptr;
   static const int stem_th = getenv("MMT_CONV_STEM_TH") ? atoi(getenv("MMT_CONV_STEM_TH")) : 16;   // tuning: 8
-  if (!stem_old && Cin == 4 && Cout == 64 && ks == 1 && kh <= 7 && kw <= 7 && stride <= 2 && Kp / 32 <= kStemMaxKt) {
+  int tpi = 0;
+  const int ppx = patch_plan(H, W, Cin, kh, kw, stride, pad, &tpi);
+  if (ppx) {
+    const dim3 pgrid((unsigned)(N * tpi), Cout / bn, G * ks);
+    const size_t lds = (size_t)(2 * kPatchMaxPx * 32 + 2 * 2 * bn * 32) * 2;   // 80 KB (BN 128): two per CU
+    if (bn == 128)
+      hipLaunchKernelGGL(conv3x3_patch_f16x3_kernel<128>, pgrid, dim3(512), lds, s, a, tpi, ppx);
+    else
+      hipLaunchKernelGGL(conv3x3_patch_f16x3_kernel<64>, pgrid, dim3(512), lds, s, a, tpi, ppx);
+  } else if (!stem_old && Cin == 4 && Cout == 64 && ks == 1 && kh <= 7 && kw <= 7 && stride <= 2 && Kp / 32 <= kStemMaxKt) {
     const int th = stem_th == 8 ? 8 : 16;
     const unsigned tiles = (unsigned)(((Ho + th - 1) / th) * ((Wo + kStemTW - 1) / kStemTW) * N);
     if (th == 8)

@@ -815,7 +815,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
     g.pos_rows = L;
     run_gemm(e, s, "patch", scaled(g, kPixScale * e->pe_s, 1.0f), EPI_POS_F32);
   }
-  init_indices(q_gidx0, q_slot2pos, n, Lz, Lx, s);
+  // (the token index arrays gidx0 / slot2pos were reset by the launch's geometry kernel, enqueue_split)
 
   PromptArgs pa{};
   pa.B = n;
@@ -1087,7 +1087,7 @@ void enqueue_split(mmt_engine* e, int b0, int n) {
   // crop geometry of all n sequences from their device-resident state (and, ring hand-off, their frame
   // parameters from the host ring), once per launch before any part starts
   crop_geometry(e->params_dev, e->state_dev + b0, n, e->cfg.search_factor, e->cfg.search_size,
-                e->ring_handoff ? &e->hring : nullptr, e->stream);
+                e->ring_handoff ? &e->hring : nullptr, e->gidx0, e->slot2pos, e->Lz, e->Lx, e->stream);
   if (e->overlap_min <= 0 || n < e->overlap_min || e->probe) {
     enqueue_forward(e, b0, 0, n, e->stream, 0);
     return;

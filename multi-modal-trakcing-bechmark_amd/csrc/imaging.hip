@@ -91,9 +91,18 @@ __device__ void geometry_one(CropParam* params, SeqState* state, int i, double f
   st.err = err;
 }
 
-// one workgroup: every thread reads the launch counter before thread 0 advances it
+// one workgroup: every thread reads the launch counter before thread 0 advances it.  It also resets the
+// launch's token index arrays (gidx[b][j] = j, slot2pos[b][j] = Lz + j: every search token kept, before the
+// first candidate elimination), which would otherwise take a launch of their own
 __global__ __launch_bounds__(256) void geometry_kernel(CropParam* params, SeqState* state, int n, double factor,
-                                                       int out_sz, RingArgs ring, int use_ring) {
+                                                       int out_sz, RingArgs ring, int use_ring, int* gidx,
+                                                       int* slot2pos, int Lz, int Lx) {
+  if (gidx)
+    for (int i = threadIdx.x; i < n * Lx; i += blockDim.x) {
+      const int j = i % Lx;
+      gidx[i] = j;
+      slot2pos[i] = Lz + j;
+    }
   int e = 0;
   if (use_ring) e = *ring.ctr;   // kept in [0, kring): launches mod kring, as the host's tickets count them
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -118,9 +127,9 @@ __global__ __launch_bounds__(256) void geometry_kernel(CropParam* params, SeqSta
 }
 
 void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, const RingArgs* ring,
-                   hipStream_t s) {
+                   int* gidx, int* slot2pos, int Lz, int Lx, hipStream_t s) {
   hipLaunchKernelGGL(geometry_kernel, dim3(1), dim3(256), 0, s, params, state, n, factor, out_sz,
-                     ring ? *ring : RingArgs{}, ring ? 1 : 0);
+                     ring ? *ring : RingArgs{}, ring ? 1 : 0, gidx, slot2pos, Lz, Lx);
 }
 
 // vipt.py:84-88 (pred_box * S / resize_factor in float32 tensors, then python floats) + map_box_back

@@ -164,7 +164,6 @@ struct CEArgs {
   int keys_pitch;         // floats between sequences of forced / keys_out
 };
 void ce_select(const CEArgs& a, hipStream_t s);
-void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s);
 
 // final norm + token recovery (zeros at pruned slots) -> head input NHWC bf16 [B][Lx][768]
 // feat_lo non-null: feat / feat_lo are the f16x3 halves of the normed rows * feat_scale
@@ -222,8 +221,9 @@ struct RingArgs {
   int* cur;                  // ring entry of the launch in flight (device)
   int kring, pitch;
 };
+// (gidx / slot2pos non-null: also the launch's token index arrays, [n][Lx] each, as before any elimination)
 void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, const RingArgs* ring,
-                   hipStream_t s);
+                   int* gidx, int* slot2pos, int Lz, int Lx, hipStream_t s);
 
 struct DecodeArgs {
   int B, fs;                       // feature map fs x fs

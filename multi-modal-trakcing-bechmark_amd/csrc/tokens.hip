@@ -617,18 +617,6 @@ void ce_select(const CEArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(ce_select_kernel, dim3(a.B), dim3(CE_THREADS), 0, s, a);
 }
 
-__global__ void init_indices_kernel(int* gidx, int* slot2pos, int B, int Lz, int Lx) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * Lx) return;
-  const int j = i % Lx;
-  gidx[i] = j;
-  slot2pos[i] = Lz + j;
-}
-
-void init_indices(int* gidx, int* slot2pos, int B, int Lz, int Lx, hipStream_t s) {
-  hipLaunchKernelGGL(init_indices_kernel, dim3((B * Lx + 255) / 256), dim3(256), 0, s, gidx, slot2pos, B, Lz, Lx);
-}
-
 // ------------------------------------------------------------------ final norm + recover_tokens
 // vit_ce_prompt.py:318-339: LN over the surviving tokens, then scatter the search tokens back
 // to their 16x16 slots; pruned slots are exact zeros.
