@@ -115,6 +115,18 @@ def cpu_baseline(workload, frames_np, gts, seconds=4.0):
                       f"'variants' adds network-only and 1-thread samples of ~{seconds:.0f} s each"}
 
 
+def dimp_traffic(batch, path=None):
+    """HBM bytes per feature-net batch of the mfDiMP line from the committed PMC summary
+    (tools/pmc_dimp_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE over the feature net's kernels, 32 images per batch)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic_dimp*.json"))) if path is None else [path]
+    if not files or batch != 32:
+        return None
+    d = json.load(open(files[-1]))
+    return {"bytes": d["bytes_per_batch"], "algorithmic_bytes": d.get("algorithmic_bytes_per_batch"),
+            "ratio": d.get("ratio_to_algorithmic"), "source": os.path.relpath(files[-1], REPO)}
+
+
 def pmc_traffic(cls, precision, path=None):
     """HBM bytes per launch of the probed kernel class from the committed PMC summary
     (tools/pmc_bench.sh + tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes)."""
@@ -423,7 +435,7 @@ def dimp_main(args, rank, world, dist):
     roof = {"bound": "mfma", "kernel": ("conv_f16x3_kernel" if f16 else "conv_f32_kernel") +
             " (2 x ResNet-50 to layer3 + clf conv, per batch)",
             "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": None,
+            "frac": round(achieved / peak, 4), "traffic": dimp_traffic(B),
             "flop_per_launch_group": flops, "avg_batch_ms": round(feat_ms, 4),
             # the feature net is partly HBM-bound (fp32 activations, 1x1 convs of K = 64..256): its per-layer
             # roofline (sum over layers of max(FLOPs / peak, min bytes / 8 TB/s)) and the fraction of it reached

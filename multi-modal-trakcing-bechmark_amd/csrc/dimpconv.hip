@@ -496,6 +496,205 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.z * 13, reinterpret_cast<float*>(&sP[0][0]));
 }
 
+// The generic conv with a deeper operand pipeline.  conv_f16x3_kernel keeps one K-tile of weights and two of
+// activations in flight per workgroup (about 48 KB), which, at the several-microsecond latency of a loaded memory
+// system, caps a workgroup near 20 GB/s and the K loop at about 1.5 us per 32-deep K-tile -- measured: removing two
+// of the three MFMAs and the whole activation split / stash together saves only a third of the kernel's time.  Here
+// the activation loads are inline-asm buffer loads (the compiler neither counts nor waits for them; every wait is
+// written out, naming the registers it guards), so the weights can go two K-tiles ahead into the three-stage ring and
+// the activations NR K-tiles ahead into NR register sets without the compiler draining one queue to reach the other.
+// Step j issues W(j + 2) then A(j + NR), multiplies K-tile j, waits for A(j + 1) -- 2 (NW + NA) younger operations
+// (for NR = 3) -- and stashes it, then waits for W(j + 1) and passes the barrier.  Same products, same summation
+// order as conv_f16x3_kernel (bit-identical).
+template <int BN, int NR>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_f16x3_deep_kernel(const ConvF16Args a) {
+  constexpr int BM = 128, BK = 32, NWS = 3;
+  constexpr int WN = BN / 2, FM = 2, FN = WN / 16;
+  constexpr int NW = BN / 64;                  // W LDS-DMA pieces per wave per K-tile
+  constexpr int NA = 2;                        // A loads per thread per K-tile
+  constexpr int WAIT_A = (NR - 1) * (NW + NA); // younger operations when A(j + 1) is waited for
+  constexpr int WAIT_W = 2 * NA + NW;          // ... when W(j + 1) is (A(j + NR - 1), W(j + 2), A(j + NR))
+  static_assert(NR == 2 || NR == 3, "register sets");
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][2][BM * BK];
+  __shared__ __attribute__((aligned(16))) uint16_t sW[NWS][2][BN * BK];
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int grp = blockIdx.z / a.ks, slice = blockIdx.z - grp * a.ks;
+  const ConvGroupArgs g = pick_group(a, grp);
+  const int M = a.N * a.Ho * a.Wo;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+
+  float sa = g.xscale;
+  if (g.xmax) {
+    const float mx = wave_max(g.xmax[lane * kShardStride]);
+    sa = mx > 0.f ? pow2_scale(mx) : 1.0f;
+  }
+  const float inv = g.inv_w / sa;
+
+  const int ar = t >> 2, ac = t & 3;
+  const int m = m0 + ar;
+  const bool mval = m < M;
+  int iy0 = 0, ix0 = 0;
+  uint32_t xrow = 0;
+  if (mval) {
+    const int nimg = m / (a.Ho * a.Wo);
+    const int r = m - nimg * a.Ho * a.Wo;
+    const int oy = r / a.Wo, ox = r - oy * a.Wo;
+    iy0 = oy * a.stride - a.pad;
+    ix0 = ox * a.stride - a.pad;
+    xrow = (uint32_t)(nimg * a.H * a.W * a.Cin);
+  }
+  const u32x4 qX = make_rsrc_words(g.x, (int64_t)a.N * a.H * a.W * a.Cin * 4);
+  const int nk = a.Kp / BK;
+  const int kt0 = (int)((int64_t)slice * nk / a.ks), nt = (int)((int64_t)(slice + 1) * nk / a.ks) - kt0;
+  const int cpt = a.Cin / BK;
+
+  struct DeepRegs {   // native vectors: an inline-asm register operand, not a struct in memory
+    f32x4 a0, a1;
+  };
+  DeepRegs r[NR];
+  // K-tile i of the slice (zeros past it: an out-of-range offset, no traffic) into register set `set`
+  auto load_a = [&](int i, DeepRegs& set) {
+    const int kt = kt0 + i;
+    const int tap = kt / cpt, c0 = (kt - tap * cpt) * BK + ac * 8;
+    const int ky = tap / a.kw, kx = tap - ky * a.kw;
+    const int iy = iy0 + ky, ix = ix0 + kx;
+    const bool ok = i < nt && mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    const uint32_t vo = ok ? (xrow + (uint32_t)((iy * a.W + ix) * a.Cin + c0)) * 4 : kBufOob;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(set.a0) : "v"(vo), "s"(qX) : "memory");
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:16" : "=v"(set.a1) : "v"(vo), "s"(qX) : "memory");
+  };
+  const u32x4 qWh = make_rsrc_words(g.wh, (int64_t)a.Cout * a.Kp * 2);
+  const u32x4 qWl = make_rsrc_words(g.wl, (int64_t)a.Cout * a.Kp * 2);
+  auto load_w = [&](int i, int st) {
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int p = wave * NW + j, img = p / (BN / 16), rb = p % (BN / 16);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(lptr_t)(&sW[st][img][rb * 16 * BK]));
+      const int row = rb * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 2);
+      const uint32_t vo = i < nt ? (uint32_t)(((n0 + row) * a.Kp + c * 8) * 2) : kBufOob;
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)((kt0 + i) * BK * 2));
+      if (img)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWl), "s"(so), "{m0}"(dst) : "memory");
+      else
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWh), "s"(so), "{m0}"(dst) : "memory");
+    }
+  };
+  // the register set's loads done: all but the CNT youngest vector-memory operations (the set named as read-write,
+  // so nothing reads it above this point)
+  auto wait_set = [&](DeepRegs& set, auto cnt) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(set.a0), "+v"(set.a1) : "n"(decltype(cnt)::value) : "memory");
+  };
+  auto pack2 = [&](float x, float y, uint32_t& h, uint32_t& l) {
+    uint16_t hx, lx, hy, ly;
+    split_h(x * sa, hx, lx);
+    split_h(y * sa, hy, ly);
+    h = hx | (uint32_t)hy << 16;
+    l = lx | (uint32_t)ly << 16;
+  };
+  auto stash = [&](const DeepRegs& rr, int st) {
+    uint4 hv, lv;
+    pack2(rr.a0[0], rr.a0[1], hv.x, lv.x);
+    pack2(rr.a0[2], rr.a0[3], hv.y, lv.y);
+    pack2(rr.a1[0], rr.a1[1], hv.z, lv.z);
+    pack2(rr.a1[2], rr.a1[3], hv.w, lv.w);
+    *reinterpret_cast<uint4*>(&sA[st][0][cswz(ar, ac)]) = hv;
+    *reinterpret_cast<uint4*>(&sA[st][1][cswz(ar, ac)]) = lv;
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int sta, int stw) {
+    const int c = lane >> 4;
+    bf16x8 ah[FM], al[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * 32 + i * 16 + (lane & 15);
+      ah[i] = *reinterpret_cast<const bf16x8*>(&sA[sta][0][cswz(row, c)]);
+      al[i] = *reinterpret_cast<const bf16x8*>(&sA[sta][1][cswz(row, c)]);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * WN + j * 16 + (lane & 15);
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(&sW[stw][0][cswz(row, c)]);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(&sW[stw][1][cswz(row, c)]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        acc[i][j] = mfma16<true>(bh, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bl, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bh, al[i], acc[i][j]);
+      }
+    }
+  };
+  using CA = std::integral_constant<int, WAIT_A>;
+
+  // prologue: the loads of steps -NR .. -1 (W(j + 2) where j + 2 >= 0, A(j + NR)), so the steady-state counts hold
+  // from step 0 on
+#pragma unroll
+  for (int j = -NR; j < 0; ++j) {
+    if (j + 2 >= 0) load_w(j + 2, j + 2);
+    load_a(j + NR, r[j + NR]);
+  }
+  wait_set(r[0], CA{});
+  stash(r[0], 0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_W) : "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int i0 = 0; i0 < nt; i0 += 6) {
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int j = i0 + u;
+      if (j >= nt) break;
+      load_w(j + 2, (u + 2) % 3);
+      load_a(j + NR, r[u % NR]);
+      compute(u & 1, u % 3);
+      wait_set(r[(u + 1) % NR], CA{});
+      stash(r[(u + 1) % NR], (u + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_W) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the zero-loads past the slice, before the LDS is left
+#pragma unroll
+  for (int k = 0; k < NR; ++k) asm volatile("" : "+v"(r[k].a0), "+v"(r[k].a1));
+
+  const int li = lane & 15, lk = lane >> 4;
+  if (a.ks > 1) {
+    const int G = gridDim.z / a.ks;
+    float* pb = a.part + ((int64_t)slice * G + grp) * M * a.Cout;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int mo = m0 + wm * 32 + i * 16 + li;
+      if (mo >= M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int no = n0 + wn * WN + j * 16 + 4 * lk;
+        const f32x4 v = acc[i][j] * inv;
+        *reinterpret_cast<float4*>(pb + (int64_t)mo * a.Cout + no) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    return;
+  }
+  float ymx = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int mo = m0 + wm * 32 + i * 16 + li;
+    if (mo >= M) continue;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int no = n0 + wn * WN + j * 16 + 4 * lk;
+      const f32x4 v = conv_out(g, acc[i][j] * inv, mo, no, a.Cout);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
+    }
+  }
+  if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.y * 7 + blockIdx.z * 13, reinterpret_cast<float*>(&sA[0][0][0]));
+}
+
 // 3 x 3 / stride 1 / pad 1 convolutions with the input PATCH staged once per 32-channel chunk.  The generic kernel
 // above gathers, splits and stashes a K-tile of activations for every (tap, chunk) K-tile, so each input element is
 // loaded, split into fp16 hi / lo and written to the LDS nine times.  Here a workgroup's tile is 128 consecutive output
@@ -867,6 +1066,8 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   // the stem on a 4-channel image: 2-D tiles from an LDS input patch (MMT_CONV_STEM_OLD: the gather kernel, tuning)
   static const bool stem_old = getenv("MMT_CONV_STEM_OLD") != nullptr;
   static const int stem_th = getenv("MMT_CONV_STEM_TH") ? atoi(getenv("MMT_CONV_STEM_TH")) : 16;   // tuning: 8
+  static const bool conv_old = getenv("MMT_CONV_OLD") != nullptr;   // tuning: conv_f16x3_kernel (two-deep)
+  static const int conv_nr = getenv("MMT_CONV_NR") ? atoi(getenv("MMT_CONV_NR")) : 2;   // tuning: 3
   int tpi = 0;
   const int ppx = patch_plan(H, W, Cin, kh, kw, stride, pad, &tpi);
   if (ppx) {
@@ -885,10 +1086,22 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
       hipLaunchKernelGGL(conv_stem_f16x3_kernel<16>, dim3(tiles, 1, G), dim3(512), 0, s, a);
   } else if (Cin <= 4)
     hipLaunchKernelGGL((conv_f16x3_kernel<64, true>), grid, dim3(512), 0, s, a);
-  else if (bn == 128)
-    hipLaunchKernelGGL((conv_f16x3_kernel<128, false>), grid, dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_f16x3_kernel<64, false>), grid, dim3(512), 0, s, a);
+  else if (conv_old) {   // tuning A/B: the two-deep pipeline
+    if (bn == 128)
+      hipLaunchKernelGGL((conv_f16x3_kernel<128, false>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_f16x3_kernel<64, false>), grid, dim3(512), 0, s, a);
+  } else if (conv_nr == 2) {
+    if (bn == 128)
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 2>), grid, dim3(512), 0, s, a);
+  } else {
+    if (bn == 128)
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3>), grid, dim3(512), 0, s, a);
+  }
   if (ks > 1) {
     const int64_t q = M * Cout / 4;
     hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((q + 255) / 256), G), dim3(256), 0, s, a);

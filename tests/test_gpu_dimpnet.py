@@ -76,6 +76,33 @@ def test_conv2d_f16x3_vs_fp64(N, C, H, W, Co, k, s, p):
     assert torch.equal(got3, got)
 
 
+def test_conv_kernels_bitwise(tmp_path):
+    """The f16x3 conv kernels against each other (tests/conv_dump.py, one child process per setting: the knobs are
+    read once per process): the deep-pipelined generic kernel (conv_f16x3_deep_kernel, three register sets / two
+    register sets) gives the bits of the two-deep conv_f16x3_kernel (same products, same summation order), with and
+    without split-K; the 3 x 3 patch kernel (another summation order) agrees with them within 1e-5 of the output
+    scale."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = {}
+    for mode, extra in (("old", {"MMT_CONV_OLD": "1", "MMT_CONV_NOPATCH": "1"}),
+                        ("deep3", {"MMT_CONV_NR": "3", "MMT_CONV_NOPATCH": "1"}), ("deep2", {"MMT_CONV_NOPATCH": "1"}),
+                        ("patch", {})):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("MMT_CONV_")}
+        env.update(extra)
+        path = str(tmp_path / f"{mode}.npz")
+        r = subprocess.run([sys.executable, os.path.join(here, "conv_dump.py"), path], env=env, capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        res[mode] = np.load(path)
+    for mode in ("deep3", "deep2"):
+        for key in res["old"].files:
+            np.testing.assert_array_equal(res[mode][key], res["old"][key], err_msg=f"{mode} {key}")
+    for key in res["old"].files:
+        close(res["patch"][key], res["old"][key], 1e-5)
+
+
 @pytest.mark.parametrize("N,C,H,W,Co,k,s,p", [(1, 1024, 18, 18, 256, 3, 1, 1), (2, 1024, 18, 18, 512, 3, 1, 1),
                                              (3, 512, 18, 18, 256, 1, 1, 0), (1, 256, 35, 33, 128, 3, 2, 1)])
 def test_conv2d_f16x3_groups_and_splitk(N, C, H, W, Co, k, s, p):

@@ -29,3 +29,14 @@ done
 unset MMT_CONV_NOPATCH
 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/vit32.json 2> $O/vit32.err || exit 1
 python -c "import json; d=json.load(open('$O/vit32.json')); print('vit32', d['value'], d['roofline']['frac'])"
+# FETCH_SIZE calibration on known byte counts (512 MB per kernel launch, 2 launches each)
+mkdir -p $O/calib
+timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/calib/fetch -- ./tools/micro/fetch_calib > $O/calib/fetch.log 2>&1 || { echo "calib failed"; exit 0; }
+python - <<PY
+import csv, glob
+for f in glob.glob('$O/calib/fetch/**/*counter_collection.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        print(r['Kernel_Name'][:30], r['Counter_Name'], float(r['Counter_Value']) * 1024 / (512 << 20), 'x of the bytes read')
+PY
+timeout -s KILL 60 rocprofv3 --list-avail > $O/calib/avail.txt 2>&1 || true
+grep -i "TCC_EA0_RDREQ\|TCC_BUBBLE\|TCC_EA0_RD" $O/calib/avail.txt | head -20
