@@ -113,6 +113,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
     m[rb] = -INFINITY;
     l[rb] = 0.f;
   }
+  const float qks = SPLIT ? a.qk_inv : 1.0f;   // the logits' scale (f16x3: applied in the exponent, see below)
   const bool ce_wave = a.ce_query >= q0 && a.ce_query < q0 + QW;
   const int ce_rb = ce_wave ? (a.ce_query - q0) >> 4 : -1;
   const bool ce_lane = ce_wave && (lane & 15) == ((a.ce_query - q0) & 15);
@@ -216,7 +217,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
           sc[0][t] = mfma16<SPLIT>(kf, qf[0][NH - 1][s], sc[0][t]);
         }
       }
-      if (SPLIT) sc[0][t] *= a.qk_inv;   // S = (K s)(Q s)^T / s^2 / 8
+      // (f16x3: S = (K s)(Q s)^T / s^2 / 8 -- qk_inv, a power of two, is folded into the exponent's scale below:
+      // the same bits as scaling the scores, 16 multiplies fewer per tile)
     }
     bf16x8 pf[RB][2], pl[RB][2];
     const bool tail = kb + KB > N;   // only the last key tile has keys past N (wave-uniform)
@@ -224,11 +226,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
     for (int rb = 0; rb < RB; ++rb) {
       float bmax = -INFINITY;
       if (tail) {
+        const int lim = N - kb - 4 * g;   // this lane's keys 16 t + 4 g + r are valid below N
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (kb + 16 * t + 4 * g + r >= N) sc[rb][t][r] = -INFINITY;
+            if (16 * t + r >= lim) sc[rb][t][r] = -INFINITY;
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -237,24 +240,26 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
       bmax = xmax16(bmax);   // xor 16, xor 32 by permlane half-exchanges (no LDS round trip)
       bmax = xmax32(bmax);
       if (ce_lane && rb == ce_rb) {
+        // the tile's 64 logits (keys past N land in ce_row's slack, CE_MAX >= N + 64, and are never read)
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kb + 16 * t + 4 * g + r;
-            if (key < N) ce_row[key] = sc[rb][t][r];
-          }
+          for (int r = 0; r < 4; ++r) ce_row[kb + 16 * t + 4 * g + r] = sc[rb][t][r];
       }
+      // f16x3: m, the logits and ce_row stay in the unscaled units of the accumulator; the scale qk_inv = 2^k
+      // enters through lg = qk_inv log2(e) (exact: a power of two times log2(e)), so fma(s, lg, -m lg) is bit for bit
+      // fma(s qk_inv, log2(e), -(m qk_inv) log2(e)) and the maxima commute with the positive scale
+      const float lg = qks * 1.44269504f;
       const float mnew = fmaxf(m[rb], bmax);
-      const float alpha = __expf(m[rb] - mnew);
+      const float alpha = __expf((m[rb] - mnew) * qks);
       // p = e^(s - m) = 2^(s log2e - m log2e): one FMA + v_exp_f32 per score
-      const float ml2 = mnew * 1.44269504f;
+      const float ml2 = mnew * lg;
       float psum = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(sc[rb][t][r], 1.44269504f, -ml2));
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[rb][t][r], lg, -ml2));
           sc[rb][t][r] = p;
           psum += p;
         }
@@ -336,14 +341,14 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
       mw[w] = st[w * 18 * 64 + lane];
       mm = fmaxf(mm, mw[w]);
     }
-    const float f0 = __expf(mw[0] - mm);
+    const float f0 = __expf((mw[0] - mm) * qks);
     float ll = l[0] * f0;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[0][dt] *= f0;
 #pragma unroll
     for (int w = 1; w < WAVES; ++w) {
       const float* ow = st + w * 18 * 64 + lane;
-      const float f = __expf(mw[w] - mm);
+      const float f = __expf((mw[w] - mm) * qks);
       ll += ow[64] * f;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
@@ -390,7 +395,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
     const float mm = __shfl(cm, src, 64), ll = __shfl(cl, src, 64);
     const int Ls = N - a.ce_lens_t;
     float* dst = a.ce_prob + ((int64_t)b * a.heads + h) * Ls;
-    for (int j = lane; j < Ls; j += 64) dst[j] = __expf(ce_row[a.ce_lens_t + j] - mm) / ll;
+    for (int j = lane; j < Ls; j += 64) dst[j] = __expf((ce_row[a.ce_lens_t + j] - mm) * qks) / ll;
   }
 }
 

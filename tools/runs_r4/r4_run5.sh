@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-4 run 5: attention softmax trimmed (qk scale folded into the exponent, CE export without per-key bounds,
+# tail mask inside its branch): attention / parity / benchpath tests, then one-box A/B old vs new library
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r4_run5
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_f16x3.py tests/test_gpu_kernels.py \
+  tests/test_gpu_parity.py tests/test_gpu_benchpath.py > $O/tests.txt 2>&1 || { grep -E "FAIL|Error|assert" $O/tests.txt | head -30; tail -5 $O/tests.txt; exit 1; }
+tail -2 $O/tests.txt
+for r in 1 2; do
+  for v in old new; do
+    MMTRACK_LIB=$PWD/abx/lib$v.so timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 --warmup 10 > $O/vit_$v.json 2>$O/err.log || exit 1
+    echo "vit32 $v round $r: $(python -c "import json; d=json.load(open('$O/vit_$v.json')); print(d['value'], d['roofline']['frac'], {c: v['avg_launch_us'] for c, v in d['roofline']['classes'].items()})")"
+  done
+done
+for v in old new; do
+  MMTRACK_LIB=$PWD/abx/lib$v.so timeout -k 10 200 python bench.py --no-cpu-baseline --batch 1 --steps 200 --warmup 20 --probe none > $O/b1_$v.json 2>$O/err.log || exit 1
+  echo "b1 $v: $(python -c "import json; print(json.load(open('$O/b1_$v.json'))['value'])")"
+done
