@@ -26,6 +26,8 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <vector>
+#include <cstdio>
 
 #include "../../include/mmtrack.h"
 #include "common.h"
@@ -33,6 +35,13 @@
 namespace mmt {
 
 constexpr int kMaxShards = 64, kShardStride = 32;   // sharded max words: 64 x 128-B lines per tensor
+
+#if defined(CONV_STAMPS)   // tuning builds only: per-workgroup phase cycles of conv_f16x3_deep_kernel
+__device__ unsigned long long* g_conv_stamps = nullptr;   // [block][8]
+#define CSTAMP_T() (threadIdx.x == 0 ? __builtin_amdgcn_s_memtime() : 0ull)
+#else
+#define CSTAMP_T() 0ull
+#endif
 constexpr int kMaxGroups = 2, kMaxSplitK = 8;
 
 struct ConvGroupArgs {            // one convolution of a grouped launch (the RGB / aux backbones' twin layers)
@@ -638,11 +647,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     if (j + 2 >= 0) load_w(j + 2, j + 2);
     load_a(j + NR, r[j + NR]);
   }
+  const unsigned long long ts0 = CSTAMP_T();
   wait_set(r[0], CA{});
   stash(r[0], 0);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_W) : "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  unsigned long long tsl = CSTAMP_T(), sum_issue = 0, sum_mma = 0, sum_awt = 0, sum_stash = 0, sum_bar = 0;
+  const unsigned long long ts1 = tsl;
   for (int i0 = 0; i0 < nt; i0 += 6) {
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
@@ -650,15 +662,38 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
       if (j >= nt) break;
       load_w(j + 2, (u + 2) % 3);
       load_a(j + NR, r[u % NR]);
+      unsigned long long tq = CSTAMP_T();
+      sum_issue += tq - tsl;
       compute(u & 1, u % 3);
+#if defined(CONV_STAMPS)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+      unsigned long long tc = CSTAMP_T();
+      sum_mma += tc - tq;
       wait_set(r[(u + 1) % NR], CA{});
+      tq = CSTAMP_T();
+      sum_awt += tq - tc;
       stash(r[(u + 1) % NR], (u + 1) & 1);
+      tc = CSTAMP_T();
+      sum_stash += tc - tq;
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_W) : "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      tsl = CSTAMP_T();
+      sum_bar += tsl - tc;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the zero-loads past the slice, before the LDS is left
+#if defined(CONV_STAMPS)
+  if (threadIdx.x == 0 && g_conv_stamps) {
+    const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    unsigned long long* o = g_conv_stamps + bid * 8;
+    o[0] = ts1 - ts0; o[1] = sum_issue; o[2] = sum_mma; o[3] = sum_awt; o[4] = sum_stash; o[5] = sum_bar;
+    o[6] = (unsigned long long)nt; o[7] = tsl - ts0;
+  }
+#else
+  (void)ts0; (void)ts1; (void)sum_issue; (void)sum_mma; (void)sum_awt; (void)sum_stash; (void)sum_bar;
+#endif
 #pragma unroll
   for (int k = 0; k < NR; ++k) asm volatile("" : "+v"(r[k].a0), "+v"(r[k].a1));
 
@@ -1102,6 +1137,31 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
     else
       hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3>), grid, dim3(512), 0, s, a);
   }
+#if defined(CONV_STAMPS)
+  if (!ppx && !conv_old && Cin > 4) {   // the deep kernel ran: per-phase cycles averaged over its workgroups
+    const size_t nb = (size_t)grid.x * grid.y * grid.z;
+    unsigned long long* buf = nullptr;
+    if (hipMalloc(&buf, nb * 64) == hipSuccess) {
+      hipMemsetAsync(buf, 0, nb * 64, s);
+      hipMemcpyToSymbolAsync(HIP_SYMBOL(g_conv_stamps), &buf, sizeof(buf), 0, hipMemcpyHostToDevice, s);
+      if (conv_nr == 2)
+        hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2>), grid, dim3(512), 0, s, a);
+      hipStreamSynchronize(s);
+      std::vector<unsigned long long> h(nb * 8);
+      hipMemcpy(h.data(), buf, nb * 64, hipMemcpyDeviceToHost);
+      double acc[8] = {0};
+      for (size_t b = 0; b < nb; ++b)
+        for (int k = 0; k < 8; ++k) acc[k] += (double)h[b * 8 + k];
+      const double kt = acc[6] > 0 ? acc[6] : 1;
+      fprintf(stderr, "conv stamps M=%lld Cin=%d Cout=%d k=%d: per K-tile cycles issue %.0f mfma %.0f a-wait %.0f stash %.0f "
+              "w-wait+barrier %.0f | prologue %.0f, total/K-tile %.0f (%zu blocks)\n", (long long)M, Cin, Cout, kh,
+              acc[1] / kt, acc[2] / kt, acc[3] / kt, acc[4] / kt, acc[5] / kt, acc[0] / nb, acc[7] / kt, nb);
+      const unsigned long long* z = nullptr;
+      hipMemcpyToSymbol(HIP_SYMBOL(g_conv_stamps), &z, sizeof(z));
+      hipFree(buf);
+    }
+  }
+#endif
   if (ks > 1) {
     const int64_t q = M * Cout / 4;
     hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((q + 255) / 256), G), dim3(256), 0, s, a);

@@ -12,6 +12,8 @@ rows = list(csv.DictReader(open(path)))
 arg = sys.argv[2] if len(sys.argv) > 2 else "auto"
 if arg == "auto":
     steps = float(sum(float(r["Calls"]) for r in rows if "geometry_kernel" in r["Name"]))
+    if not steps:   # the mfDiMP path: one dimp_localize_kernel per tracked frame of the batch
+        steps = float(sum(float(r["Calls"]) for r in rows if "dimp_localize_kernel" in r["Name"]))
 else:
     steps = float(arg)
 tot = sum(float(r["TotalDurationNs"]) for r in rows)

@@ -17,3 +17,6 @@ for v in old new; do
   MMTRACK_LIB=$PWD/abx/lib$v.so timeout -k 10 200 python bench.py --no-cpu-baseline --batch 1 --steps 200 --warmup 20 --probe none > $O/b1_$v.json 2>$O/err.log || exit 1
   echo "b1 $v: $(python -c "import json; print(json.load(open('$O/b1_$v.json'))['value'])")"
 done
+# phase stamps of the deep generic conv (tuning build abx/libstamps.so; all shapes through the generic kernel)
+MMTRACK_LIB=$PWD/abx/libstamps.so MMT_CONV_NOPATCH=1 timeout -k 10 120 python tools/bench_conv_f16x3.py > $O/stamps.jsonl 2> $O/stamps.err || { tail -3 $O/stamps.err; exit 0; }
+grep "conv stamps" $O/stamps.err | sort | uniq -c | head -20
