@@ -133,6 +133,52 @@ def test_dimp_branch_golden_covers_every_flag():
     assert not np.array_equal(ev[8], plain[8])
 
 
+def test_oracle_dimp_decisions_match_reference():
+    """oracle/dimp_decide.py (localize_advanced, update_state, update_memory / update_sample_weights and the
+    Gauss-Newton iteration choice of DeT's DiMP tracker) on the decision records of tracker_dimp_branches.npz:
+    from the reference's state before every frame and its score map, the reference's flag, iteration count,
+    replaced slot, sample count and -- bit for bit -- its position, size, scale, sample weights and boxes after it
+    (the same float32 tensor arithmetic), over every branch sequence (261 frames)."""
+    import json
+    from types import SimpleNamespace
+
+    import torch
+
+    from oracle import dimp_decide as odd
+    g = np.load(os.path.join(GOLDEN, "tracker_dimp_branches.npz"))
+    base = dict(target_not_found_threshold=0.25, distractor_threshold=0.8, hard_negative_threshold=0.5,
+                target_neighborhood_scale=2.2, dispalcement_scale=0.8, hard_negative_learning_rate=0.02,
+                learning_rate=0.01, init_samples_minimum_weight=0.25, train_skipping=20, update_classifier=True,
+                net_opt_update_iter=2, net_opt_hn_iter=1)
+    n_dec = 0
+    for name in g["names"]:
+        p = f"{name}/"
+        prm = SimpleNamespace(**{**base, **json.loads(str(g[p + "params"]))})
+        bt0, bt1, ih, iw, smin, smax, ninit = g[p + "const"]
+        flags = g[p + "flags"]
+        T = lambda a: torch.from_numpy(np.array(a, dtype=np.float32))
+        for i in range(len(flags) - 1):
+            prev = int(g[p + "dec_pre_prev"][i])
+            st = dict(pos=T(g[p + "dec_pre_pos"][i]), target_sz=T(g[p + "dec_pre_sz"][i]), base_target_sz=T([bt0, bt1]),
+                      image_sz=T([ih, iw]), target_scale=T(g[p + "dec_pre_scale"][i]), min_scale_factor=T(smin),
+                      max_scale_factor=T(smax), frame_num=int(g[p + "dec_pre_frame"][i]), num_init=int(ninit),
+                      num_stored=int(g[p + "dec_pre_nstored"][i]), prev_replace=None if prev < 0 else prev,
+                      sample_weights=T(g[p + "dec_pre_sw"][i]), target_boxes=T(g[p + "dec_pre_tb"][i]))
+            flag, num_iter, r_ind, box = odd.decide(st, T(g[p + "dec_scores"][i]), T(g[p + "dec_coords"][i]), prm)
+            t = i + 1
+            assert flag == str(flags[t]), (name, t, flag, flags[t])
+            assert num_iter == int(g[p + "dec_num_iter"][i]), (name, t)
+            assert st["num_stored"] == int(g[p + "dec_post_nstored"][i])
+            assert (-1 if st["prev_replace"] is None else st["prev_replace"]) == int(g[p + "dec_post_prev"][i])
+            for key, gk in (("pos", "dec_post_pos"), ("target_sz", "dec_post_sz"), ("sample_weights", "dec_post_sw"),
+                            ("target_boxes", "dec_post_tb")):
+                np.testing.assert_array_equal(st[key].numpy(), g[p + gk][i], err_msg=f"{name} {t} {key}")
+            assert float(st["target_scale"]) == float(g[p + "dec_post_scale"][i])
+            np.testing.assert_allclose(box.numpy(), g[p + "boxes"][t], rtol=0, atol=1e-4)
+            n_dec += 1
+    assert n_dec == 261
+
+
 def test_cv2_resize_restatement_properties():
     """Unpinned piece: self-consistency of the INTER_LINEAR restatement."""
     rng = np.random.Generator(np.random.PCG64(3))
