@@ -515,14 +515,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 // Step j issues W(j + 2) then A(j + NR), multiplies K-tile j, waits for A(j + 1) -- 2 (NW + NA) younger operations
 // (for NR = 3) -- and stashes it, then waits for W(j + 1) and passes the barrier.  Same products, same summation
 // order as conv_f16x3_kernel (bit-identical).
-template <int BN, int NR>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_f16x3_deep_kernel(const ConvF16Args a) {
-  constexpr int BM = 128, BK = 32, NWS = 3;
-  constexpr int WN = BN / 2, FM = 2, FN = WN / 16;
+// BM = 256 (tuning, MMT_CONV_BM=256): 64 x 64 per wave -- 16 fragment reads per 48 MFMAs instead of 12 per 24, one
+// barrier per 48 -- at one workgroup per CU (112 KB of LDS)
+// OVL: K-tile j + 1's activations are waited for BEFORE K-tile j is multiplied, and split and stashed in the same
+// scheduling region as its MFMAs (no inline asm between them), so the split's VALU work and the LDS stores issue
+// between the MFMAs instead of after them while every wave of the CU sits in the same phase between two barriers.
+template <int BN, int NR, int BM = 128, bool OVL = false>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ? 4 : 2))) void conv_f16x3_deep_kernel(
+    const ConvF16Args a) {
+  constexpr int BK = 32, NWS = 3;
+  constexpr int WN = BN / 2, FM = BM / 64, FN = WN / 16;
+  constexpr int SL = BM / 128;                 // activation slots (a row's 8 K values) per thread
   constexpr int NW = BN / 64;                  // W LDS-DMA pieces per wave per K-tile
-  constexpr int NA = 2;                        // A loads per thread per K-tile
+  constexpr int NA = 2 * SL;                   // A loads per thread per K-tile
   constexpr int WAIT_A = (NR - 1) * (NW + NA); // younger operations when A(j + 1) is waited for
   constexpr int WAIT_W = 2 * NA + NW;          // ... when W(j + 1) is (A(j + NR - 1), W(j + 2), A(j + NR))
+  constexpr int WAIT_AE = (NR - 2) * (NW + NA); // OVL: ... when A(j + 1) is, before step j's loads
   static_assert(NR == 2 || NR == 3, "register sets");
   __shared__ __attribute__((aligned(16))) uint16_t sA[2][2][BM * BK];
   __shared__ __attribute__((aligned(16))) uint16_t sW[NWS][2][BN * BK];
@@ -540,18 +548,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   }
   const float inv = g.inv_w / sa;
 
-  const int ar = t >> 2, ac = t & 3;
-  const int m = m0 + ar;
-  const bool mval = m < M;
-  int iy0 = 0, ix0 = 0;
-  uint32_t xrow = 0;
-  if (mval) {
-    const int nimg = m / (a.Ho * a.Wo);
-    const int r = m - nimg * a.Ho * a.Wo;
-    const int oy = r / a.Wo, ox = r - oy * a.Wo;
-    iy0 = oy * a.stride - a.pad;
-    ix0 = ox * a.stride - a.pad;
-    xrow = (uint32_t)(nimg * a.H * a.W * a.Cin);
+  const int ac = t & 3;   // slot s: row (t >> 2) + 128 s, K chunk ac (8 values)
+  bool mval[SL];
+  int iy0[SL], ix0[SL];
+  uint32_t xrow[SL];
+#pragma unroll
+  for (int sl = 0; sl < SL; ++sl) {
+    const int m = m0 + (t >> 2) + 128 * sl;
+    mval[sl] = m < M;
+    iy0[sl] = ix0[sl] = 0;
+    xrow[sl] = 0;
+    if (mval[sl]) {
+      const int nimg = m / (a.Ho * a.Wo);
+      const int r = m - nimg * a.Ho * a.Wo;
+      const int oy = r / a.Wo, ox = r - oy * a.Wo;
+      iy0[sl] = oy * a.stride - a.pad;
+      ix0[sl] = ox * a.stride - a.pad;
+      xrow[sl] = (uint32_t)(nimg * a.H * a.W * a.Cin);
+    }
   }
   const u32x4 qX = make_rsrc_words(g.x, (int64_t)a.N * a.H * a.W * a.Cin * 4);
   const int nk = a.Kp / BK;
@@ -559,7 +573,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   const int cpt = a.Cin / BK;
 
   struct DeepRegs {   // native vectors: an inline-asm register operand, not a struct in memory
-    f32x4 a0, a1;
+    f32x4 a[2 * SL];
   };
   DeepRegs r[NR];
   // K-tile i of the slice (zeros past it: an out-of-range offset, no traffic) into register set `set`
@@ -567,11 +581,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     const int kt = kt0 + i;
     const int tap = kt / cpt, c0 = (kt - tap * cpt) * BK + ac * 8;
     const int ky = tap / a.kw, kx = tap - ky * a.kw;
-    const int iy = iy0 + ky, ix = ix0 + kx;
-    const bool ok = i < nt && mval && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-    const uint32_t vo = ok ? (xrow + (uint32_t)((iy * a.W + ix) * a.Cin + c0)) * 4 : kBufOob;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(set.a0) : "v"(vo), "s"(qX) : "memory");
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:16" : "=v"(set.a1) : "v"(vo), "s"(qX) : "memory");
+#pragma unroll
+    for (int sl = 0; sl < SL; ++sl) {
+      const int iy = iy0[sl] + ky, ix = ix0[sl] + kx;
+      const bool ok = i < nt && mval[sl] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const uint32_t vo = ok ? (xrow[sl] + (uint32_t)((iy * a.W + ix) * a.Cin + c0)) * 4 : kBufOob;
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(set.a[2 * sl]) : "v"(vo), "s"(qX) : "memory");
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:16" : "=v"(set.a[2 * sl + 1]) : "v"(vo), "s"(qX)
+                   : "memory");
+    }
   };
   const u32x4 qWh = make_rsrc_words(g.wh, (int64_t)a.Cout * a.Kp * 2);
   const u32x4 qWl = make_rsrc_words(g.wl, (int64_t)a.Cout * a.Kp * 2);
@@ -593,7 +611,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   // the register set's loads done: all but the CNT youngest vector-memory operations (the set named as read-write,
   // so nothing reads it above this point)
   auto wait_set = [&](DeepRegs& set, auto cnt) {
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(set.a0), "+v"(set.a1) : "n"(decltype(cnt)::value) : "memory");
+    if constexpr (SL == 1)
+      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(set.a[0]), "+v"(set.a[1]) : "n"(decltype(cnt)::value) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%4)" : "+v"(set.a[0]), "+v"(set.a[1]), "+v"(set.a[2]), "+v"(set.a[3])
+                   : "n"(decltype(cnt)::value) : "memory");
   };
   auto pack2 = [&](float x, float y, uint32_t& h, uint32_t& l) {
     uint16_t hx, lx, hy, ly;
@@ -603,13 +625,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     l = lx | (uint32_t)ly << 16;
   };
   auto stash = [&](const DeepRegs& rr, int st) {
-    uint4 hv, lv;
-    pack2(rr.a0[0], rr.a0[1], hv.x, lv.x);
-    pack2(rr.a0[2], rr.a0[3], hv.y, lv.y);
-    pack2(rr.a1[0], rr.a1[1], hv.z, lv.z);
-    pack2(rr.a1[2], rr.a1[3], hv.w, lv.w);
-    *reinterpret_cast<uint4*>(&sA[st][0][cswz(ar, ac)]) = hv;
-    *reinterpret_cast<uint4*>(&sA[st][1][cswz(ar, ac)]) = lv;
+#pragma unroll
+    for (int sl = 0; sl < SL; ++sl) {
+      const f32x4 &x0 = rr.a[2 * sl], &x1 = rr.a[2 * sl + 1];
+      uint4 hv, lv;
+      pack2(x0[0], x0[1], hv.x, lv.x);
+      pack2(x0[2], x0[3], hv.y, lv.y);
+      pack2(x1[0], x1[1], hv.z, lv.z);
+      pack2(x1[2], x1[3], hv.w, lv.w);
+      const int ar = (t >> 2) + 128 * sl;
+      *reinterpret_cast<uint4*>(&sA[st][0][cswz(ar, ac)]) = hv;
+      *reinterpret_cast<uint4*>(&sA[st][1][cswz(ar, ac)]) = lv;
+    }
   };
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -621,7 +648,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     bf16x8 ah[FM], al[FM];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int row = wm * 32 + i * 16 + (lane & 15);
+      const int row = wm * (BM / 4) + i * 16 + (lane & 15);
       ah[i] = *reinterpret_cast<const bf16x8*>(&sA[sta][0][cswz(row, c)]);
       al[i] = *reinterpret_cast<const bf16x8*>(&sA[sta][1][cswz(row, c)]);
     }
@@ -636,6 +663,62 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
         acc[i][j] = mfma16<true>(bl, ah[i], acc[i][j]);
         acc[i][j] = mfma16<true>(bh, al[i], acc[i][j]);
       }
+    }
+  };
+  // OVL: K-tile (sta, stw) multiplied with the next K-tile's split woven in: all fragment reads first, then after
+  // every other MFMA triple one pack2 (two values) of the split -- fenced (sched_barrier) so the compiler keeps the
+  // weave instead of clustering the MFMAs -- and the stash's LDS stores last
+  auto compute_split = [&](int sta, int stw, const DeepRegs& rr, int st) {
+    const int c = lane >> 4;
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * (BM / 4) + i * 16 + (lane & 15);
+      ah[i] = *reinterpret_cast<const bf16x8*>(&sA[sta][0][cswz(row, c)]);
+      al[i] = *reinterpret_cast<const bf16x8*>(&sA[sta][1][cswz(row, c)]);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * WN + j * 16 + (lane & 15);
+      bh[j] = *reinterpret_cast<const bf16x8*>(&sW[stw][0][cswz(row, c)]);
+      bl[j] = *reinterpret_cast<const bf16x8*>(&sW[stw][1][cswz(row, c)]);
+    }
+    uint32_t hw[4 * SL], lw[4 * SL];
+    constexpr int NP = 4 * SL, NT = FM * FN, EVERY = NT / NP > 0 ? NT / NP : 1;
+    int p = 0;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        // empty asm on the operands pins the order (instruction selection moves pure operations across fences)
+        asm volatile("" : "+v"(acc[i][j]));
+        acc[i][j] = mfma16<true>(bh[j], ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bl[j], ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bh[j], al[i], acc[i][j]);
+        asm volatile("" : "+v"(acc[i][j]));
+        __builtin_amdgcn_sched_barrier(0);
+        if ((j * FM + i) % EVERY == EVERY - 1 && p < NP) {
+          const f32x4& x = rr.a[p >> 1];
+          float x0 = x[(p & 1) * 2], x1 = x[(p & 1) * 2 + 1];
+          asm volatile("" : "+v"(x0), "+v"(x1));
+          pack2(x0, x1, hw[p], lw[p]);
+          asm volatile("" : "+v"(hw[p]), "+v"(lw[p]));
+          ++p;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+    for (; p < NP; ++p) {
+      const f32x4& x = rr.a[p >> 1];
+      pack2(x[(p & 1) * 2], x[(p & 1) * 2 + 1], hw[p], lw[p]);
+    }
+#pragma unroll
+    for (int sl = 0; sl < SL; ++sl) {
+      const int ar = (t >> 2) + 128 * sl;
+      *reinterpret_cast<uint4*>(&sA[st][0][cswz(ar, ac)]) =
+          make_uint4(hw[4 * sl], hw[4 * sl + 1], hw[4 * sl + 2], hw[4 * sl + 3]);
+      *reinterpret_cast<uint4*>(&sA[st][1][cswz(ar, ac)]) =
+          make_uint4(lw[4 * sl], lw[4 * sl + 1], lw[4 * sl + 2], lw[4 * sl + 3]);
     }
   };
   using CA = std::integral_constant<int, WAIT_A>;
@@ -660,22 +743,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     for (int u = 0; u < 6; ++u) {
       const int j = i0 + u;
       if (j >= nt) break;
-      load_w(j + 2, (u + 2) % 3);
-      load_a(j + NR, r[u % NR]);
-      unsigned long long tq = CSTAMP_T();
-      sum_issue += tq - tsl;
-      compute(u & 1, u % 3);
+      unsigned long long tq, tc;
+      if constexpr (OVL) {
+        wait_set(r[(u + 1) % NR], std::integral_constant<int, WAIT_AE>{});
+        tq = CSTAMP_T();
+        sum_awt += tq - tsl;
+        load_w(j + 2, (u + 2) % 3);
+        load_a(j + NR, r[u % NR]);
+        tc = CSTAMP_T();
+        sum_issue += tc - tq;
+        compute_split(u & 1, u % 3, r[(u + 1) % NR], (u + 1) & 1);
 #if defined(CONV_STAMPS)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
-      unsigned long long tc = CSTAMP_T();
-      sum_mma += tc - tq;
-      wait_set(r[(u + 1) % NR], CA{});
-      tq = CSTAMP_T();
-      sum_awt += tq - tc;
-      stash(r[(u + 1) % NR], (u + 1) & 1);
-      tc = CSTAMP_T();
-      sum_stash += tc - tq;
+        tq = CSTAMP_T();
+        sum_mma += tq - tc;
+        tc = tq;
+      } else {
+        load_w(j + 2, (u + 2) % 3);
+        load_a(j + NR, r[u % NR]);
+        tq = CSTAMP_T();
+        sum_issue += tq - tsl;
+        compute(u & 1, u % 3);
+#if defined(CONV_STAMPS)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+        tc = CSTAMP_T();
+        sum_mma += tc - tq;
+        wait_set(r[(u + 1) % NR], CA{});
+        tq = CSTAMP_T();
+        sum_awt += tq - tc;
+        stash(r[(u + 1) % NR], (u + 1) & 1);
+        tc = CSTAMP_T();
+        sum_stash += tc - tq;
+      }
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_W) : "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -694,8 +795,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #else
   (void)ts0; (void)ts1; (void)sum_issue; (void)sum_mma; (void)sum_awt; (void)sum_stash; (void)sum_bar;
 #endif
-#pragma unroll
-  for (int k = 0; k < NR; ++k) asm volatile("" : "+v"(r[k].a0), "+v"(r[k].a1));
 
   const int li = lane & 15, lk = lane >> 4;
   if (a.ks > 1) {
@@ -703,7 +802,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     float* pb = a.part + ((int64_t)slice * G + grp) * M * a.Cout;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int mo = m0 + wm * 32 + i * 16 + li;
+      const int mo = m0 + wm * (BM / 4) + i * 16 + li;
       if (mo >= M) continue;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -717,7 +816,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   float ymx = 0.f;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int mo = m0 + wm * 32 + i * 16 + li;
+    const int mo = m0 + wm * (BM / 4) + i * 16 + li;
     if (mo >= M) continue;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -1043,15 +1142,23 @@ int patch_plan(int H, int W, int Cin, int kh, int kw, int stride, int pad, int* 
   return px;
 }
 
+// output pixels per tile of the generic kernel: 128, or 256 with MMT_CONV_BM=256 (tuning) for 128-wide tiles
+int conv_bm_for(int Cin, int bn) {
+  static const bool old = getenv("MMT_CONV_OLD") != nullptr;
+  static const int bm = getenv("MMT_CONV_BM") ? atoi(getenv("MMT_CONV_BM")) : 128;
+  return bm == 256 && !old && Cin > 4 && bn == 128 ? 256 : 128;
+}
+
 // M tiles of a launch (the patch kernel tiles each image separately) and its K split
 int64_t conv_ks_for(int N, int H, int W, int Ho, int Wo, int Cin, int Cout, int kh, int kw, int stride, int pad, int Kp,
                     int G) {
-  const int64_t gm = ((int64_t)N * Ho * Wo + 127) / 128;
-  const int bn = conv_bn(gm, Cin, Cout, G);
+  const int64_t M = (int64_t)N * Ho * Wo;
+  const int bn = conv_bn((M + 127) / 128, Cin, Cout, G);
   int tpi = 0;
   if (patch_plan(H, W, Cin, kh, kw, stride, pad, &tpi))
     return std::min<int64_t>(conv_pick_ks((int64_t)N * tpi * (Cout / bn) * G, Kp / 32), Cin / 32);
-  return conv_pick_ks(gm * (Cout / bn) * G, Kp / 32);
+  const int bm = conv_bm_for(Cin, bn);
+  return conv_pick_ks((M + bm - 1) / bm * (Cout / bn) * G, Kp / 32);
 }
 
 }  // namespace
@@ -1094,8 +1201,9 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   if (ks > 1 && (!ws || ws_bytes < (size_t)(ks * G * M * (int64_t)Cout * 4))) ks = 1;
   a.ks = ks;
   a.part = static_cast<float*>(ws);
-  const unsigned gm = (unsigned)((M + 127) / 128);
   const int bn = conv_bn((M + 127) / 128, Cin, Cout, G);
+  const int conv_bm = conv_bm_for(Cin, bn);
+  const unsigned gm = (unsigned)((M + conv_bm - 1) / conv_bm);
   const dim3 grid(gm, Cout / bn, G * ks);
   const hipStream_t s = (hipStream_t)stream;
   // the stem on a 4-channel image: 2-D tiles from an LDS input patch (MMT_CONV_STEM_OLD: the gather kernel, tuning)
@@ -1103,6 +1211,7 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   static const int stem_th = getenv("MMT_CONV_STEM_TH") ? atoi(getenv("MMT_CONV_STEM_TH")) : 16;   // tuning: 8
   static const bool conv_old = getenv("MMT_CONV_OLD") != nullptr;   // tuning: conv_f16x3_kernel (two-deep)
   static const int conv_nr = getenv("MMT_CONV_NR") ? atoi(getenv("MMT_CONV_NR")) : 2;   // tuning: 3
+  static const bool conv_ovl = getenv("MMT_CONV_OVL") != nullptr;   // tuning: split overlapped with the MFMAs
   int tpi = 0;
   const int ppx = patch_plan(H, W, Cin, kh, kw, stride, pad, &tpi);
   if (ppx) {
@@ -1126,6 +1235,13 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
       hipLaunchKernelGGL((conv_f16x3_kernel<128, false>), grid, dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL((conv_f16x3_kernel<64, false>), grid, dim3(512), 0, s, a);
+  } else if (conv_bm == 256) {
+    hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2, 256>), grid, dim3(512), 0, s, a);
+  } else if (conv_ovl) {
+    if (bn == 128)
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3, 128, true>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3, 128, true>), grid, dim3(512), 0, s, a);
   } else if (conv_nr == 2) {
     if (bn == 128)
       hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2>), grid, dim3(512), 0, s, a);
@@ -1138,13 +1254,15 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
       hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3>), grid, dim3(512), 0, s, a);
   }
 #if defined(CONV_STAMPS)
-  if (!ppx && !conv_old && Cin > 4) {   // the deep kernel ran: per-phase cycles averaged over its workgroups
+  if (!ppx && !conv_old && Cin > 4 && conv_bm == 128) {   // the deep kernel ran: per-phase cycles averaged over its workgroups
     const size_t nb = (size_t)grid.x * grid.y * grid.z;
     unsigned long long* buf = nullptr;
     if (hipMalloc(&buf, nb * 64) == hipSuccess) {
       hipMemsetAsync(buf, 0, nb * 64, s);
       hipMemcpyToSymbolAsync(HIP_SYMBOL(g_conv_stamps), &buf, sizeof(buf), 0, hipMemcpyHostToDevice, s);
-      if (conv_nr == 2)
+      if (conv_ovl)
+        hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3, 128, true>), grid, dim3(512), 0, s, a);
+      else if (conv_nr == 2)
         hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2>), grid, dim3(512), 0, s, a);
       hipStreamSynchronize(s);
       std::vector<unsigned long long> h(nb * 8);

@@ -88,7 +88,8 @@ def test_conv_kernels_bitwise(tmp_path):
     res = {}
     for mode, extra in (("old", {"MMT_CONV_OLD": "1", "MMT_CONV_NOPATCH": "1"}),
                         ("deep3", {"MMT_CONV_NR": "3", "MMT_CONV_NOPATCH": "1"}), ("deep2", {"MMT_CONV_NOPATCH": "1"}),
-                        ("patch", {})):
+                        ("bm256", {"MMT_CONV_BM": "256", "MMT_CONV_NOPATCH": "1"}),
+                        ("ovl", {"MMT_CONV_OVL": "1", "MMT_CONV_NOPATCH": "1"}), ("patch", {})):
         env = {k: v for k, v in os.environ.items() if not k.startswith("MMT_CONV_")}
         env.update(extra)
         path = str(tmp_path / f"{mode}.npz")
@@ -96,11 +97,16 @@ def test_conv_kernels_bitwise(tmp_path):
                            text=True, timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr
         res[mode] = np.load(path)
-    for mode in ("deep3", "deep2"):
+    for mode in ("deep3", "deep2", "ovl"):
         for key in res["old"].files:
             np.testing.assert_array_equal(res[mode][key], res["old"][key], err_msg=f"{mode} {key}")
     for key in res["old"].files:
         close(res["patch"][key], res["old"][key], 1e-5)
+        # 256-pixel tiles: same products and order per output (bit-identical) unless fewer tiles pick another K split
+        if key.startswith("y"):
+            np.testing.assert_array_equal(res["bm256"][key], res["old"][key], err_msg=f"bm256 {key}")
+        else:
+            close(res["bm256"][key], res["old"][key], 1e-5)
 
 
 @pytest.mark.parametrize("N,C,H,W,Co,k,s,p", [(1, 1024, 18, 18, 256, 3, 1, 1), (2, 1024, 18, 18, 512, 3, 1, 1),
