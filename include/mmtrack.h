@@ -184,6 +184,9 @@ int mmt_rgbx_merge(const uint8_t* rgb, int64_t rgb_stride, const uint8_t* aux, i
 #define MMT_CONV_RELU 1   /* y = max(y, 0) after bias / residual                                    */
 #define MMT_CONV_MAX 2    /* y = max(y_old, y): the 'max' merge of the two backbones (dimpnet.py:103) */
 #define MMT_CONV_W4 4     /* Cin == 3 and w is [Cout][kh][kw][4] (4th channel zero): the stem, one tap per load */
+#define MMT_CONV_POOL 8   /* f16x3 stem (7x7 / stride 2, 4 channels, 64 outputs) with ResNet's 3x3 / stride-2 / pad-1
+                             max-pool fused: y is the pooled [N][(Ho-1)/2+1][(Wo-1)/2+1][64] map (dimpnet.py backbone
+                             conv1 -> bn1 -> relu -> maxpool); every group of the launch sets it or none          */
 /* nn.Conv2d (+ folded BN, + residual, ReLU): y [N*Ho*Wo][Cout] = conv(x [N][H][W][Cin]); Cout % 64 == 0 */
 int mmt_conv2d_f32(const float* x, int N, int H, int W, int Cin, const float* w, const float* bias, int Cout, int kh,
                    int kw, int stride, int pad, const float* resid, float* y, int flags, void* hip_stream);

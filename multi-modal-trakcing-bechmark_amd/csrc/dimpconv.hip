@@ -505,6 +505,206 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.z * 13, reinterpret_cast<float*>(&sP[0][0]));
 }
 
+// The stem with ResNet's max-pool (3 x 3 / stride 2 / pad 1, dimpnet.py's backbone conv1 -> bn1 -> relu -> maxpool)
+// fused in (MMT_CONV_POOL): a workgroup owns an 8 x 8 tile of POOLED outputs, computes the 17 x 17 stem outputs
+// their windows read (rows 16 ty - 1 .. 16 ty + 15; the shared edge row / column is computed by both neighbours), max-
+// pools them from the LDS and writes only the pooled map -- the full-resolution stem map (4x the pooled bytes) is never
+// written or read back, and the separate max-pool launch goes.  The 289 stem pixels run as 19 MFMA row fragments
+// (five per wave row, the twentieth idle) over the conv_stem_f16x3_kernel K order; same products, same order, and the
+// window max in maxpool4_kernel's order over the valid pixels (-inf elsewhere): the pooled map is the two kernels'
+// bit for bit.  7 x 7 / stride 2 / 4 channels / 64 outputs only: K = 49 taps x 4 = 196, so the last of the seven
+// 32-deep K-tiles holds one tap and only its first 16-B chunk of each weight row is staged (the other three lanes'
+// fragments read the same finite weights against the zero pixel).
+constexpr int kPoolT = 8, kPoolS = 2 * kPoolT + 1, kPoolPx = kPoolS * kPoolS;   // 8 x 8 pooled, 17 x 17 stem
+constexpr int kPoolPW = (kPoolS - 1) * 2 + 7, kPoolMaxP = kPoolPW * kPoolPW;      // 39 x 39 input pixels
+constexpr int kPoolLdsP = 2 * (kPoolMaxP + 1) * 4 * 2;                               // patch hi / lo (+ zero pixel)
+constexpr int kPoolLdsW = 6 * 2 * 64 * 32 * 2 + 2 * 64 * 8 * 2;                     // K-tiles 0-5, chunk 0 of 6
+constexpr int kPoolLds = kPoolLdsP + kPoolLdsW > kPoolPx * 64 * 4 ? kPoolLdsP + kPoolLdsW : kPoolPx * 64 * 4;
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_stem_pool_f16x3_kernel(
+    const ConvF16Args a, int PHo, int PWo) {
+  constexpr int BN = 64, BK = 32, WN = BN / 2, FM = 5, FN = WN / 16, NPL = (kPoolMaxP + 511) / 512;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kPoolLds];
+  uint16_t* sPh = reinterpret_cast<uint16_t*>(lds);
+  uint16_t* sPl = sPh + (kPoolMaxP + 1) * 4;
+  uint16_t* sW = reinterpret_cast<uint16_t*>(lds + kPoolLdsP);          // [6][2][64 x 32], cswz rows
+  uint16_t* sW6 = sW + 6 * 2 * BN * BK;                                  // [2][64][8]: K-tile 6, chunk 0
+  float* sOut = reinterpret_cast<float*>(lds);                           // [289][64] after the K loop
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const ConvGroupArgs g = pick_group(a, blockIdx.z);
+  const int tiles_x = (PWo + kPoolT - 1) / kPoolT, tiles_y = (PHo + kPoolT - 1) / kPoolT;
+  const int img = blockIdx.x / (tiles_x * tiles_y), trem = blockIdx.x - img * (tiles_x * tiles_y);
+  const int ty = trem / tiles_x, tx = trem - ty * tiles_x;
+  const int sy0 = 2 * kPoolT * ty - 1, sx0 = 2 * kPoolT * tx - 1;       // the stem tile's first output row / col
+  const int iy0 = sy0 * 2 - a.pad, ix0 = sx0 * 2 - a.pad;
+
+  float sa = g.xscale;
+  if (g.xmax) {
+    const float mx = wave_max(g.xmax[lane * kShardStride]);
+    sa = mx > 0.f ? pow2_scale(mx) : 1.0f;
+  }
+  const float inv = g.inv_w / sa;
+
+  const u32x4 qWh = make_rsrc_words(g.wh, (int64_t)a.Cout * a.Kp * 2);
+  const u32x4 qWl = make_rsrc_words(g.wl, (int64_t)a.Cout * a.Kp * 2);
+  {
+    const int wimg = wave / (BN / 16), rb = wave % (BN / 16);
+    const int row = rb * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 2);
+    const uint32_t vo = (uint32_t)((row * a.Kp + c * 8) * 2);
+    for (int kt = 0; kt < 6; ++kt) {
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(lptr_t)(&sW[(kt * 2 + wimg) * BN * BK + rb * 16 * BK]));
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(kt * BK * 2));
+      if (wimg)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWl), "s"(so), "{m0}"(dst) : "memory");
+      else
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(vo), "s"(qWh), "s"(so), "{m0}"(dst) : "memory");
+    }
+    if (wave < 2) {   // K-tile 6, chunk 0 (K 192-199) of row = lane: 16 B per lane, rows contiguous
+      const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lptr_t)(&sW6[wave * BN * 8]));
+      const uint32_t vo6 = (uint32_t)((lane * a.Kp + 6 * BK) * 2);
+      if (wave)
+        asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(vo6), "s"(qWl), "{m0}"(dst) : "memory");
+      else
+        asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(vo6), "s"(qWh), "{m0}"(dst) : "memory");
+    }
+  }
+  const rsrc_t rX = make_rsrc(g.x, (int64_t)a.N * a.H * a.W * 16);
+  float4 pv[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int q = t + 512 * k, py = q / kPoolPW, px = q - py * kPoolPW;
+    const int iy = iy0 + py, ix = ix0 + px;
+    const bool ok = q < kPoolMaxP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    const uint32_t vo = ok ? (uint32_t)(((img * a.H + iy) * a.W + ix) * 16) : kBufOob;
+    pv[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rX, vo, 0, 0));
+  }
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int q = t + 512 * k;
+    if (q < kPoolMaxP) {
+      uint16_t h[4], l[4];
+      split_h(pv[k].x * sa, h[0], l[0]);
+      split_h(pv[k].y * sa, h[1], l[1]);
+      split_h(pv[k].z * sa, h[2], l[2]);
+      split_h(pv[k].w * sa, h[3], l[3]);
+      *reinterpret_cast<uint2*>(&sPh[q * 4]) = make_uint2(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16);
+      *reinterpret_cast<uint2*>(&sPl[q * 4]) = make_uint2(l[0] | (uint32_t)l[1] << 16, l[2] | (uint32_t)l[3] << 16);
+    }
+  }
+  if (t < 2) *reinterpret_cast<uint2*>(&(t ? sPl : sPh)[kPoolMaxP * 4]) = make_uint2(0u, 0u);   // the zero pixel
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // fragment i of wave row wm: stem pixels p = (wm + 4 i) * 16 + (lane & 15) of the 17 x 17 tile (p >= 289: idle)
+  const int c = lane >> 4, col = lane & 15;
+  int pbase[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int p = (wm + 4 * i) * 16 + col, sr = p / kPoolS, sc = p - sr * kPoolS;
+    pbase[i] = p < kPoolPx ? (sr * 2) * kPoolPW + sc * 2 : -1;
+  }
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool last_idle = wm == 3;   // fragment 19 (wave row 3, i = 4) holds no pixel
+#pragma unroll
+  for (int kt = 0; kt < 7; ++kt) {
+    bf16x8 ah[FM], al[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      uint2 hv[2], lv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int tap = kt * 8 + 2 * c + h, ky = tap / 7, kx = tap - ky * 7;
+        const int pix = tap < 49 && pbase[i] >= 0 ? pbase[i] + ky * kPoolPW + kx : kPoolMaxP;
+        hv[h] = *reinterpret_cast<const uint2*>(&sPh[pix * 4]);
+        lv[h] = *reinterpret_cast<const uint2*>(&sPl[pix * 4]);
+      }
+      ah[i] = __builtin_bit_cast(bf16x8, make_uint4(hv[0].x, hv[0].y, hv[1].x, hv[1].y));
+      al[i] = __builtin_bit_cast(bf16x8, make_uint4(lv[0].x, lv[0].y, lv[1].x, lv[1].y));
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * WN + j * 16 + (lane & 15);
+      bf16x8 bh, bl;
+      if (kt < 6) {
+        bh = *reinterpret_cast<const bf16x8*>(&sW[(kt * 2 + 0) * BN * BK + cswz(row, c)]);
+        bl = *reinterpret_cast<const bf16x8*>(&sW[(kt * 2 + 1) * BN * BK + cswz(row, c)]);
+      } else {
+        bh = *reinterpret_cast<const bf16x8*>(&sW6[row * 8]);
+        bl = *reinterpret_cast<const bf16x8*>(&sW6[BN * 8 + row * 8]);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if (i == FM - 1 && last_idle) continue;
+        acc[i][j] = mfma16<true>(bh, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bl, ah[i], acc[i][j]);
+        acc[i][j] = mfma16<true>(bh, al[i], acc[i][j]);
+      }
+    }
+  }
+  __syncthreads();   // the patch and weights are free: the stem tile goes to sOut
+
+  // bias + ReLU per stem pixel (-inf outside the stem map: the pool's padding); 16-B chunk q of pixel p at
+  // q ^ (p & 15) (the 16 lanes of one fragment column write 16 distinct chunks: no bank conflict)
+  const int lk = lane >> 4;
+  float ymx = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int p = (wm + 4 * i) * 16 + col;
+    if (p >= kPoolPx) continue;
+    const int sr = p / kPoolS, sc = p - sr * kPoolS, oy = sy0 + sr, ox = sx0 + sc;
+    const bool valid = oy >= 0 && oy < a.Ho && ox >= 0 && ox < a.Wo;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int no = wn * WN + j * 16 + 4 * lk;
+      f32x4 v = acc[i][j] * inv;
+      if (g.bias) {
+        const float4 b = *reinterpret_cast<const float4*>(g.bias + no);
+        v += f32x4{b.x, b.y, b.z, b.w};
+      }
+      if (g.flags & MMT_CONV_RELU)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      if (valid) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
+      } else {
+        v = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      }
+      *reinterpret_cast<f32x4*>(&sOut[p * 64 + (((no >> 2) ^ (p & 15)) << 2)]) = v;
+    }
+  }
+  __syncthreads();
+  // the pooled 8 x 8 tile: thread t takes 4 channels (chunk t & 15) of pooled pixels t >> 4 and (t >> 4) + 32
+  {
+    const int q = t & 15;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pq = (t >> 4) + 32 * h, pr = pq >> 3, pc = pq & 7;
+      const int py = kPoolT * ty + pr, px = kPoolT * tx + pc;
+      if (py >= PHo || px >= PWo) continue;
+      f32x4 m = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int p = (2 * pr + dy) * kPoolS + 2 * pc + dx;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(&sOut[p * 64 + ((q ^ (p & 15)) << 2)]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], v[e]);
+        }
+      *reinterpret_cast<float4*>(g.y + (((int64_t)img * PHo + py) * PWo + px) * 64 + 4 * q) =
+          make_float4(m[0], m[1], m[2], m[3]);
+    }
+  }
+  __syncthreads();   // sOut is free for the max fold
+  if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.z * 13, reinterpret_cast<float*>(lds));
+}
+
 // The generic conv with a deeper operand pipeline.  conv_f16x3_kernel keeps one K-tile of weights and two of
 // activations in flight per workgroup (about 48 KB), which, at the several-microsecond latency of a loaded memory
 // system, caps a workgroup near 20 GB/s and the K loop at about 1.5 us per 32-deep K-tile -- measured: removing two
@@ -576,11 +776,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
     f32x4 a[2 * SL];
   };
   DeepRegs r[NR];
-  // K-tile i of the slice (zeros past it: an out-of-range offset, no traffic) into register set `set`
+  // K-tile i of the slice (zeros past it: an out-of-range offset, no traffic) into register set `set`.  The calls
+  // come in order i = 0, 1, 2, ...: the (tap, chunk) position advances by one chunk per call (wave-uniform
+  // counters instead of two integer divisions per K-tile)
+  int a_ch, a_ky, a_kx;
+  {
+    const int tap = kt0 / cpt;
+    a_ch = kt0 - tap * cpt;
+    a_ky = tap / a.kw;
+    a_kx = tap - a_ky * a.kw;
+  }
   auto load_a = [&](int i, DeepRegs& set) {
-    const int kt = kt0 + i;
-    const int tap = kt / cpt, c0 = (kt - tap * cpt) * BK + ac * 8;
-    const int ky = tap / a.kw, kx = tap - ky * a.kw;
+    const int c0 = a_ch * BK + ac * 8, ky = a_ky, kx = a_kx;
+    if (++a_ch == cpt) {
+      a_ch = 0;
+      if (++a_kx == a.kw) {
+        a_kx = 0;
+        ++a_ky;
+      }
+    }
 #pragma unroll
     for (int sl = 0; sl < SL; ++sl) {
       const int iy = iy0[sl] + ky, ix = ix0[sl] + kx;
@@ -1186,8 +1400,9 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   ConvF16Args a{};
   for (int i = 0; i < G; ++i) {
     const mmt_conv_group& c = groups[i];
-    if (!c.x || !c.w_hi || !c.w_lo || !c.y || !(c.w_scale > 0) || (c.flags & ~(MMT_CONV_RELU | MMT_CONV_MAX)) ||
-        (!c.x_max && !(c.x_scale > 0)))
+    if (!c.x || !c.w_hi || !c.w_lo || !c.y || !(c.w_scale > 0) ||
+        (c.flags & ~(MMT_CONV_RELU | MMT_CONV_MAX | MMT_CONV_POOL)) || (!c.x_max && !(c.x_scale > 0)) ||
+        (c.flags & MMT_CONV_POOL) != (groups[0].flags & MMT_CONV_POOL))
       return MMT_E_ARG;
     a.g[i] = ConvGroupArgs{c.x, c.w_hi, c.w_lo, c.bias, c.resid, c.y, c.x_max, c.y_max, c.x_scale, 1.0f / c.w_scale,
                            c.flags};
@@ -1197,6 +1412,17 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad;
   a.Ho = Ho; a.Wo = Wo; a.Kp = Kp;
   const int64_t M = (int64_t)N * Ho * Wo;
+  const hipStream_t s = (hipStream_t)stream;
+  if (groups[0].flags & MMT_CONV_POOL) {
+    // the 7 x 7 / stride-2 stem with the 3 x 3 / stride-2 / pad-1 max-pool fused; y is the pooled map
+    if (Cin != 4 || Cout != 64 || kh != 7 || kw != 7 || stride != 2 || Kp != 224 || (groups[0].flags & MMT_CONV_MAX))
+      return MMT_E_ARG;
+    const int PHo = (Ho - 1) / 2 + 1, PWo = (Wo - 1) / 2 + 1;
+    const unsigned tiles = (unsigned)(N * ((PHo + kPoolT - 1) / kPoolT) * ((PWo + kPoolT - 1) / kPoolT));
+    a.ks = 1;
+    hipLaunchKernelGGL(conv_stem_pool_f16x3_kernel, dim3(tiles, 1, G), dim3(512), 0, s, a, PHo, PWo);
+    return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+  }
   int ks = (int)conv_ks_for(N, H, W, Ho, Wo, Cin, Cout, kh, kw, stride, pad, Kp, G);
   if (ks > 1 && (!ws || ws_bytes < (size_t)(ks * G * M * (int64_t)Cout * 4))) ks = 1;
   a.ks = ks;
@@ -1205,7 +1431,6 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   const int conv_bm = conv_bm_for(Cin, bn);
   const unsigned gm = (unsigned)((M + conv_bm - 1) / conv_bm);
   const dim3 grid(gm, Cout / bn, G * ks);
-  const hipStream_t s = (hipStream_t)stream;
   // the stem on a 4-channel image: 2-D tiles from an LDS input patch (MMT_CONV_STEM_OLD: the gather kernel, tuning)
   static const bool stem_old = getenv("MMT_CONV_STEM_OLD") != nullptr;
   static const int stem_th = getenv("MMT_CONV_STEM_TH") ? atoi(getenv("MMT_CONV_STEM_TH")) : 16;   // tuning: 8

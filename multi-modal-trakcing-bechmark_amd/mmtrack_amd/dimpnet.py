@@ -52,6 +52,9 @@ def range_scale(m):
 
 
 MAX_WORDS = 64 * 32   # sharded max|y| words per tensor (mmt_conv_max_words)
+# f16x3: the stem writes the max-pooled map directly (MMT_CONV_POOL); MMT_DIMP_STEMPOOL=0 (tuning A/B): the stem map
+# and a separate max-pool launch
+STEM_POOL = os.environ.get("MMT_DIMP_STEMPOOL", "1") != "0"
 
 
 class _Conv:
@@ -93,9 +96,11 @@ class _Conv:
     def out_hw(self, H, W):
         return (H + 2 * self.pad - self.kh) // self.stride + 1, (W + 2 * self.pad - self.kw) // self.stride + 1
 
-    def group(self, x, out, relu=False, resid=None, merge_max=False, x_max=None, x_scale=0.0, y_max=None):
-        """This conv's operands as one mmt_conv_group of an f16x3 launch."""
-        flags = (1 if relu else 0) | (2 if merge_max else 0)
+    def group(self, x, out, relu=False, resid=None, merge_max=False, x_max=None, x_scale=0.0, y_max=None,
+              pool=False):
+        """This conv's operands as one mmt_conv_group of an f16x3 launch (pool: the stem with the 3 x 3 / stride-2
+        max-pool fused, MMT_CONV_POOL; out is then the pooled map)."""
+        flags = (1 if relu else 0) | (2 if merge_max else 0) | (8 if pool else 0)
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         return _lib.MmtConvGroup(x.data_ptr(), self.wh.data_ptr(), self.wl.data_ptr(), self.w_scale, ptr(self.b),
                                  ptr(resid), out.data_ptr(), ptr(x_max), float(x_scale), ptr(y_max), flags)
@@ -225,15 +230,19 @@ class DiMPNet:
         K = range(len(self.backbones))
         stems = [bb[0] for bb in self.backbones]
         h, w = stems[0].out_hw(H, W)
-        t0 = [self._buf(f"stem{k}", N * h * w * 64) for k in K]
         t0_max = [self._slot() for k in K]
         f16 = self.precision == "f16x3"   # f16x3: the images come padded to 4 channels
-        self._layer(stems, [dict(x=xs[k], out=t0[k], relu=True, x_scale=self.image_scale, y_max=t0_max[k])
-                            for k in K], N, H, W, s, cin=4 if f16 else None)
         H2, W2 = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
         cur = [self._buf(f"ping{k}", N * H2 * W2 * 256) for k in K]
-        for k in K:
-            _rc(lib.mmt_maxpool2d_f32(_p(t0[k]), N, h, w, 64, 3, 2, 1, _p(cur[k]), s), "mmt_maxpool2d_f32")
+        if f16 and STEM_POOL:   # the max-pool fused into the stem: the full-resolution map is never written
+            self._layer(stems, [dict(x=xs[k], out=cur[k], relu=True, x_scale=self.image_scale, y_max=t0_max[k],
+                                     pool=True) for k in K], N, H, W, s, cin=4)
+        else:
+            t0 = [self._buf(f"stem{k}", N * h * w * 64) for k in K]
+            self._layer(stems, [dict(x=xs[k], out=t0[k], relu=True, x_scale=self.image_scale, y_max=t0_max[k])
+                                for k in K], N, H, W, s, cin=4 if f16 else None)
+            for k in K:
+                _rc(lib.mmt_maxpool2d_f32(_p(t0[k]), N, h, w, 64, 3, 2, 1, _p(cur[k]), s), "mmt_maxpool2d_f32")
         cur_max = t0_max   # a max-pool never exceeds its input's maximum
         H, W = H2, W2
         nxt_name = "pong"

@@ -192,6 +192,54 @@ def test_conv2d_f16x3_stem_padded_input_bitwise():
     assert float(a4[..., 3].abs().max()) == 0.0 and float(b4[..., 3].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("N,H,W", [(3, 75, 61), (2, 288, 288), (1, 33, 50)])
+def test_conv2d_f16x3_stem_pool_bitwise(N, H, W):
+    """The stem with the 3 x 3 / stride-2 / pad-1 max-pool fused (MMT_CONV_POOL, conv_stem_pool_f16x3_kernel: 8 x 8
+    pooled tiles over 17 x 17 stem tiles) gives the bits of the stem kernel followed by mmt_maxpool2d_f32, for both
+    groups of a grouped launch, and the same max|y| (max over the sharded words); launches it does not cover are
+    refused."""
+    import ctypes
+    from mmtrack_amd import _lib, dimpnet
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(N * 1000 + H)
+    convs, xs = [], []
+    for k in range(2):
+        w = torch.randn(64, 3, 7, 7, generator=g) / math.sqrt(147)
+        b = torch.randn(64, generator=g) * 0.1
+        convs.append(dimpnet._Conv(w, bias=b, stride=2, pad=3, dev="cuda", f16x3=True))
+        x = torch.randn(N, 3, H, W, generator=g) * (1 + k)
+        xs.append(torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 1)).contiguous().cuda())
+    Ho, Wo = convs[0].out_hw(H, W)
+    PHo, PWo = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    MW = lib.mmt_conv_max_words()
+    words = torch.zeros(4, MW, device="cuda")
+    scale = dimpnet.range_scale(6.0)
+    full = [torch.empty(N, Ho, Wo, 64, device="cuda") for _ in range(2)]
+    ref = [torch.empty(N, PHo, PWo, 64, device="cuda") for _ in range(2)]
+    dimpnet.run_f16x3(lib, convs[0], [c.group(x, y, relu=True, x_scale=scale, y_max=words[k])
+                                      for k, (c, x, y) in enumerate(zip(convs, xs, full))], N, H, W, None, stream, cin=4)
+    for y, r in zip(full, ref):
+        assert lib.mmt_maxpool2d_f32(ctypes.c_void_p(y.data_ptr()), N, Ho, Wo, 64, 3, 2, 1, ctypes.c_void_p(r.data_ptr()),
+                                     stream) == 0
+    got = [torch.full((N, PHo, PWo, 64), float("nan"), device="cuda") for _ in range(2)]
+    dimpnet.run_f16x3(lib, convs[0], [c.group(x, y, relu=True, x_scale=scale, y_max=words[2 + k], pool=True)
+                                      for k, (c, x, y) in enumerate(zip(convs, xs, got))], N, H, W, None, stream, cin=4)
+    torch.cuda.synchronize()
+    for k in range(2):
+        assert torch.equal(got[k], ref[k]), f"group {k}: max |diff| {float((got[k] - ref[k]).abs().max())}"
+        assert float(words[2 + k].max()) == float(words[k].max()) == float(full[k].abs().max())
+    # refused: the pool with a MAX merge, on another conv shape, or set on one group only
+    gr = [c.group(x, y, relu=True, x_scale=scale, pool=True) for c, x, y in zip(convs, xs, got)]
+    bad = convs[0].group(xs[0], got[0], relu=True, merge_max=True, x_scale=scale, pool=True)
+    arr = (_lib.MmtConvGroup * 1)(bad)
+    assert lib.mmt_conv2d_f16x3_groups(arr, 1, N, H, W, 4, convs[0].kp, 64, 7, 7, 2, 3, None, 0, stream) == -1
+    arr = (_lib.MmtConvGroup * 2)(gr[0], convs[1].group(xs[1], got[1], relu=True, x_scale=scale))
+    assert lib.mmt_conv2d_f16x3_groups(arr, 2, N, H, W, 4, convs[0].kp, 64, 7, 7, 2, 3, None, 0, stream) == -1
+    arr = (_lib.MmtConvGroup * 1)(gr[0])
+    assert lib.mmt_conv2d_f16x3_groups(arr, 1, N, H, W, 4, convs[0].kp, 64, 7, 7, 1, 3, None, 0, stream) == -1
+
+
 def test_conv2d_stem_w4():
     """The 3-channel stem through MMT_CONV_W4 (weights padded to 4 channels per tap) and through the generic
     per-element path agree with torch and each other (summation orders differ: fp32 rounding)."""
