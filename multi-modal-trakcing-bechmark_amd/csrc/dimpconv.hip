@@ -831,6 +831,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
       asm volatile("s_waitcnt vmcnt(%4)" : "+v"(set.a[0]), "+v"(set.a[1]), "+v"(set.a[2]), "+v"(set.a[3])
                    : "n"(decltype(cnt)::value) : "memory");
   };
+  auto keep_set = [&](DeepRegs& set) {   // the set's registers live up to here (no code, no wait)
+    if constexpr (SL == 1)
+      asm volatile("" : "+v"(set.a[0]), "+v"(set.a[1]));
+    else
+      asm volatile("" : "+v"(set.a[0]), "+v"(set.a[1]), "+v"(set.a[2]), "+v"(set.a[3]));
+  };
   auto pack2 = [&](float x, float y, uint32_t& h, uint32_t& l) {
     uint16_t hx, lx, hy, ly;
     split_h(x * sa, hx, lx);
@@ -998,7 +1004,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
       sum_bar += tsl - tc;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the zero-loads past the slice, before the LDS is left
+  // the zero-loads past the slice land before the LDS is left -- and before their registers are reused: the last
+  // sets' loads are dead to the compiler, which would otherwise hand their registers to the epilogue while the
+  // loads are still in flight (the landing zeros then overwrite epilogue values), so every set is named live across
+  // the wait
+  wait_set(r[0], std::integral_constant<int, 0>{});
+#pragma unroll
+  for (int k = 1; k < NR; ++k) keep_set(r[k]);
 #if defined(CONV_STAMPS)
   if (threadIdx.x == 0 && g_conv_stamps) {
     const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
