@@ -1448,7 +1448,9 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   static const int stem_th = getenv("MMT_CONV_STEM_TH") ? atoi(getenv("MMT_CONV_STEM_TH")) : 16;   // tuning: 8
   static const bool conv_old = getenv("MMT_CONV_OLD") != nullptr;   // tuning: conv_f16x3_kernel (two-deep)
   static const int conv_nr = getenv("MMT_CONV_NR") ? atoi(getenv("MMT_CONV_NR")) : 2;   // tuning: 3
-  static const bool conv_ovl = getenv("MMT_CONV_OVL") != nullptr;   // tuning: split overlapped with the MFMAs
+  // the next K-tile's split woven into the MFMAs (+1 % on the mfDiMP line, tools/runs_r4/r4_run8.sh); MMT_CONV_OVL=0
+  // (tuning): the split after them
+  static const bool conv_ovl = !getenv("MMT_CONV_OVL") || atoi(getenv("MMT_CONV_OVL")) != 0;
   int tpi = 0;
   const int ppx = patch_plan(H, W, Cin, kh, kw, stride, pad, &tpi);
   if (ppx) {

@@ -78,18 +78,20 @@ def test_conv2d_f16x3_vs_fp64(N, C, H, W, Co, k, s, p):
 
 def test_conv_kernels_bitwise(tmp_path):
     """The f16x3 conv kernels against each other (tests/conv_dump.py, one child process per setting: the knobs are
-    read once per process): the deep-pipelined generic kernel (conv_f16x3_deep_kernel, three register sets / two
-    register sets) gives the bits of the two-deep conv_f16x3_kernel (same products, same summation order), with and
-    without split-K; the 3 x 3 patch kernel (another summation order) agrees with them within 1e-5 of the output
-    scale."""
+    read once per process): the deep-pipelined generic kernel (conv_f16x3_deep_kernel: three or two register sets,
+    the default three-set kernel with the next K-tile's split woven into the MFMAs, 256-pixel tiles) gives the bits
+    of the two-deep conv_f16x3_kernel (same products, same summation order) -- split-K launches too, except where
+    256-pixel tiles pick another K split (within 1e-5 then); the 3 x 3 patch kernel (another summation order)
+    agrees with them within 1e-5 of the output scale."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
     for mode, extra in (("old", {"MMT_CONV_OLD": "1", "MMT_CONV_NOPATCH": "1"}),
-                        ("deep3", {"MMT_CONV_NR": "3", "MMT_CONV_NOPATCH": "1"}), ("deep2", {"MMT_CONV_NOPATCH": "1"}),
+                        ("deep3", {"MMT_CONV_NR": "3", "MMT_CONV_OVL": "0", "MMT_CONV_NOPATCH": "1"}),
+                        ("deep2", {"MMT_CONV_OVL": "0", "MMT_CONV_NOPATCH": "1"}),
                         ("bm256", {"MMT_CONV_BM": "256", "MMT_CONV_NOPATCH": "1"}),
-                        ("ovl", {"MMT_CONV_OVL": "1", "MMT_CONV_NOPATCH": "1"}), ("patch", {})):
+                        ("ovl", {"MMT_CONV_NOPATCH": "1"}), ("patch", {})):
         env = {k: v for k, v in os.environ.items() if not k.startswith("MMT_CONV_")}
         env.update(extra)
         path = str(tmp_path / f"{mode}.npz")
