@@ -13,5 +13,5 @@ OUT=$O/pmc bash tools/pmc_bench.sh || exit 1
 python tools/pmc_traffic.py $O/pmc $O/r04_pmc_traffic_fp32_b32.json > $O/pmc_traffic.txt 2>&1 || exit 1
 head -12 $O/pmc_traffic.txt
 OUT=$O/pmc_dimp DEST=$O/r04_pmc_traffic_dimp.json bash tools/pmc_dimp_traffic.sh || exit 1
-rm -rf $O/pmc/fetch $O/pmc/write $O/pmc/l2 $O/pmc_dimp/fetch $O/pmc_dimp/write
+rm -rf $O/pmc/fetch $O/pmc/write $O/pmc/l2
 for d in prof32 prof32_halves_off prof1 profdimp; do head -14 $O/$d/summary.txt; done
