@@ -432,10 +432,14 @@ def dimp_main(args, rank, world, dist):
     achieved = flops / (feat_ms * 1e-3) / 1e12
     f16 = args.dimp_precision == "f16x3"
     peak = PEAK_BF16_TFLOPS / 3 if f16 else PEAK_FP32_MATRIX_TFLOPS
-    roof = {"bound": "mfma", "kernel": ("conv_f16x3_kernel" if f16 else "conv_f32_kernel") +
+    tr = dimp_traffic(B) if f16 else None
+    roof = {"bound": "mfma", "kernel": ("f16x3 convs: conv_f16x3_deep_kernel, conv3x3_patch_f16x3_kernel, "
+                                        "conv_stem_pool_f16x3_kernel" if f16 else "conv_f32_kernel") +
             " (2 x ResNet-50 to layer3 + clf conv, per batch)",
             "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": dimp_traffic(B),
+            "frac": round(achieved / peak, 4), "traffic": round(tr["bytes"]) if tr else None,
+            "traffic_unit": "bytes per 32-image feature-net batch (FETCH_SIZE x2 + WRITE_SIZE, PMC)",
+            "traffic_detail": tr,
             "flop_per_launch_group": flops, "avg_batch_ms": round(feat_ms, 4),
             # the feature net is partly HBM-bound (fp32 activations, 1x1 convs of K = 64..256): its per-layer
             # roofline (sum over layers of max(FLOPs / peak, min bytes / 8 TB/s)) and the fraction of it reached
