@@ -62,6 +62,7 @@ struct ConvF16Args {
   ConvGroupArgs g[kMaxGroups];
   float* part;                    // split-K partials [ks][G][M][Cout] (ks > 1)
   int N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, Kp, ks;
+  int xcd_order;                  // conv_f16x3_deep_kernel: XCD-aware tile order (else M tiles fastest)
 };
 
 __device__ __forceinline__ int cswz(int r, int c) { return r * 32 + ((c ^ ((r >> 2) & 2)) << 3); }   // gemm.hip swzk<32>
@@ -739,7 +740,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
   const int grp = blockIdx.z / a.ks, slice = blockIdx.z - grp * a.ks;
   const ConvGroupArgs g = pick_group(a, grp);
   const int M = a.N * a.Ho * a.Wo;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // XCD-aware tile order (grid.x = M tiles x N tiles): the workgroups of XCD x (= b % 8) take a contiguous range of
+  // tile ids, N fastest, so the column-tile siblings of an activation tile run on one XCD and share its L2 (the
+  // activation tile is fetched from beyond the L2 once per XCD instead of once per column tile)
+  // (the default: mfDiMP 6 350 -> 6 394 frames/s in two rounds; applied only to wide outputs and short launches it
+  // measured level, although layer1 conv3 alone, without its residual, runs 128 -> 150 us in this order;
+  // MMT_CONV_XCD=0: M tiles fastest over the whole chip, profiles/r04_ab_conv_xcd_order.txt)
+  int m0, n0;
+  {
+    const int gn = a.Cout / BN, ntl = gridDim.x, b = blockIdx.x;
+    if (a.xcd_order) {
+      const int x = b & 7, j = b >> 3, q = ntl >> 3, r8 = ntl & 7;
+      const int id = (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + j;
+      m0 = (id / gn) * BM;
+      n0 = (id - (id / gn) * gn) * BN;
+    } else {
+      const int gm = ntl / gn;
+      m0 = (b % gm) * BM;
+      n0 = (b / gm) * BN;
+    }
+  }
 
   float sa = g.xscale;
   if (g.xmax) {
@@ -1443,6 +1463,9 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   const int conv_bm = conv_bm_for(Cin, bn);
   const unsigned gm = (unsigned)((M + conv_bm - 1) / conv_bm);
   const dim3 grid(gm, Cout / bn, G * ks);
+  const dim3 dgrid(gm * (Cout / bn), 1, G * ks);   // the deep kernel: M x N tiles flattened
+  static const int xcd_env = getenv("MMT_CONV_XCD") ? atoi(getenv("MMT_CONV_XCD")) : -1;   // tuning: 0 / 1 force
+  a.xcd_order = xcd_env != 0;
   // the stem on a 4-channel image: 2-D tiles from an LDS input patch (MMT_CONV_STEM_OLD: the gather kernel, tuning)
   static const bool stem_old = getenv("MMT_CONV_STEM_OLD") != nullptr;
   static const int stem_th = getenv("MMT_CONV_STEM_TH") ? atoi(getenv("MMT_CONV_STEM_TH")) : 16;   // tuning: 8
@@ -1475,34 +1498,34 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
     else
       hipLaunchKernelGGL((conv_f16x3_kernel<64, false>), grid, dim3(512), 0, s, a);
   } else if (conv_bm == 256) {
-    hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2, 256>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2, 256>), dgrid, dim3(512), 0, s, a);
   } else if (conv_ovl) {
     if (bn == 128)
-      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3, 128, true>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3, 128, true>), dgrid, dim3(512), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3, 128, true>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3, 128, true>), dgrid, dim3(512), 0, s, a);
   } else if (conv_nr == 2) {
     if (bn == 128)
-      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2>), dgrid, dim3(512), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 2>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 2>), dgrid, dim3(512), 0, s, a);
   } else {
     if (bn == 128)
-      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3>), dgrid, dim3(512), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3>), dgrid, dim3(512), 0, s, a);
   }
 #if defined(CONV_STAMPS)
   if (!ppx && !conv_old && Cin > 4 && conv_bm == 128) {   // the deep kernel ran: per-phase cycles averaged over its workgroups
-    const size_t nb = (size_t)grid.x * grid.y * grid.z;
+    const size_t nb = (size_t)dgrid.x * dgrid.y * dgrid.z;
     unsigned long long* buf = nullptr;
     if (hipMalloc(&buf, nb * 64) == hipSuccess) {
       hipMemsetAsync(buf, 0, nb * 64, s);
       hipMemcpyToSymbolAsync(HIP_SYMBOL(g_conv_stamps), &buf, sizeof(buf), 0, hipMemcpyHostToDevice, s);
       if (conv_ovl)
-        hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3, 128, true>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3, 128, true>), dgrid, dim3(512), 0, s, a);
       else if (conv_nr == 2)
-        hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 2>), dgrid, dim3(512), 0, s, a);
       hipStreamSynchronize(s);
       std::vector<unsigned long long> h(nb * 8);
       hipMemcpy(h.data(), buf, nb * 64, hipMemcpyDeviceToHost);
