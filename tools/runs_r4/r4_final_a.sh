@@ -2,7 +2,7 @@
 # Round-4 final measurements, part A: the GPU suite, smoke, and the bench lines (default ViT 32 sequences with its CPU
 # baseline, one sequence, OSTrack-384, mfDiMP with its CPU baseline)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r4_final
+O=gpurun_out/${FINAL_TAG:-r4_final}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/ > $O/gpu_suite.txt 2>&1 || { grep -E "FAIL|Error" $O/gpu_suite.txt | head -20; tail -3 $O/gpu_suite.txt; exit 1; }
 tail -2 $O/gpu_suite.txt
