@@ -40,10 +40,14 @@ __global__ __launch_bounds__(256) void dimp_maps_kernel(DimpMaps m) {
 // interleaved channels (c = wave + 4 k) of chunks of CC channels, every lane one output position; the 4
 // partial sums combine in a fixed order, the band's squares (mode 1 / 2) in position order into
 // partial[is][band].  ctl: sequence s skips (no output) when it >= ctl[s].num_iter or i >= n_samples.
-template <int FH, int FW>
+// STRIP (4 x 4 filters, <= 16 four-position strips per band, CC % 16 == 0): register-blocked -- lane (strip,
+// channel subgroup) keeps four adjacent positions' sums and reads each feature value once per 4 x 7 window row
+// (8-B reads) and its channel's 16 weights as four 16-B reads: 20 LDS reads per 64 FMAs instead of 32 per 16; the
+// 16 channel groups (c = group + 16 k) combine in group order.
+template <int FH, int FW, bool STRIP = false>
 __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   extern __shared__ float sm[];   // 2 x ([CC][rows][Wp] padded feature rows + [CC][T] weights)
-  __shared__ float red[4][64];
+  __shared__ float red[STRIP ? 16 : 4][64];
   if constexpr (FH > 0) {
     a.fh = FH;
     a.fw = FW;
@@ -97,6 +101,11 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   const int ly = slot / a.Wo, x = slot - ly * a.Wo;
   const bool pv = slot < nrow * a.Wo;
   float acc = 0.f;
+  // STRIP: lane = strip (ly_s, 4 sx) + 16 x channel subgroup; channel group cg = 4 g + subgroup
+  const int nsx = (a.Wo + 3) >> 2, st = t & 15, cg = 4 * g + ((t >> 4) & 3);
+  const int sly = st / nsx, sx0 = 4 * (st - sly * nsx);
+  const bool sv = STRIP && sly < nrow;
+  float sacc[4] = {0.f, 0.f, 0.f, 0.f};
   fetch(0);
   put(0);
   __syncthreads();
@@ -104,7 +113,37 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
     if (ch + 1 < nch) fetch(ch + 1);
     const float* sf = sm + (ch & 1) * stage;
     const float* sw = sf + fsz;
-    if (pv) {
+    if constexpr (STRIP) {
+      if (sv) {
+        for (int c = cg; c < CC; c += 16) {
+          const float4* wq = reinterpret_cast<const float4*>(sw + c * 16);
+          float wv[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 w4 = wq[q];
+            wv[4 * q] = w4.x;
+            wv[4 * q + 1] = w4.y;
+            wv[4 * q + 2] = w4.z;
+            wv[4 * q + 3] = w4.w;
+          }
+#pragma unroll
+          for (int ky = 0; ky < 4; ++ky) {
+            const float2* fr = reinterpret_cast<const float2*>(sf + c * plane + (sly + ky) * Wp + sx0);
+            float fv[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float2 f2 = fr[q];
+              fv[2 * q] = f2.x;
+              fv[2 * q + 1] = f2.y;
+            }
+#pragma unroll
+            for (int kx = 0; kx < 4; ++kx)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) sacc[e] += fv[e + kx] * wv[ky * 4 + kx];
+          }
+        }
+      }
+    } else if (pv) {
       for (int c = g; c < CC; c += 4) {
         const float* fp = sf + c * plane + ly * Wp + x;
         const float* wp = sw + c * T;
@@ -122,11 +161,24 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
     if (ch + 1 < nch) put((ch + 1) & 1);
     __syncthreads();
   }
-  red[g][slot] = acc;
+  if constexpr (STRIP) {
+    if (sv)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (sx0 + e < a.Wo) red[cg][sly * a.Wo + sx0 + e] = sacc[e];
+  } else {
+    red[g][slot] = acc;
+  }
   __syncthreads();
   float r2 = 0.f;
   if (g == 0 && pv) {
-    acc = ((red[0][slot] + red[1][slot]) + red[2][slot]) + red[3][slot];
+    if constexpr (STRIP) {
+      acc = red[0][slot];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) acc += red[k][slot];
+    } else {
+      acc = ((red[0][slot] + red[1][slot]) + red[2][slot]) + red[3][slot];
+    }
     const int npos = a.Ho * a.Wo;
     const int64_t o = (int64_t)is * npos + (y0 + ly) * a.Wo + x;
     if (a.mode == 0) {
@@ -402,7 +454,12 @@ void dimp_filter(const DimpFilter& a_, hipStream_t s) {
   a.CC = g.CC;
   const size_t lds = 2 * (size_t)g.filter_stage * sizeof(float);
   const dim3 grid(a.I * a.S, g.nbands);
-  if (a.fh == 4 && a.fw == 4)
+  static const bool strip_off = getenv("MMT_DIMP_NOSTRIP") != nullptr;   // tuning A/B: the 4-group kernel
+  const int nstrips = g.RB * ((g.Wo + 3) / 4);
+  if (a.fh == 4 && a.fw == 4 && !strip_off && nstrips <= 16 && g.CC % 16 == 0 && ((g.RB + 3) * (g.Wo + 3)) % 2 == 0 &&
+      (g.Wo + 3) % 2 == 0)
+    hipLaunchKernelGGL((dimp_filter_kernel<4, 4, true>), grid, dim3(256), lds, s, a);
+  else if (a.fh == 4 && a.fw == 4)
     hipLaunchKernelGGL((dimp_filter_kernel<4, 4>), grid, dim3(256), lds, s, a);
   else
     hipLaunchKernelGGL((dimp_filter_kernel<0, 0>), grid, dim3(256), lds, s, a);
