@@ -43,7 +43,9 @@ __global__ __launch_bounds__(256) void dimp_maps_kernel(DimpMaps m) {
 // STRIP (4 x 4 filters, <= 16 four-position strips per band, CC % 16 == 0): register-blocked -- lane (strip,
 // channel subgroup) keeps four adjacent positions' sums and reads each feature value once per 4 x 7 window row
 // (8-B reads) and its channel's 16 weights as four 16-B reads: 20 LDS reads per 64 FMAs instead of 32 per 16; the
-// 16 channel groups (c = group + 16 k) combine in group order.
+// 16 channel groups (c = group + 16 k) combine in group order.  Explicit fmaf: a `+=` of a product lets the backend
+// split some of them into a separately rounded multiply and add (it did, for packed pairs, in one build), so the bits
+// would depend on instruction selection.
 template <int FH, int FW, bool STRIP = false>
 __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   extern __shared__ float sm[];   // 2 x ([CC][rows][Wp] padded feature rows + [CC][T] weights)
@@ -79,8 +81,10 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
     }
     soff[k] = o;
   }
-  float rg[kDimpStage];
-  auto fetch = [&](int ch) {
+  // the STRIP kernel keeps two chunks in flight (registers ra / rb alternate; its multiply is short enough that one
+  // chunk's latency was the bound), the 4-group kernel one (ra)
+  float ra[kDimpStage], rb[kDimpStage];
+  auto fetch = [&](int ch, float (&rg)[kDimpStage]) {
     const float* fb = f + (int64_t)ch * CC * a.H * a.W;   // C % CC == 0 (dimp_geo)
     const float* wb = wsrc + ch * CC * T;
 #pragma unroll
@@ -89,7 +93,7 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
       rg[k] = soff[k] < 0 ? 0.f : (e < fsz ? fb : wb)[soff[k]];
     }
   };
-  auto put = [&](int buf) {
+  auto put = [&](int buf, const float (&rg)[kDimpStage]) {
     float* d = sm + buf * stage;
 #pragma unroll
     for (int k = 0; k < kDimpStage; ++k) {
@@ -106,15 +110,10 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   const int sly = st / nsx, sx0 = 4 * (st - sly * nsx);
   const bool sv = STRIP && sly < nrow;
   float sacc[4] = {0.f, 0.f, 0.f, 0.f};
-  fetch(0);
-  put(0);
-  __syncthreads();
-  for (int ch = 0; ch < nch; ++ch) {
-    if (ch + 1 < nch) fetch(ch + 1);
+  auto mult_strip = [&](int ch) {
     const float* sf = sm + (ch & 1) * stage;
     const float* sw = sf + fsz;
-    if constexpr (STRIP) {
-      if (sv) {
+    if (sv) {
         for (int c = cg; c < CC; c += 16) {
           const float4* wq = reinterpret_cast<const float4*>(sw + c * 16);
           float wv[16];
@@ -139,11 +138,36 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
 #pragma unroll
             for (int kx = 0; kx < 4; ++kx)
 #pragma unroll
-              for (int e = 0; e < 4; ++e) sacc[e] += fv[e + kx] * wv[ky * 4 + kx];
+              for (int e = 0; e < 4; ++e) sacc[e] = fmaf(fv[e + kx], wv[ky * 4 + kx], sacc[e]);   // fused always
           }
         }
-      }
-    } else if (pv) {
+    }
+  };
+  if constexpr (STRIP) {
+    fetch(0, ra);
+    if (nch > 1) fetch(1, rb);
+    put(0, ra);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ch += 2) {
+      if (ch + 2 < nch) fetch(ch + 2, ra);   // rb holds ch + 1
+      mult_strip(ch);
+      if (ch + 1 < nch) put((ch + 1) & 1, rb);
+      __syncthreads();
+      if (ch + 1 >= nch) break;
+      if (ch + 3 < nch) fetch(ch + 3, rb);   // ra holds ch + 2
+      mult_strip(ch + 1);
+      if (ch + 2 < nch) put((ch + 2) & 1, ra);
+      __syncthreads();
+    }
+  } else {
+  fetch(0, ra);
+  put(0, ra);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    if (ch + 1 < nch) fetch(ch + 1, ra);
+    const float* sf = sm + (ch & 1) * stage;
+    const float* sw = sf + fsz;
+    if (pv) {
       for (int c = g; c < CC; c += 4) {
         const float* fp = sf + c * plane + ly * Wp + x;
         const float* wp = sw + c * T;
@@ -158,8 +182,9 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
         }
       }
     }
-    if (ch + 1 < nch) put((ch + 1) & 1);
+    if (ch + 1 < nch) put((ch + 1) & 1, ra);
     __syncthreads();
+  }
   }
   if constexpr (STRIP) {
     if (sv)

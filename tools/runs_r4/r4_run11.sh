@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 run 11b: the register-blocked 4 x 4 DiMP filter kernel (STRIP) against the previous build (abx/libprev.so)
-# correlation dump comparison (not bitwise: another channel-group order), DiMP tests, mfDiMP line
+# Round-4 run 11c: the strip DiMP filter kernel with two chunks in flight against the strip kernel with one (abx/libprev.so)
+# correlation dump comparison (bitwise expected), DiMP tests, mfDiMP line
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/r4_run11
 mkdir -p $O
