@@ -2,13 +2,13 @@
 # Round-4 final measurements, part B: rocprofv3 kernel traces (32 sequences halves on / off, one sequence, mfDiMP)
 # and the PMC traffic passes (ViT fc2 classes, mfDiMP feature net), summaries for profiles/
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r4_final
+O=gpurun_out/${FINAL_TAG:-r4_final}
 mkdir -p $O
-TAG=r4_final/prof32 STEPS=25 ARGS="--batch 32" bash tools/prof_bench.sh || exit 1
-MMT_OVERLAP_MIN=0 TAG=r4_final/prof32_halves_off STEPS=25 ARGS="--batch 32" bash tools/prof_bench.sh || exit 1
+TAG=${FINAL_TAG:-r4_final}/prof32 STEPS=25 ARGS="--batch 32" bash tools/prof_bench.sh || exit 1
+MMT_OVERLAP_MIN=0 TAG=${FINAL_TAG:-r4_final}/prof32_halves_off STEPS=25 ARGS="--batch 32" bash tools/prof_bench.sh || exit 1
 python tools/prof_split_resid.py $(find $O/prof32_halves_off -name '*kernel_trace.csv' | head -1) >> $O/prof32_halves_off/summary.txt 2>&1 || true
-TAG=r4_final/prof1 STEPS=200 ARGS="--batch 1" bash tools/prof_bench.sh || exit 1
-TAG=r4_final/profdimp STEPS=20 ARGS="--workload mfdimp_rgbt --batch 32" bash tools/prof_bench.sh || exit 1
+TAG=${FINAL_TAG:-r4_final}/prof1 STEPS=200 ARGS="--batch 1" bash tools/prof_bench.sh || exit 1
+TAG=${FINAL_TAG:-r4_final}/profdimp STEPS=20 ARGS="--workload mfdimp_rgbt --batch 32" bash tools/prof_bench.sh || exit 1
 OUT=$O/pmc bash tools/pmc_bench.sh || exit 1
 python tools/pmc_traffic.py $O/pmc $O/r04_pmc_traffic_fp32_b32.json > $O/pmc_traffic.txt 2>&1 || exit 1
 head -12 $O/pmc_traffic.txt
