@@ -46,7 +46,9 @@ __global__ __launch_bounds__(256) void dimp_maps_kernel(DimpMaps m) {
 // 16 channel groups (c = group + 16 k) combine in group order.  Explicit fmaf: a `+=` of a product lets the backend
 // split some of them into a separately rounded multiply and add (it did, for packed pairs, in one build), so the bits
 // would depend on instruction selection.
-template <int FH, int FW, bool STRIP = false>
+// STG: staged floats per thread and chunk (kDimpStage; 10 for the STRIP kernel's 16-channel chunks, its default:
+// 72 -> 30 staging / offset registers, four workgroups per CU)
+template <int FH, int FW, bool STRIP = false, int STG = kDimpStage>
 __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   extern __shared__ float sm[];   // 2 x ([CC][rows][Wp] padded feature rows + [CC][T] weights)
   __shared__ float red[STRIP ? 16 : 4][64];
@@ -67,9 +69,9 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   const int t = threadIdx.x;
   // each staged element's source offset within its chunk (fixed over the chunks; -1: a zero pad tap), so a
   // chunk's fetch is one add and one load per register
-  int soff[kDimpStage];
+  int soff[STG];
 #pragma unroll
-  for (int k = 0; k < kDimpStage; ++k) {
+  for (int k = 0; k < STG; ++k) {
     const int e = t + k * 256;
     int o = -1;
     if (e < fsz) {
@@ -83,20 +85,20 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
   }
   // the STRIP kernel keeps two chunks in flight (registers ra / rb alternate; its multiply is short enough that one
   // chunk's latency was the bound), the 4-group kernel one (ra)
-  float ra[kDimpStage], rb[kDimpStage];
-  auto fetch = [&](int ch, float (&rg)[kDimpStage]) {
+  float ra[STG], rb[STG];
+  auto fetch = [&](int ch, float (&rg)[STG]) {
     const float* fb = f + (int64_t)ch * CC * a.H * a.W;   // C % CC == 0 (dimp_geo)
     const float* wb = wsrc + ch * CC * T;
 #pragma unroll
-    for (int k = 0; k < kDimpStage; ++k) {
+    for (int k = 0; k < STG; ++k) {
       const int e = t + k * 256;
       rg[k] = soff[k] < 0 ? 0.f : (e < fsz ? fb : wb)[soff[k]];
     }
   };
-  auto put = [&](int buf, const float (&rg)[kDimpStage]) {
+  auto put = [&](int buf, const float (&rg)[STG]) {
     float* d = sm + buf * stage;
 #pragma unroll
-    for (int k = 0; k < kDimpStage; ++k) {
+    for (int k = 0; k < STG; ++k) {
       const int e = t + k * 256;
       if (e < stage) d[e] = rg[k];
     }
@@ -480,9 +482,17 @@ void dimp_filter(const DimpFilter& a_, hipStream_t s) {
   const size_t lds = 2 * (size_t)g.filter_stage * sizeof(float);
   const dim3 grid(a.I * a.S, g.nbands);
   static const bool strip_off = getenv("MMT_DIMP_NOSTRIP") != nullptr;   // tuning A/B: the 4-group kernel
+  // 16-channel chunks (one channel per lane and chunk; 108 VGPRs, four workgroups per CU): GN steps 50.5 -> 43.9 us,
+  // the per-frame scores 44.4 -> 37.4 us, mfDiMP +0.9 % (tools/runs_r4/r4_run14.sh); MMT_DIMP_STRIP_CC=32 (tuning)
+  static const int strip_cc = getenv("MMT_DIMP_STRIP_CC") ? atoi(getenv("MMT_DIMP_STRIP_CC")) : 16;
   const int nstrips = g.RB * ((g.Wo + 3) / 4);
-  if (a.fh == 4 && a.fw == 4 && !strip_off && nstrips <= 16 && g.CC % 16 == 0 && ((g.RB + 3) * (g.Wo + 3)) % 2 == 0 &&
-      (g.Wo + 3) % 2 == 0)
+  const int fplane = (g.RB + 3) * (g.Wo + 3);
+  const bool strip = a.fh == 4 && a.fw == 4 && !strip_off && nstrips <= 16 && g.CC % 16 == 0 && fplane % 2 == 0 &&
+                     (g.Wo + 3) % 2 == 0;
+  if (strip && strip_cc == 16 && 16 * (fplane + 16) <= 10 * 256) {
+    a.CC = 16;
+    hipLaunchKernelGGL((dimp_filter_kernel<4, 4, true, 10>), grid, dim3(256), 2 * (size_t)16 * (fplane + 16) * 4, s, a);
+  } else if (strip)
     hipLaunchKernelGGL((dimp_filter_kernel<4, 4, true>), grid, dim3(256), lds, s, a);
   else if (a.fh == 4 && a.fw == 4)
     hipLaunchKernelGGL((dimp_filter_kernel<4, 4>), grid, dim3(256), lds, s, a);
