@@ -101,6 +101,53 @@ __device__ __forceinline__ f32x4 conv_out(const ConvGroupArgs& g, f32x4 v, int64
   return v;
 }
 
+// a wave's FM x FN output fragments (rows mo[i] where mv[i], columns nb + 16 j .. + 3) through conv_out's arithmetic
+// in its order, the operands requested together before any is used (the FN bias groups, every fragment's residual)
+// through raw buffer loads -- an absent operand is a zero-sized buffer, a row past the map an out-of-range offset, both
+// read zeros -- so the FM x FN residual round trips overlap instead of each waiting in place (the K loop's registers
+// are dead by now: no register cost); returns the lane's max |y|.  rows = the launch's output rows (M)
+template <int FM, int FN>
+__device__ __forceinline__ float conv_store_tile(const ConvGroupArgs& g, const f32x4 (&acc)[FM][FN], float inv,
+                                                 const int64_t (&mo)[FM], const bool (&mv)[FM], int nb, int Cout,
+                                                 int64_t rows) {
+  const rsrc_t rR = make_rsrc(g.resid, g.resid ? rows * Cout * 4 : 0);
+  const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)Cout * 4 : 0);
+  f32x4 bv[FN], rv[FM][FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+    bv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, (uint32_t)((nb + 16 * j) * 4), 0, 0));
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const uint32_t vo = mv[i] ? (uint32_t)((mo[i] * Cout + nb + 16 * j) * 4) : kBufOob;
+      rv[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rR, vo, 0, 0));
+    }
+  float ymx = 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    if (!mv[i]) continue;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      f32x4 v = acc[i][j] * inv;
+      if (g.bias) v += bv[j];
+      if (g.resid) v += rv[i][j];
+      if (g.flags & MMT_CONV_RELU)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      float4* dst = reinterpret_cast<float4*>(g.y + mo[i] * Cout + nb + 16 * j);
+      if (g.flags & MMT_CONV_MAX) {
+        const float4 o = *dst;   // torch.max(color, depth) (dimpnet.py:103)
+        v = f32x4{fmaxf(o.x, v[0]), fmaxf(o.y, v[1]), fmaxf(o.z, v[2]), fmaxf(o.w, v[3])};
+      }
+      *dst = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
+    }
+  }
+  return ymx;
+}
+
 // the workgroup's max|y| into shard word blockIdx-derived: one agent-scope atomic max per workgroup (a per-wave
 // atomic put ~1 300 atomics on each of the 64 words for the stem's 10 368 workgroups); every thread calls it
 template <int NWAVES>
@@ -1059,19 +1106,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
     }
     return;
   }
-  float ymx = 0.f;
+  int64_t mo[FM];
+  bool mv[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int mo = m0 + wm * (BM / 4) + i * 16 + li;
-    if (mo >= M) continue;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int no = n0 + wn * WN + j * 16 + 4 * lk;
-      const f32x4 v = conv_out(g, acc[i][j] * inv, mo, no, a.Cout);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
-    }
+    mo[i] = m0 + wm * (BM / 4) + i * 16 + li;
+    mv[i] = mo[i] < M;
   }
+  const float ymx = conv_store_tile<FM, FN>(g, acc, inv, mo, mv, n0 + wn * WN + 4 * lk, a.Cout, M);
   if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.y * 7 + blockIdx.z * 13, reinterpret_cast<float*>(&sA[0][0][0]));
 }
 
@@ -1273,20 +1315,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     }
     return;
   }
-  float ymx = 0.f;
+  int64_t mo[FM];
+  bool mv[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int o = o0 + wm * 32 + i * 16 + li;
-    if (o >= o_end) continue;
-    const int64_t mo = (int64_t)img * HW + o;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int no = n0 + wn * WN + j * 16 + 4 * lk;
-      const f32x4 v = conv_out(g, acc[i][j] * inv, mo, no, a.Cout);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
-    }
+    mo[i] = (int64_t)img * HW + o;
+    mv[i] = o < o_end;
   }
+  const float ymx = conv_store_tile<FM, FN>(g, acc, inv, mo, mv, n0 + wn * WN + 4 * lk, a.Cout, (int64_t)a.N * HW);
   __syncthreads();   // the LDS is free for the max fold
   if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.y * 7 + blockIdx.z * 13, reinterpret_cast<float*>(dynlds));
 }

@@ -1,7 +1,8 @@
 """ISA audit for kernels that issue inline-asm vector loads (the compiler neither counts nor waits for them): along
 the text of each kernel, model the in-order vector-memory queue (every buffer / global load and store joins it; an
 `s_waitcnt vmcnt(k)` retires all but the k youngest) and report any instruction other than a load that reads or
-writes a VGPR an outstanding load still has to write.  Straight-line model: branches are followed in text order,
+writes a VGPR an outstanding inline-asm load (between ;;#ASMSTART / ;;#ASMEND) still has to write -- the compiler
+waits for its own loads itself.  Straight-line model: branches are followed in text order,
 which is what the unrolled K loops of these kernels are.
 
 usage: isa_audit.py file.s [kernel-substring ...]   (exit 1 on a finding)"""
@@ -21,8 +22,12 @@ def audit(asm_text, kernel):
     """Findings (line, instruction, registers) for one kernel's symbol in an assembly listing."""
     i = asm_text.index(kernel + ":")
     body = [ln.strip() for ln in asm_text[i:asm_text.index(".Lfunc_end", i)].split("\n")]
-    queue, found = [], []
+    queue, found, in_asm = [], [], False
     for n, ln in enumerate(body):
+        if ln.startswith(";;#ASMSTART"):
+            in_asm = True
+        elif ln.startswith(";;#ASMEND"):
+            in_asm = False
         if not ln or ln.startswith((";", ".")):
             continue
         op = ln.split()[0]
@@ -37,8 +42,8 @@ def audit(asm_text, kernel):
         is_load = op.startswith(("buffer_load", "global_load"))
         if used & pending and not is_load:
             found.append((n, ln, sorted(used & pending)))
-        if is_load:
-            queue.append((n, set() if " lds" in ln else _regs(ops[0])))
+        if is_load:   # only inline-asm loads are untracked by the compiler; its own loads it waits for itself
+            queue.append((n, _regs(ops[0]) if in_asm and " lds" not in ln else set()))
         elif op.startswith(("buffer_store", "global_store", "global_atomic", "buffer_atomic")):
             queue.append((n, set()))
     return found
