@@ -239,7 +239,10 @@ __global__ __launch_bounds__(256) void dimp_filter_kernel(DimpFilter a) {
 // (sequence, CT channels), looping over the samples i < I (ctl: < n_samples; the sequence skips when it >=
 // num_iter): the sample's padded planes of the CT channels and its residual map are staged double-buffered;
 // G = 256 / (CT T) threads per (channel, tap) take interleaved positions, combined in a fixed order.
-template <int FH, int FW>
+// STRIP (4 x 4, even padded row pitch): each lane takes four-position strips of its channel -- four residuals and a
+// 4 x 8 window read once (8-B reads) feed 64 FMAs (explicit fmaf), instead of 17 LDS reads per 16 FMAs; the PG lanes
+// of a channel combine in lane order.  Buffers start on 16-B boundaries (stage rounded up to 4 floats).
+template <int FH, int FW, bool STRIP = false>
 __global__ __launch_bounds__(256) void dimp_transpose_kernel(DimpTranspose a) {
   extern __shared__ float sm[];   // 2 x ([CT][Hp][Wp] padded planes + [npos] residuals)
   __shared__ float red[256];
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(256) void dimp_transpose_kernel(DimpTranspose a) {
   const int nI = a.ctl ? min(a.I, a.ctl[s].n_samples) : a.I;
   const int T = a.fh * a.fw, P0 = a.fh / 2, P1 = a.fw / 2, npos = a.Ho * a.Wo;
   const int Wp = a.Wo + a.fw - 1, plane = (a.Ho + a.fh - 1) * Wp, CT = a.CT;
-  const int fsz = CT * plane, stage = fsz + npos;
+  const int fsz = CT * plane, stage = STRIP ? (fsz + npos + 3) & ~3 : fsz + npos;
   const int t = threadIdx.x;
   int soff[kDimpStage];   // as dimp_filter_kernel: fixed over the samples
 #pragma unroll
@@ -263,7 +266,7 @@ __global__ __launch_bounds__(256) void dimp_transpose_kernel(DimpTranspose a) {
       const int c = e / plane, r = e - c * plane, py = r / Wp, px = r - py * Wp;
       const int yy = py - P0, xx = px - P1;
       if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) o = (c0 + c) * a.H * a.W + yy * a.W + xx;
-    } else if (e < stage) {
+    } else if (e < fsz + npos) {   // the residual map (STRIP's rounding-up pad stays a zero)
       o = e - fsz;
     }
     soff[k] = o;
@@ -303,11 +306,36 @@ __global__ __launch_bounds__(256) void dimp_transpose_kernel(DimpTranspose a) {
     float accb[TT];
 #pragma unroll
     for (int k = 0; k < TT; ++k) accb[k] = 0.f;
+    const int nsx = (a.Wo + 3) >> 2, nstrips = a.Ho * nsx;
     for (int i = 0; i < nI; ++i) {
       if (i + 1 < nI) fetch(i + 1);
       const float* sf = sm + (i & 1) * stage;
       const float* sr = sf + fsz;
-      if (c < CT) {
+      if constexpr (STRIP) {
+        if (c < CT) {
+          for (int st = pg; st < nstrips; st += PG) {
+            const int y = st / nsx, x0 = 4 * (st - y * nsx);
+            float rv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rv[e] = x0 + e < a.Wo ? sr[y * a.Wo + x0 + e] : 0.f;
+#pragma unroll
+            for (int ky = 0; ky < 4; ++ky) {
+              const float2* fr = reinterpret_cast<const float2*>(sf + c * plane + (y + ky) * Wp + x0);
+              float fv[8];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float2 f2 = fr[q];
+                fv[2 * q] = f2.x;
+                fv[2 * q + 1] = f2.y;
+              }
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int kx = 0; kx < 4; ++kx) accb[ky * 4 + kx] = fmaf(rv[e], fv[e + kx], accb[ky * 4 + kx]);
+            }
+          }
+        }
+      } else if (c < CT) {
         int y = pg / a.Wo, x = pg - y * a.Wo;
         for (int p = pg; p < npos; p += PG) {
           const float rv = sr[p];
@@ -505,7 +533,12 @@ void dimp_transpose(const DimpTranspose& a_, hipStream_t s) {
   a.CT = g.CT;
   const size_t lds = 2 * (size_t)g.transpose_stage * sizeof(float);
   const dim3 grid(a.S, (a.C + g.CT - 1) / g.CT);
-  if (a.fh == 4 && a.fw == 4 && 2 * g.transpose_stage >= 256 * 16)   // the blocked form's group sums fit the staging
+  static const bool strip_off = getenv("MMT_DIMP_NOSTRIP") != nullptr;   // tuning A/B
+  const int stage4 = (g.transpose_stage + 3) & ~3;
+  if (a.fh == 4 && a.fw == 4 && !strip_off && (g.Wo + 3) % 2 == 0 && 256 % g.CT == 0 &&
+      2 * g.transpose_stage >= 256 * 16 && stage4 <= kDimpStage * 256)
+    hipLaunchKernelGGL((dimp_transpose_kernel<4, 4, true>), grid, dim3(256), 2 * (size_t)stage4 * sizeof(float), s, a);
+  else if (a.fh == 4 && a.fw == 4 && 2 * g.transpose_stage >= 256 * 16)   // the blocked form's group sums fit the staging
     hipLaunchKernelGGL((dimp_transpose_kernel<4, 4>), grid, dim3(256), lds, s, a);
   else
     hipLaunchKernelGGL((dimp_transpose_kernel<0, 0>), grid, dim3(256), lds, s, a);
