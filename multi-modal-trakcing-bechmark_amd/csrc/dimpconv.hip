@@ -1144,10 +1144,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   const int grp = blockIdx.z / a.ks, slice = blockIdx.z - grp * a.ks;
   const ConvGroupArgs g = pick_group(a, grp);
   const int HW = a.Ho * a.Wo, Wd = a.W, PW = a.W + 2;
-  const int img = blockIdx.x / tiles_per_img, tile = blockIdx.x - img * tiles_per_img;
-  const int o0 = tile * BM, o_end = min(o0 + BM, HW);
-  const int y_first = o0 / Wd;
-  const int npx = ((o_end - 1) / Wd - y_first + 3) * PW;   // patch pixels of this tile
+  // the tile: global output pixels [g0, gend) -- per image (tiles_per_img > 0: 128 raster pixels of one image) or
+  // over the flattened batch (tiles_per_img == 0: no partial tile at each image's end; a tile then spans at most two
+  // images, HW >= 128): segment A = image nA's output rows yA0.. (patch rows 0 .. rowsA - 1 with their halo rows),
+  // segment B = the next image's first rows (patch rows rowsA .., its own halo above and below)
+  int g0, gend, nA, yA0, rowsA, rowsB = 0;
+  if (tiles_per_img > 0) {
+    const int img = blockIdx.x / tiles_per_img, o0 = (blockIdx.x - img * tiles_per_img) * BM;
+    g0 = img * HW + o0;
+    gend = img * HW + min(o0 + BM, HW);
+  } else {
+    g0 = blockIdx.x * BM;
+    gend = min(g0 + BM, a.N * HW);
+  }
+  nA = g0 / HW;
+  yA0 = (g0 - nA * HW) / Wd;
+  rowsA = (min(gend, (nA + 1) * HW) - nA * HW - 1) / Wd - yA0 + 3;
+  if (gend > (nA + 1) * HW) rowsB = (gend - (nA + 1) * HW - 1) / Wd + 3;
+  const int npx = (rowsA + rowsB) * PW;   // patch pixels of this tile
   const int n0 = blockIdx.y * BN;
 
   float sa = g.xscale;
@@ -1168,9 +1182,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     for (int j = 0; j < kPatchNPL; ++j) {
       const int f = t + 512 * j, px = f >> 3, part = f & 7;
       const int pr = px / PW, pc = px - pr * PW;
-      const int iy = y_first - 1 + pr, ix = pc - 1;
+      const bool segb = pr >= rowsA;
+      const int im = segb ? nA + 1 : nA, iy = segb ? pr - rowsA - 1 : yA0 - 1 + pr, ix = pc - 1;
       const bool ok = px < npx && iy >= 0 && iy < a.H && ix >= 0 && ix < Wd;
-      const uint32_t vo = ok ? (uint32_t)((((img * a.H + iy) * Wd + ix) * a.Cin + c * BK + 4 * part) * 4) : kBufOob;
+      const uint32_t vo = ok ? (uint32_t)((((im * a.H + iy) * Wd + ix) * a.Cin + c * BK + 4 * part) * 4) : kBufOob;
       pv[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rX, vo, 0, 0));
     }
   };
@@ -1213,14 +1228,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     }
   };
 
-  // this lane's fragment rows: patch pixel of tap (0, 0) for output pixel o0 + 32 wm + 16 i + (lane & 15) (rows past
+  // this lane's fragment rows: patch pixel of tap (0, 0) for output pixel g0 + 32 wm + 16 i + (lane & 15) (rows past
   // the tile's end read the tile's last pixel; their outputs are dropped)
   int pbase[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int o = min(o0 + wm * 32 + i * 16 + (lane & 15), o_end - 1);
-    const int y = o / Wd, x = o - y * Wd;
-    pbase[i] = (y - y_first) * PW + x;
+    const int o = min(g0 + wm * 32 + i * 16 + (lane & 15), gend - 1);
+    const int n = o / HW, r = o - n * HW, y = r / Wd, x = r - y * Wd;
+    pbase[i] = (n == nA ? y - yA0 : rowsA + y) * PW + x;
   }
   const int q = lane >> 4;
 
@@ -1303,9 +1318,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     float* pb = a.part + ((int64_t)slice * G + grp) * M * a.Cout;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int o = o0 + wm * 32 + i * 16 + li;
-      if (o >= o_end) continue;
-      const int64_t mo = (int64_t)img * HW + o;
+      const int64_t mo = g0 + wm * 32 + i * 16 + li;
+      if (mo >= gend) continue;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int no = n0 + wn * WN + j * 16 + 4 * lk;
@@ -1319,9 +1333,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   bool mv[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int o = o0 + wm * 32 + i * 16 + li;
-    mo[i] = (int64_t)img * HW + o;
-    mv[i] = o < o_end;
+    mo[i] = g0 + wm * 32 + i * 16 + li;
+    mv[i] = mo[i] < gend;
   }
   const float ymx = conv_store_tile<FM, FN>(g, acc, inv, mo, mv, n0 + wn * WN + 4 * lk, a.Cout, (int64_t)a.N * HW);
   __syncthreads();   // the LDS is free for the max fold
@@ -1409,19 +1422,40 @@ int conv_bn(int64_t gm, int Cin, int Cout, int G) {
   return 128;
 }
 
-// the 3 x 3 / stride-1 patch kernel's geometry: tiles per image (128 raster pixels each) and the largest tile's
-// patch (pixels); 0 when the shape is not one it runs
-int patch_plan(int H, int W, int Cin, int kh, int kw, int stride, int pad, int* tiles_per_img) {
+// the 3 x 3 / stride-1 patch kernel's geometry: *tiles = the launch's tiles, *tiles_per_img = tiles per image (128
+// raster pixels each) or 0 for tiles over the flattened batch (chosen when the images' partial last tiles would waste
+// more than 4 % of the rows and every batch tile's patch fits -- HW >= 128, so a tile spans at most two images);
+// returns the largest tile's patch (pixels), 0 when the shape is not one it runs
+int patch_plan(int N, int H, int W, int Cin, int kh, int kw, int stride, int pad, int* tiles, int* tiles_per_img) {
   static const bool off = getenv("MMT_CONV_NOPATCH") != nullptr;   // tuning A/B: the generic kernel
+  static const bool per_img = getenv("MMT_CONV_PATCH_PERIMG") != nullptr;   // tuning A/B: per-image tiles only
   if (off || kh != 3 || kw != 3 || stride != 1 || pad != 1 || Cin % 32 || Cin < 32) return 0;
-  const int HW = H * W, tiles = (HW + 127) / 128;
+  const int HW = H * W, tpi = (HW + 127) / 128, PW = W + 2;
   int px = 0;
-  for (int tl = 0; tl < tiles; ++tl) {
+  for (int tl = 0; tl < tpi; ++tl) {
     const int o0 = tl * 128, o1 = std::min(o0 + 128, HW);
-    px = std::max(px, ((o1 - 1) / W - o0 / W + 3) * (W + 2));
+    px = std::max(px, ((o1 - 1) / W - o0 / W + 3) * PW);
+  }
+  const int64_t total = (int64_t)N * HW, gtiles = (total + 127) / 128;
+  if (!per_img && HW >= 128 && (int64_t)N * tpi * 128 > total * 104 / 100 && N > 1) {
+    int gpx = 0;
+    for (int64_t tl = 0; tl < gtiles; ++tl) {
+      const int64_t g0 = tl * 128, gend = std::min(g0 + 128, total);
+      const int64_t nA = g0 / HW, y0 = (g0 - nA * HW) / W;
+      const int64_t aend = std::min(gend, (nA + 1) * HW) - nA * HW;
+      int rows = (int)((aend - 1) / W - y0 + 3);
+      if (gend > (nA + 1) * HW) rows += (int)((gend - (nA + 1) * HW - 1) / W + 3);
+      gpx = std::max(gpx, rows * PW);
+    }
+    if (gpx <= kPatchMaxPx) {
+      *tiles = (int)gtiles;
+      *tiles_per_img = 0;
+      return gpx;
+    }
   }
   if (px > kPatchMaxPx) return 0;
-  *tiles_per_img = tiles;
+  *tiles = N * tpi;
+  *tiles_per_img = tpi;
   return px;
 }
 
@@ -1437,9 +1471,9 @@ int64_t conv_ks_for(int N, int H, int W, int Ho, int Wo, int Cin, int Cout, int 
                     int G) {
   const int64_t M = (int64_t)N * Ho * Wo;
   const int bn = conv_bn((M + 127) / 128, Cin, Cout, G);
-  int tpi = 0;
-  if (patch_plan(H, W, Cin, kh, kw, stride, pad, &tpi))
-    return std::min<int64_t>(conv_pick_ks((int64_t)N * tpi * (Cout / bn) * G, Kp / 32), Cin / 32);
+  int ptiles = 0, tpi = 0;
+  if (patch_plan(N, H, W, Cin, kh, kw, stride, pad, &ptiles, &tpi))
+    return std::min<int64_t>(conv_pick_ks((int64_t)ptiles * (Cout / bn) * G, Kp / 32), Cin / 32);
   const int bm = conv_bm_for(Cin, bn);
   return conv_pick_ks((M + bm - 1) / bm * (Cout / bn) * G, Kp / 32);
 }
@@ -1511,10 +1545,10 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   // the next K-tile's split woven into the MFMAs (+1 % on the mfDiMP line, tools/runs_r4/r4_run8.sh); MMT_CONV_OVL=0
   // (tuning): the split after them
   static const bool conv_ovl = !getenv("MMT_CONV_OVL") || atoi(getenv("MMT_CONV_OVL")) != 0;
-  int tpi = 0;
-  const int ppx = patch_plan(H, W, Cin, kh, kw, stride, pad, &tpi);
+  int ptiles = 0, tpi = 0;
+  const int ppx = patch_plan(N, H, W, Cin, kh, kw, stride, pad, &ptiles, &tpi);
   if (ppx) {
-    const dim3 pgrid((unsigned)(N * tpi), Cout / bn, G * ks);
+    const dim3 pgrid((unsigned)ptiles, Cout / bn, G * ks);
     const size_t lds = (size_t)(2 * kPatchMaxPx * 32 + 2 * 2 * bn * 32) * 2;   // 80 KB (BN 128): two per CU
     if (bn == 128)
       hipLaunchKernelGGL(conv3x3_patch_f16x3_kernel<128>, pgrid, dim3(512), lds, s, a, tpi, ppx);
