@@ -110,6 +110,20 @@ template <int FM, int FN>
 __device__ __forceinline__ float conv_store_tile(const ConvGroupArgs& g, const f32x4 (&acc)[FM][FN], float inv,
                                                  const int64_t (&mo)[FM], const bool (&mv)[FM], int nb, int Cout,
                                                  int64_t rows) {
+  if (rows * Cout * 4 >= ((int64_t)1 << 31)) {   // past a 32-bit buffer offset: conv_out's plain loads
+    float ymx = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (!mv[i]) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const f32x4 v = conv_out(g, acc[i][j] * inv, mo[i], nb + 16 * j, Cout);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
+      }
+    }
+    return ymx;
+  }
   const rsrc_t rR = make_rsrc(g.resid, g.resid ? rows * Cout * 4 : 0);
   const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)Cout * 4 : 0);
   f32x4 bv[FN], rv[FM][FN];
