@@ -1387,11 +1387,14 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvF16Ar
 // slices), at least 8 K-tiles per slice.  256 slots (one workgroup per CU) measured +1 % over 512 and level
 // with no split at all once the two backbones share a launch (profiles/r03_ab_conv_slots.txt)
 int conv_pick_ks(int64_t tiles, int nk) {
-  // slots: 256 (one workgroup per CU); long-K layers (>= 72 K-tiles: layer3's 3 x 3 convs, the 3 x 3 clf conv
-  // over 1 024 channels) count two per CU -- the clf conv 466 -> 410 us, layer3 conv2 117 -> 113 us, while the
-  // short-K layers lose with it (layer3 conv1 58 -> 70 us; tests/bench_conv_f16x3.py, r3_run30.sh)
+  // slots: 256 (one workgroup per CU): a launch with a workgroup for every CU is not split.  (Round 3 counted the
+  // long-K layers -- >= 72 K-tiles: layer3's 3 x 3 convs and the clf conv -- two per CU, splitting them 4 ways at 32
+  // images; with the patch kernel's tiles over the flattened batch, 324 tiles, no split measured +0.3 % on the mfDiMP
+  // line and drops the 7 slice-reduce launches of a step, tools/runs_r4/r4_run19.sh.  Small batches still split.)
+  // The clf conv's K (288 K-tiles) is long enough that two slices per CU still pay: 512 slots from 144 K-tiles
+  // (unsplit 324 us against 254 + 14 us, r4_run20).
   static const int64_t kSlotsEnv = getenv("MMT_CONV_SLOTS") ? atoi(getenv("MMT_CONV_SLOTS")) : 0;   // tuning
-  const int64_t kSlots = kSlotsEnv > 0 ? kSlotsEnv : (nk >= 72 ? 512 : 256);
+  const int64_t kSlots = kSlotsEnv > 0 ? kSlotsEnv : (nk >= 144 ? 512 : 256);
   static const bool nosplit = getenv("MMT_CONV_NOSPLIT") != nullptr;   // batch-invariant summation order
   if (tiles >= kSlots || nosplit) return 1;
   int best = 1;

@@ -46,19 +46,19 @@ def test_conv_launch_plan_without_gpu():
     follow the output tiles -- the 3 x 3 stride-1 patch kernel tiles 18 x 18 maps over the flattened batch (32 images:
     81 tiles of 128 pixels instead of 96 per-image ones), the generic kernel's 1 x 1 layers fill the chip unsplit."""
     lib = _lib.load()
-    M = 32 * 18 * 18
 
     def slices(N, H, W, Cin, Cout, k, s, p, G):
         b = lib.mmt_conv2d_f16x3_ws_bytes(N, H, W, Cin, Cout, k, k, s, p, G)
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         return b // (G * N * Ho * Wo * Cout * 4) if b else 1
 
-    # layer3 conv2 (2 backbones): 81 tiles x 2 column tiles x 2 = 324 < 512 slots (72 K-tiles) -> 3 slices fill 972 of
-    # 2 x 512 (per-image tiles: 384 -> 4 slices)
-    assert slices(32, 18, 18, 256, 256, 3, 1, 1, 2) == 3
-    assert lib.mmt_conv2d_f16x3_ws_bytes(32, 18, 18, 256, 256, 3, 3, 1, 1, 2) == 3 * 2 * M * 256 * 4
-    # the clf conv (one group, 1 024 -> 512): 81 x 4 = 324 tiles -> 3 slices
+    # layer3 conv2 (2 backbones): 81 tiles x 2 column tiles x 2 = 324 >= 256 slots -> no split (per-image tiles would
+    # be 384); the clf conv (one group, 1 024 -> 512, 288 K-tiles: 512 slots): 81 x 4 = 324 -> 3 slices
+    assert lib.mmt_conv2d_f16x3_ws_bytes(32, 18, 18, 256, 256, 3, 3, 1, 1, 2) == 0
     assert slices(32, 18, 18, 1024, 512, 3, 1, 1, 1) == 3
+    # 4 images: 11 batch tiles (1 296 pixels) x 2 x 2 = 44 -> split K: 5 slices fill 220 of 256 slots
+    assert slices(4, 18, 18, 256, 256, 3, 1, 1, 2) == 5
+    assert lib.mmt_conv2d_f16x3_ws_bytes(4, 18, 18, 256, 256, 3, 3, 1, 1, 2) == 5 * 2 * 4 * 324 * 256 * 4
     # layer1 conv3 (1 x 1, 72 x 72): 1 296 x 2 x 2 tiles -- no split
     assert lib.mmt_conv2d_f16x3_ws_bytes(32, 72, 72, 64, 256, 1, 1, 1, 0, 2) == 0
     # one image: per-image tiles (3), few tiles -> split over the chunks (at most Cin / 32)
