@@ -124,7 +124,8 @@ def dimp_traffic(batch, path=None):
         return None
     d = json.load(open(files[-1]))
     return {"bytes": d["bytes_per_batch"], "algorithmic_bytes": d.get("algorithmic_bytes_per_batch"),
-            "ratio": d.get("ratio_to_algorithmic"), "source": os.path.relpath(files[-1], REPO)}
+            "ratio": d.get("ratio_to_algorithmic"), "source": os.path.relpath(files[-1], REPO),
+            "build": d.get("build"), "note": "committed PMC summary (tools/pmc_dimp_traffic.sh), not measured by this run"}
 
 
 def pmc_traffic(cls, precision, path=None):
@@ -140,6 +141,46 @@ def pmc_traffic(cls, precision, path=None):
     if not c or "traffic_bytes_per_dispatch" not in c:
         return None, None
     return c["traffic_bytes_per_dispatch"], os.path.relpath(files[-1], REPO) + ":" + cls
+
+
+# C3 per GPU (one sequence), C4 and C5 as short samples after nothing has touched the GPU: each in a fresh child
+# process (its own HIP context), so the default invocation's JSON line carries every single-GPU configuration of
+# BASELINE.json, timed under the driver's clock.  name -> extra argv
+EXTRAS = {
+    "vipt_deep_rgbt_b1": ["--workload", "vipt_deep_rgbt", "--batch", "1", "--steps", "300", "--warmup", "30"],
+    "ostrack384": ["--workload", "ostrack384", "--steps", "20", "--warmup", "5"],
+    "mfdimp_rgbt": ["--workload", DIMP_WORKLOAD, "--steps", "30", "--warmup", "10"],
+}
+
+
+def run_extras(timeout=150):
+    """The EXTRAS samples, one child process each (run before this process touches a GPU); per workload the
+    child's own JSON line reduced to its rate, step time and roofline fraction."""
+    out = {}
+    for name, argv in EXTRAS.items():
+        cmd = [sys.executable, os.path.abspath(__file__), "--no-extras", "--no-cpu-baseline", "--host-frames", "0"] + argv
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+            rc, text, err = r.returncode, r.stdout, r.stderr
+        except subprocess.TimeoutExpired:
+            rc, text, err = "timeout", "", ""
+        rec = {"rc": rc, "seconds": round(time.perf_counter() - t0, 1), "argv": " ".join(argv)}
+        lines = [ln for ln in text.splitlines() if ln.startswith("{")]
+        if rc == 0 and lines:
+            d = json.loads(lines[-1])
+            roof = d.get("roofline") or {}
+            rec.update({"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
+                        "warmup": d["warmup"], "sequences_per_gpu": d["config"]["sequences_per_gpu"],
+                        "dtype": d["dtype"], "frac": roof.get("frac"), "roofline_kernel": roof.get("kernel"),
+                        "roofline_achieved": roof.get("achieved"), "roofline_peak": roof.get("peak"),
+                        "frac_of_layer_roofline": roof.get("frac_of_layer_roofline"),
+                        "step_frac_of_peak": d.get("step_frac_of_peak"), "description": d["config"]["description"]})
+        else:
+            rec["stderr_tail"] = err[-600:]
+        log(f"bench extra {name}: {rec.get('value')} frames/s ({rec['seconds']} s, rc {rc})")
+        out[name] = rec
+    return out
 
 
 def free_port():
@@ -214,7 +255,10 @@ def roofline_from(classes, precision, workload, batch):
     return {"bound": "mfma", "kernel": dom, "achieved": c["achieved_tflops"], "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(c["achieved_tflops"] / peak, 4),
             "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (HBM, PMC)",
-            "traffic_source": src, "algorithmic_bytes_per_launch": c["algorithmic_bytes_per_launch"],
+            "traffic_source": src,
+            "traffic_note": ("from the committed PMC pass of this build (tools/pmc_bench.sh, FETCH_SIZE x2 + WRITE_SIZE, halves "
+                             "off as the probe runs), not measured by this run") if src else None,
+            "algorithmic_bytes_per_launch": c["algorithmic_bytes_per_launch"],
             "avg_launch_us": c["avg_launch_us"], "flop_per_launch": c["flop_per_launch"],
             "launches": c["launches"],
             "peak_note": ("f16x3 split products (Wh*Ah + Wl*Ah + Wh*Al, fp16 MFMA at the bf16 rate): dense 2500 TF/s / 3; achieved counts "
@@ -247,6 +291,8 @@ def main():
     ap.add_argument("--dimp-groups", type=int, default=1, help="mfdimp: PipelinedBatch groups of sequences")
     ap.add_argument("--dimp-precision", default="f16x3", choices=("f16x3", "fp32"),
                     help="mfdimp_rgbt: ResNet-50 convs on fp32-faithful f16x3 split products (default) or fp32 MFMA")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the one-sequence / OSTrack-384 / mfDiMP samples the default 1-GPU line carries")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -264,6 +310,10 @@ def main():
         args.batch = 32
     if args.dry:
         return dry_main(args, rank, world, dist)
+    extras = None
+    if (world == 1 and "WORLD_SIZE" not in os.environ and not args.no_extras and args.workload == "vipt_deep_rgbt"
+            and args.batch == 32 and args.precision == "fp32"):
+        extras = run_extras()   # children first: this process has not touched the GPU yet
     torch.cuda.set_device(local)
     if args.workload == DIMP_WORKLOAD:
         return dimp_main(args, rank, world, dist)
@@ -362,6 +412,8 @@ def main():
                                                                                          else 1)), 4),
             "cpu_baseline": cpu,
         }
+        if extras is not None:
+            line["extra_workloads"] = extras
         print(json.dumps(line), flush=True)
     eng.close()
     if dist:
@@ -437,9 +489,10 @@ def dimp_main(args, rank, world, dist):
                                         "conv_stem_pool_f16x3_kernel" if f16 else "conv_f32_kernel") +
             " (2 x ResNet-50 to layer3 + clf conv, per batch)",
             "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": round(tr["bytes"]) if tr else None,
+            "frac": round(achieved / peak, 4), "traffic": None,
+            # no PMC pass runs inside bench.py: the committed summary's figure, named as such
+            "traffic_committed": tr,
             "traffic_unit": "bytes per 32-image feature-net batch (FETCH_SIZE x2 + WRITE_SIZE, PMC)",
-            "traffic_detail": tr,
             "flop_per_launch_group": flops, "avg_batch_ms": round(feat_ms, 4),
             # the feature net is partly HBM-bound (fp32 activations, 1x1 convs of K = 64..256): its per-layer
             # roofline (sum over layers of max(FLOPs / peak, min bytes / 8 TB/s)) and the fraction of it reached

@@ -81,6 +81,12 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out);
 void mmt_destroy(mmt_engine* e);
 const char* mmt_last_error(const mmt_engine* e);
 const char* mmt_version(void);
+/* ABI revision of this header; a binding checks it once at load.  5: the strided DiMP optimiser is
+ * mmt_dimp_optimize_strided (-1 = contiguous stride, 0 = broadcast; the round-3 entry point
+ * mmt_dimp_optimize_dev, where 0 meant contiguous, is gone, so an old binding fails to resolve it
+ * instead of silently reading sample 0 everywhere). */
+#define MMT_ABI_VERSION 5
+int mmt_abi_version(void);
 
 /* weights: every reference state_dict key, fp32, row-major (load_state_dict(strict=True)) */
 int mmt_set_tensor(mmt_engine* e, const char* key, const float* data, const int64_t* shape, int ndim);
@@ -306,7 +312,7 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
  * of n sequences is: mmt_dimp_track_sample (patch geometry + sampling from the state) -> features ->
  * mmt_dimp_apply_filter -> mmt_dimp_track_update (get_sample_location, localize_advanced, update_state, memory
  * bookkeeping, the Gauss-Newton iteration choice; the frame's features into the chosen memory slot) -> the
- * host reads the n results (boxes, scores, flags, iterations) and runs mmt_dimp_optimize_dev for the
+ * host reads the n results (boxes, scores, flags, iterations) and runs mmt_dimp_optimize_strided for the
  * sequences that asked for steps.  Arrays of structs below are device memory.                          */
 #define MMT_DIMP_MEMORY 50
 typedef struct mmt_dimp_state {
@@ -351,7 +357,7 @@ int mmt_dimp_track_update(mmt_dimp_state* states, int n, const float* scores, in
  * of states / results / filters, memory [n][MMT_DIMP_MEMORY][C][H][W]) results[s].num_iter Gauss-Newton steps
  * over its first results[s].n_samples memory samples with its state's boxes and sample weights, in one
  * launch sequence of max_iter steps (a sequence with fewer, or none, skips the rest); bitwise the filter
- * mmt_dimp_optimize_dev gives over the same samples.  Nothing comes back to the host.                   */
+ * mmt_dimp_optimize_strided gives over the same samples.  Nothing comes back to the host.                   */
 size_t mmt_dimp_track_optimize_ws_bytes(int n, int C, int H, int W, int fh, int fw, int max_iter);
 int mmt_dimp_track_optimize(const mmt_dimp_state* states, int n, const mmt_dimp_result* results, const float* memory,
                             int C, int H, int W, float* filters, int fh, int fw, const mmt_dimp_params* p,
@@ -365,11 +371,11 @@ int mmt_dimp_track_optimize(const mmt_dimp_state* states, int n, const mmt_dimp_
  * target_boxes / sample_weights) are optimised in one call, their filters weights [S][C][fh][fw].  Samples
  * with weight 0 contribute exact zeros: sequences with fewer stored samples than I give the same filter as
  * a call over their own samples.                                                                           */
-int mmt_dimp_optimize_dev(const float* feat, int64_t feat_img_stride, int64_t feat_seq_stride, int I, int S, int C,
-                          int H, int W, float* weights, int fh, int fw, const float* bb_dev, int64_t bb_img_stride,
-                          int64_t bb_seq_stride, const float* sample_weight_dev, int64_t sw_img_stride,
-                          int64_t sw_seq_stride, const mmt_dimp_params* p, int num_iter, void* workspace,
-                          size_t ws_bytes, void* hip_stream);
+int mmt_dimp_optimize_strided(const float* feat, int64_t feat_img_stride, int64_t feat_seq_stride, int I, int S,
+                              int C, int H, int W, float* weights, int fh, int fw, const float* bb_dev,
+                              int64_t bb_img_stride, int64_t bb_seq_stride, const float* sample_weight_dev,
+                              int64_t sw_img_stride, int64_t sw_seq_stride, const mmt_dimp_params* p, int num_iter,
+                              void* workspace, size_t ws_bytes, void* hip_stream);
 
 /* ---- operator-level entry points (device pointers; used by the parity tests and by hosts that
  *      compose their own pipelines).  epi: 0 bias->bf16, 1 bias+GELU->bf16, 2 C(f32) = R + acc + bias,

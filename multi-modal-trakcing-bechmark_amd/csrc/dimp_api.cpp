@@ -200,11 +200,11 @@ int mmt_dimp_optimize(const float* feat, int I, int S, int C, int H, int W, floa
   return optimize_body(feat, S * chw, chw, I, S, C, H, W, weights, fh, fw, p, num_iter, ws, L, losses, st);
 }
 
-int mmt_dimp_optimize_dev(const float* feat, int64_t feat_img_stride, int64_t feat_seq_stride, int I, int S, int C,
-                          int H, int W, float* weights, int fh, int fw, const float* bb_dev, int64_t bb_img_stride,
-                          int64_t bb_seq_stride, const float* sample_weight_dev, int64_t sw_img_stride,
-                          int64_t sw_seq_stride, const mmt_dimp_params* p, int num_iter, void* workspace,
-                          size_t ws_bytes, void* stream_) {
+int mmt_dimp_optimize_strided(const float* feat, int64_t feat_img_stride, int64_t feat_seq_stride, int I, int S,
+                              int C, int H, int W, float* weights, int fh, int fw, const float* bb_dev,
+                              int64_t bb_img_stride, int64_t bb_seq_stride, const float* sample_weight_dev,
+                              int64_t sw_img_stride, int64_t sw_seq_stride, const mmt_dimp_params* p, int num_iter,
+                              void* workspace, size_t ws_bytes, void* stream_) {
   if (!feat || !weights || !bb_dev || !p || !workspace || num_iter < 0 || bad_dims(I, S, C, H, W, fh, fw) ||
       p->num_dist_bins <= 0 || p->num_dist_bins > 128 || feat_img_stride < -1 || feat_seq_stride < -1 ||
       bb_img_stride < -1 || bb_seq_stride < -1 || sw_img_stride < -1 || sw_seq_stride < -1)

@@ -1522,7 +1522,9 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
     const mmt_conv_group& c = groups[i];
     if (!c.x || !c.w_hi || !c.w_lo || !c.y || !(c.w_scale > 0) ||
         (c.flags & ~(MMT_CONV_RELU | MMT_CONV_MAX | MMT_CONV_POOL)) || (!c.x_max && !(c.x_scale > 0)) ||
-        (c.flags & MMT_CONV_POOL) != (groups[0].flags & MMT_CONV_POOL))
+        (c.flags & MMT_CONV_POOL) != (groups[0].flags & MMT_CONV_POOL) ||
+        // the pooled stem kernel neither max-merges nor adds a residual: refuse operands it would drop
+        ((c.flags & MMT_CONV_POOL) && ((c.flags & MMT_CONV_MAX) || c.resid)))
       return MMT_E_ARG;
     a.g[i] = ConvGroupArgs{c.x, c.w_hi, c.w_lo, c.bias, c.resid, c.y, c.x_max, c.y_max, c.x_scale, 1.0f / c.w_scale,
                            c.flags};
@@ -1535,7 +1537,7 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   const hipStream_t s = (hipStream_t)stream;
   if (groups[0].flags & MMT_CONV_POOL) {
     // the 7 x 7 / stride-2 stem with the 3 x 3 / stride-2 / pad-1 max-pool fused; y is the pooled map
-    if (Cin != 4 || Cout != 64 || kh != 7 || kw != 7 || stride != 2 || Kp != 224 || (groups[0].flags & MMT_CONV_MAX))
+    if (Cin != 4 || Cout != 64 || kh != 7 || kw != 7 || stride != 2 || Kp != 224)
       return MMT_E_ARG;
     const int PHo = (Ho - 1) / 2 + 1, PWo = (Wo - 1) / 2 + 1;
     const unsigned tiles = (unsigned)(N * ((PHo + kPoolT - 1) / kPoolT) * ((PWo + kPoolT - 1) / kPoolT));

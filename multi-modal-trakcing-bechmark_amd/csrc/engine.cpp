@@ -1173,6 +1173,7 @@ int check_engine(mmt_engine* e) {
 extern "C" {
 
 const char* mmt_version(void) { return "mmtrack-mi355x 0.1 (gfx950)"; }
+int mmt_abi_version(void) { return MMT_ABI_VERSION; }
 
 int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   if (!cfg || !out) return MMT_E_ARG;

@@ -111,6 +111,8 @@ class MmtDimpResult(ctypes.Structure):
                 ("aux", ctypes.c_int * 4)]
 
 
+ABI_VERSION = 5   # include/mmtrack.h MMT_ABI_VERSION
+
 # every symbol include/mmtrack.h declares: name -> (restype, argtypes)
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -122,6 +124,7 @@ SIGNATURES = {
     "mmt_destroy": (None, [_P]),
     "mmt_last_error": (ctypes.c_char_p, [_P]),
     "mmt_version": (ctypes.c_char_p, []),
+    "mmt_abi_version": (_I, []),
     "mmt_set_tensor": (_I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(_I64), _I]),
     "mmt_finalize": (_I, [_P]),
     "mmt_num_expected_keys": (_I, [_P]),
@@ -168,7 +171,7 @@ SIGNATURES = {
     "mmt_dimp_feat_transpose": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_dimp_optimize": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, ctypes.POINTER(MmtDimpParams), _I, _P,
                                ctypes.c_size_t, _P, _P]),
-    "mmt_dimp_optimize_dev": (_I, [_P, _I64, _I64, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I64, _I64, _P, _I64, _I64,
+    "mmt_dimp_optimize_strided": (_I, [_P, _I64, _I64, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I64, _I64, _P, _I64, _I64,
                                    ctypes.POINTER(MmtDimpParams), _I, _P, ctypes.c_size_t, _P]),
     "mmt_dimp_state_bytes": (ctypes.c_size_t, []),
     "mmt_dimp_track_optimize_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I]),
@@ -202,5 +205,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.mmt_abi_version() != ABI_VERSION:   # a stale library whose argument conventions differ
+        raise ImportError(f"libmmtrack.so ABI {lib.mmt_abi_version()} != {ABI_VERSION} (include/mmtrack.h "
+                          f"MMT_ABI_VERSION); rebuild it")
     _lib = lib
     return lib

@@ -140,7 +140,7 @@ class DiMPSteepestDescentGN:
         """num_iter steps in place on ``weights`` (a contiguous [S, C, fh, fw] CUDA tensor) over ``feat``
         [I, S, C, H, W] -- any strides on the first two dims, e.g. a DimpPool's memory[a:b, :I].transpose(0, 1)
         -- with the boxes and sample weights at device addresses (the device tracker state), strides in floats
-        as (sample, sequence), -1: contiguous [I][S] (0 is a real stride: a broadcast operand); no host staging, no synchronisation (mmt_dimp_optimize_dev)."""
+        as (sample, sequence), -1: contiguous [I][S] (0 is a real stride: a broadcast operand); no host staging, no synchronisation (mmt_dimp_optimize_strided)."""
         lib = _lib.load()
         if not (isinstance(feat, torch.Tensor) and feat.is_cuda and feat.dtype == torch.float32 and feat.dim() == 5):
             raise ValueError("feat must be a 5-dim float32 CUDA tensor")
@@ -154,11 +154,11 @@ class DiMPSteepestDescentGN:
         if nbytes == 0:
             raise ValueError("unsupported DiMP problem shape")
         ws = self._workspace(feat.device, nbytes)
-        _rc(lib.mmt_dimp_optimize_dev(feat.data_ptr(), feat.stride(0), feat.stride(1), I, S, C, H, W,
-                                      weights.data_ptr(), fh, fw, ctypes.c_void_p(bb_ptr), bb_strides[0],
-                                      bb_strides[1], ctypes.c_void_p(sw_ptr) if sw_ptr else None, sw_strides[0],
-                                      sw_strides[1], ctypes.byref(self.params), num_iter, ws.data_ptr(), nbytes,
-                                      _stream(feat.device)), "mmt_dimp_optimize_dev")
+        _rc(lib.mmt_dimp_optimize_strided(feat.data_ptr(), feat.stride(0), feat.stride(1), I, S, C, H, W,
+                                          weights.data_ptr(), fh, fw, ctypes.c_void_p(bb_ptr), bb_strides[0],
+                                          bb_strides[1], ctypes.c_void_p(sw_ptr) if sw_ptr else None, sw_strides[0],
+                                          sw_strides[1], ctypes.byref(self.params), num_iter, ws.data_ptr(), nbytes,
+                                          _stream(feat.device)), "mmt_dimp_optimize_strided")
         return weights
 
     def optimize(self, weights, feat, bb, sample_weight=None, num_iter=None):

@@ -1,0 +1,156 @@
+"""How far the reference DiMP tracker's confidences move under fp32-level arithmetic differences, to derive the
+end-to-end DiMP tolerance instead of assuming it.  Writes tests/golden/dimp_spread.npz.
+
+Runs the REFERENCE DeT tracker (pytracking/tracker/dimp/dimp.py DiMP, DeT_DiMP50_Max parameters, use_iou_net
+False) on the tracker_dimp.npz sequence (make_golden_dimp.SEQ, TRACK_SEED) in this build container, on the CPU,
+in variants that differ only in rounding:
+* ``base``      -- the golden's own run (reproduced; its confidences must equal tracker_dimp.npz's);
+* ``feat5e-7``  -- every backbone output (layer2 / layer3 after the max merge) multiplied by (1 + 5e-7 n), n a
+                   seeded standard normal per element: the relative feature error the HIP backbone shows against
+                   the reference (layer3 within ~5e-7 relative);
+* ``feat1e-6``, ``feat2e-7`` -- the same at twice / 0.4 times that error;
+* ``clf64``     -- the classification feature block (clf conv + InstanceL2Norm, dimpnet.py:85-86) evaluated in
+                   float64 and cast to float32: the clf features with their fp32 summation-order error removed;
+* ``opt64``     -- the whole classifier (filter initialiser, Gauss-Newton steepest descent, apply_filter) in
+                   float64: the optimiser's own fp32 rounding removed.
+For every variant the per-frame confidences, boxes and flags are stored; the spread of a variant is its largest
+relative confidence difference to ``base`` over the frames whose flags agree.
+
+Build container only (needs /root/reference); the reference is imported exactly as make_golden_dimp.py does
+(stand-ins listed there).  Usage:  python tests/golden/make_dimp_spread.py
+"""
+import copy
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import make_golden_dimp as mgd  # noqa: E402
+from mmtrack_amd import synth  # noqa: E402
+
+
+def run_tracker(wnet, feat_noise=0.0, clf64=False, opt64=False, noise_seed=1234):
+    from pytracking.parameter.dimp import DeT_DiMP50_Max as P
+    from pytracking.tracker.dimp.dimp import DiMP
+    net = wnet.net
+    ebf = net.extract_backbone_features
+    ecf = net.extract_classification_feat
+    clf = net.classifier
+    gen = torch.Generator().manual_seed(noise_seed)
+    saved = {}
+
+    def noisy_backbone(im, layers=None):
+        out = ebf(im, layers) if layers is not None else ebf(im)
+        if feat_noise > 0:
+            out = {k: v * (1 + feat_noise * torch.randn(v.shape, generator=gen)) for k, v in out.items()}
+        return out
+
+    def clf_feat64(backbone_feat):
+        fe = copy.deepcopy(clf.feature_extractor).double()
+        x = net.get_backbone_clf_feat(backbone_feat).double()
+        return fe(x).float()
+
+    net.extract_backbone_features = noisy_backbone
+    if clf64:
+        net.extract_classification_feat = clf_feat64
+    if opt64:   # the classifier's filter initialiser / optimiser / classify in float64 on float64 features
+        saved["clf"] = clf
+        c64 = copy.deepcopy(clf).double()
+        fe32 = clf.feature_extractor
+
+        class Clf64(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.c = c64
+                self.feature_extractor = fe32
+
+            def extract_classification_feat(self, f):
+                return clf.extract_classification_feat(f)
+
+            def get_filter(self, feat, bb, *a, **k):
+                w, ws, losses = self.c.get_filter(feat.double(), bb.double(), *a, **k)
+                return w.float(), [x.float() for x in ws], losses
+
+            def classify(self, w, feat):
+                return self.c.classify(w.double(), feat.double()).float()
+
+            def __getattr__(self, name):
+                try:
+                    return super().__getattr__(name)
+                except AttributeError:
+                    return getattr(self.c, name)
+        net.classifier = Clf64()
+    try:
+        params = P.parameters()
+        params.use_gpu, params.device, params.use_iou_net, params.net = False, "cpu", False, wnet
+        tr = DiMP(params)
+        tr.features_initialized = True
+        if opt64:   # the tracker's own filter updates call the optimiser directly on float32 tensors
+            fo = c64.filter_optimizer
+            fwd = fo.forward
+
+            def fwd64(w, feat=None, bb=None, *a, **k):
+                k = {kk: (v.double() if torch.is_tensor(v) else v) for kk, v in k.items()}
+                r = fwd(w.double(), feat.double(), bb.double() if bb is not None else None, *a, **k)
+                return (r[0].float(),) + tuple(r[1:])
+            fo.forward = fwd64
+        S = mgd.SEQ
+        frames, _ = synth.make_frames(S["seed"], S["n"], S["H"], S["W"], S["C"], box=S["box"])
+        torch.manual_seed(mgd.TRACK_SEED)
+        tr.initialize(frames[0], {"init_bbox": list(S["box"])})
+        boxes, conf, flags = [list(S["box"])], [1.0], ["init"]
+        for t in range(1, S["n"]):
+            o = tr.track(frames[t])
+            boxes.append([float(v) for v in o["target_bbox"]])
+            conf.append(float(o["confidence"]))
+            flags.append(tr.debug_info["flag"])
+        return np.array(boxes), np.array(conf), np.array(flags)
+    finally:
+        net.extract_backbone_features = ebf
+        net.extract_classification_feat = ecf
+        if "clf" in saved:
+            net.classifier = saved["clf"]
+
+
+def spread(base, other):
+    """Largest relative confidence difference over frames 1.. whose flags agree, and how many disagree."""
+    bc, bf = base[1], base[2]
+    oc, of = other[1], other[2]
+    same = bf[1:] == of[1:]
+    rel = np.abs(oc[1:] - bc[1:]) / np.maximum(np.abs(bc[1:]), 1e-12)
+    return float(rel[same].max()) if same.any() else float("nan"), int((~same).sum())
+
+
+def main():
+    mgd.install()
+    torch.set_num_threads(8)
+    sd = synth.make_dimp_state_dict(0)
+    wnet = mgd.wrap(mgd.build_net(sd))
+    gold = np.load(os.path.join(HERE, "tracker_dimp.npz"))
+    variants = {"base": {}, "feat2e-7": dict(feat_noise=2e-7), "feat5e-7": dict(feat_noise=5e-7),
+                "feat1e-6": dict(feat_noise=1e-6), "feat5e-7_s2": dict(feat_noise=5e-7, noise_seed=99),
+                "clf64": dict(clf64=True), "opt64": dict(opt64=True)}
+    out = {}
+    res = {}
+    for name, kw in variants.items():
+        b, c, f = run_tracker(wnet, **kw)
+        res[name] = (b, c, f)
+        out[name + "/boxes"], out[name + "/confidence"], out[name + "/flags"] = b, c, f
+        if name == "base":
+            assert np.array_equal(c, gold["confidence"]) and list(f) == list(gold["flags"]), "base != golden"
+        s, nflip = spread(res["base"], res[name])
+        out[name + "/spread"] = np.array(s)
+        out[name + "/flag_flips"] = np.array(nflip)
+        print(f"{name:12s} max rel confidence diff vs base {s:.3e}  flag flips {nflip}  "
+              f"per frame {np.round(np.abs(c[1:] - res['base'][1][1:]) / res['base'][1][1:], 6).tolist()}", flush=True)
+    out["names"] = np.array(list(variants))
+    np.savez_compressed(os.path.join(HERE, "dimp_spread.npz"), **out)
+
+
+if __name__ == "__main__":
+    main()

@@ -22,7 +22,8 @@ fills the 50-sample memory and replaces samples.  Per frame it records the flag,
 masked second maximum (max_score2, NaN where the branch returns before computing it); per sequence the filter
 after the first hard-negative update and at the end, and the memory bookkeeping (sample weights, boxes,
 num_stored, previous replace index).
-Usage:  python tests/golden/make_golden_dimp.py [net] [tracker] [branches]   (default: all three)
+dimp_stages.npz (``stages``, not in the default set) records every stage of the tracker_dimp.npz run (stages_fixture).
+Usage:  python tests/golden/make_golden_dimp.py [net] [tracker] [branches] [stages]   (default: the first three)
 """
 import importlib
 import json
@@ -346,6 +347,102 @@ def branch_fixture(wnet, seqs=None, path=None):
                         init_box=np.array(SEQ["box"]), **out)
 
 
+def _summ(t, step):
+    """A stage tensor [n, C, H, W] as (per-sample channel sums in float64, every step-th channel's full maps)."""
+    t = t.detach().float()
+    return t.double().sum(dim=(2, 3)).numpy(), t[:, ::step].numpy()
+
+
+def stages_fixture(wnet, n_frames=6):
+    """dimp_stages.npz: the tracker_dimp.npz run (same sequence, seed and parameters) with every stage of
+    initialize() and of the first frames recorded, so the HIP path can be compared stage by stage (VERDICT r4
+    item 3): the 15 augmented init patches (every 8th pixel of every channel) and their sums, the backbone
+    layer3 and the classification features (per-channel sums + every 64th / 32nd channel), the dropout-augmented
+    feature stack's sums, the initial filter and all Gauss-Newton iterates, the target boxes; per frame the
+    sampled patch (every 8th pixel), its sample coordinates, the clf features' sums, the raw score map and the
+    filter the frame's scores used."""
+    from pytracking.parameter.dimp import DeT_DiMP50_Max as P
+    from pytracking.tracker.dimp.dimp import DiMP
+    net = wnet.net
+    params = P.parameters()
+    params.use_gpu, params.device, params.use_iou_net, params.net = False, "cpu", False, wnet
+    tr = DiMP(params)
+    tr.features_initialized = True
+    cap = {"bb_in": [], "bb_out": [], "clf": [], "scores": []}
+    eb, gcf, ct = wnet.extract_backbone, tr.get_classification_features, tr.classify_target
+    fi = net.classifier.filter_initializer
+    fo = net.classifier.filter_optimizer
+    fi_fwd, fo_fwd = fi.forward, fo.forward
+
+    def extract(im):
+        r = eb(im)
+        cap["bb_in"].append(im.clone())
+        cap["bb_out"].append(r["layer3"].clone())
+        return r
+
+    def clf_feat(f):
+        r = gcf(f)
+        cap["clf"].append(r.clone())
+        return r
+
+    def classify(x):
+        cap["filter_used"] = tr.target_filter.clone()
+        r = ct(x)
+        cap["scores"].append((r.clone(), cap["filter_used"]))
+        return r
+
+    def init_fwd(feat, bb):
+        r = fi_fwd(feat, bb)
+        cap["init_in_sums"] = feat.double().sum(dim=tuple(range(2, feat.dim()))).numpy()
+        cap["init_bb"] = bb.clone()
+        cap["init_filter"] = r.clone()
+        return r
+
+    def opt_fwd(w, *a, **k):
+        r = fo_fwd(w, *a, **k)
+        if "iterates" not in cap:
+            cap["iterates"] = [x.clone() for x in r[1]]
+        return r
+    wnet.extract_backbone = extract
+    tr.get_classification_features, tr.classify_target = clf_feat, classify
+    fi.forward, fo.forward = init_fwd, opt_fwd
+    try:
+        frames, _ = synth.make_frames(SEQ["seed"], SEQ["n"], SEQ["H"], SEQ["W"], SEQ["C"], box=SEQ["box"])
+        torch.manual_seed(TRACK_SEED)
+        tr.initialize(frames[0], {"init_bbox": list(SEQ["box"])})
+        res = {}
+        p = cap["bb_in"][0]
+        res["init_patch_sums"] = p.double().sum(dim=(1, 2, 3)).numpy()
+        res["init_patch_sub"] = p[:, :, ::8, ::8].numpy()
+        res["init_l3_sums"], res["init_l3_ch"] = _summ(cap["bb_out"][0], 64)
+        res["init_clf_sums"], res["init_clf_ch"] = _summ(cap["clf"][0], 32)
+        res["init_stack_sums"] = cap["init_in_sums"]
+        res["init_target_boxes"] = cap["init_bb"].reshape(-1, 4).numpy()
+        res["init_filter"] = cap["init_filter"].numpy()
+        res["iterates"] = torch.stack(cap["iterates"]).numpy()
+        conf = []
+        for t in range(1, n_frames + 1):
+            o = tr.track(frames[t])
+            conf.append(float(o["confidence"]))
+            k = t   # capture index: bb_in[0] / clf[0] are the init ones
+            pf = cap["bb_in"][k]
+            res[f"f{t}_patch_sums"] = pf.double().sum(dim=(1, 2, 3)).numpy()
+            res[f"f{t}_patch_sub"] = pf[:, :, ::8, ::8].numpy()
+            res[f"f{t}_l3_sums"] = cap["bb_out"][k].double().sum(dim=(2, 3)).numpy()
+            res[f"f{t}_clf_sums"] = cap["clf"][k].double().sum(dim=(2, 3)).numpy()
+            sc, fu = cap["scores"][t - 1]
+            res[f"f{t}_scores"] = sc.numpy()
+            res[f"f{t}_filter"] = fu.numpy()
+        res["confidence"] = np.array(conf)
+        gold = np.load(os.path.join(HERE, "tracker_dimp.npz"))
+        assert np.array_equal(res["confidence"], gold["confidence"][1:n_frames + 1]), "stage run != tracker golden"
+        np.savez_compressed(os.path.join(HERE, "dimp_stages.npz"), **res)
+        print("wrote dimp_stages:", {k: v.shape for k, v in res.items() if k.startswith("init")}, conf)
+    finally:
+        wnet.extract_backbone = eb
+        fi.forward, fo.forward = fi_fwd, fo_fwd
+
+
 def main():
     what = set(sys.argv[1:]) or {"net", "tracker", "branches"}
     install()
@@ -359,6 +456,8 @@ def main():
         tracker_fixture(wnet)
     if "branches" in what:
         branch_fixture(wnet)
+    if "stages" in what:
+        stages_fixture(wnet)
 
 
 if __name__ == "__main__":

@@ -31,6 +31,16 @@ def test_version_without_gpu():
     assert _lib.load().mmt_version().startswith(b"mmtrack-mi355x")
 
 
+def test_abi_version_matches_header_and_binding():
+    """The library, the header's MMT_ABI_VERSION and the ctypes binding agree; the pre-5 strided optimiser
+    (stride 0 = contiguous) is not exported, so a binding written against it fails to resolve the symbol."""
+    hdr = open(HDR).read()
+    v = int(re.search(r"#define\s+MMT_ABI_VERSION\s+(\d+)", hdr).group(1))
+    lib = _lib.load()
+    assert lib.mmt_abi_version() == v == _lib.ABI_VERSION
+    assert not hasattr(lib, "mmt_dimp_optimize_dev")
+
+
 def test_dimp_state_layout_matches_binding():
     """The device DiMP tracker state / record structs of include/mmtrack.h and the ctypes binding agree in size
     (the library reports sizeof(mmt_dimp_state); no GPU needed)."""

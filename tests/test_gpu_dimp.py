@@ -142,3 +142,15 @@ def test_track_optimize_matches_per_sequence():
     ref0 = opt.optimize(filt[0:1].cuda(), mem[0].unsqueeze(1).contiguous(), bb[0].view(I, 1, 4),
                         sample_weight=sw[0].view(I, 1), num_iter=2)
     assert torch.equal(fd2[0:1].cpu(), ref0.cpu())
+    # stride 0 is a broadcast (ABI 5): one box / weight column shared by both sequences equals the same values
+    # repeated per sequence (a binding that meant 'contiguous' by 0 would get sample 0's box everywhere instead)
+    fd3 = filt[0:2].clone().cuda()
+    feat2 = mem[0:2, :I].transpose(0, 1)
+    bbs = bb[0].contiguous().cuda()
+    sws = sw[0].contiguous().cuda()
+    opt.optimize_dev(fd3, feat2, bbs.data_ptr(), sws.data_ptr(), 2, bb_strides=(4, 0), sw_strides=(1, 0))
+    ref3 = opt.optimize(filt[0:2].cuda(), mem[0:2, :I].transpose(0, 1).contiguous(),
+                        bb[0].unsqueeze(1).expand(I, 2, 4).contiguous(),
+                        sample_weight=sw[0].unsqueeze(1).expand(I, 2).contiguous(), num_iter=2)
+    assert torch.equal(fd3.cpu(), ref3.cpu())
+    assert not torch.equal(fd3[1].cpu(), filt[1])

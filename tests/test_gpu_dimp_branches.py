@@ -255,8 +255,10 @@ def test_dimp_pool32_bench_launch_matches_reference(nets, precision):
 
 def test_pool_launch_does_not_block_the_host(nets):
     """DimpPool.launch queues a frame without waiting for the device (the frame descriptors and host
-    frames go through pinned buffers with asynchronous copies): with a long GPU job queued ahead on the stream,
-    launch() returns while that job is still running, for device frames and for numpy host frames alike."""
+    frames go through pinned buffers with asynchronous copies): with a GPU job queued ahead on the stream that
+    spins for ~1e9 clock cycles (torch.cuda._sleep: a fixed count, not a race against the speed of some matrix
+    work), launch() returns while that job is still running, for device frames and for numpy host frames alike.
+    One launch runs first, untimed, so lazy allocations are not inside the window."""
     from mmtrack_amd import synth
     from mmtrack_amd.dimp_tracker import DiMP, DimpPool, parameters
     net = nets["f16x3"]
@@ -266,11 +268,10 @@ def test_pool_launch_does_not_block_the_host(nets):
     for tr in trs:
         tr.initialize(frames[0], {"init_bbox": list(gts[0])})
     dev = torch.from_numpy(frames).cuda()
-    a = torch.randn(8192, 8192, device="cuda")
+    pool.finish(trs, 0, pool.launch(trs, [dev[1], dev[1]], 0))
     for k, fr in enumerate(([dev[1], dev[1]], [frames[2], frames[2]], [frames[3], dev[3]])):
         torch.cuda.synchronize()
-        for _ in range(40):   # ~0.3 s of matrix work queued ahead of the launch
-            a = torch.tanh(a @ a * 1e-4)
+        torch.cuda._sleep(1_000_000_000)   # a spin of ~0.4 s at the shader clock, queued ahead of the launch
         busy = torch.cuda.Event()
         busy.record()
         ticket = pool.launch(trs, fr, 0)

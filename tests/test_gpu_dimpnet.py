@@ -240,6 +240,15 @@ def test_conv2d_f16x3_stem_pool_bitwise(N, H, W):
     assert lib.mmt_conv2d_f16x3_groups(arr, 2, N, H, W, 4, convs[0].kp, 64, 7, 7, 2, 3, None, 0, stream) == -1
     arr = (_lib.MmtConvGroup * 1)(gr[0])
     assert lib.mmt_conv2d_f16x3_groups(arr, 1, N, H, W, 4, convs[0].kp, 64, 7, 7, 1, 3, None, 0, stream) == -1
+    # ... and operands the pooled kernel would drop: a MAX merge on the second group only, a residual on either
+    bad1 = convs[1].group(xs[1], got[1], relu=True, merge_max=True, x_scale=scale, pool=True)
+    arr = (_lib.MmtConvGroup * 2)(gr[0], bad1)
+    assert lib.mmt_conv2d_f16x3_groups(arr, 2, N, H, W, 4, convs[0].kp, 64, 7, 7, 2, 3, None, 0, stream) == -1
+    for k in range(2):
+        pair = list(gr)
+        pair[k] = convs[k].group(xs[k], got[k], relu=True, resid=full[k], x_scale=scale, pool=True)
+        arr = (_lib.MmtConvGroup * 2)(*pair)
+        assert lib.mmt_conv2d_f16x3_groups(arr, 2, N, H, W, 4, convs[0].kp, 64, 7, 7, 2, 3, None, 0, stream) == -1
 
 
 def test_conv2d_stem_w4():
