@@ -63,12 +63,16 @@ __device__ __forceinline__ void tile_of(int id, int tiles_m, int tiles_n, int gm
   tm = first + (rem - tn * h);
 }
 
-// optional per-block cycle stamps (tuning: mmt_gemm_stamps); null in production
+// optional per-block cycle stamps (tuning: mmt_gemm_stamps); null in production.  The pointer is read ONCE, at
+// kernel entry (GEMM_STAMP_DECL, a scalar load before any operand load): re-reading the global inside the kernel
+// compiled to a vector load plus s_waitcnt vmcnt(0), which drained every LDS-DMA load in flight at the stamp after
+// the prologue -- one dependent memory round trip per tile in production builds (found round 5)
 __device__ unsigned long long* g_gemm_stamps = nullptr;
+#define GEMM_STAMP_DECL unsigned long long* const gemm_stamps_ = g_gemm_stamps
 #define GEMM_STAMP(k)                                                                      \
   do {                                                                                     \
-    if (g_gemm_stamps && threadIdx.x == 0)                                                 \
-      g_gemm_stamps[(size_t)blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memtime();          \
+    if (gemm_stamps_ && threadIdx.x == 0)                                                  \
+      gemm_stamps_[(size_t)blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memtime();           \
   } while (0)
 
 
@@ -281,6 +285,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   static_assert(BK == 64 || (BK == 32 && AM == A_DENSE), "BK 32: dense A only");
   using T = Tile<BM, BN, WMW, WNW, SPLIT, STAGES, BK>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[T::NSTAGE * T::STAGE];
+  GEMM_STAMP_DECL;
 
   const GemmGroup& g = args.g[blockIdx.z];
   const int M = args.M, K = args.K;
@@ -311,6 +316,16 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
   if constexpr (RPRE > 0) {
 #pragma unroll
     for (int k = 0; k < RPRE; ++k) rpre[k] = LT::r_chunk(g, args, tid + k * T::NT, m0, n0, M);
+  }
+  // the fragment-shaped epilogue's bias chunks (split mode), requested now through branch-free raw buffer loads: they
+  // are the oldest loads in the queue, so the main loop's first counted wait retires them and the epilogue starts
+  // without a dependent round trip (one-sequence qkv / fc1: ~1 us of a ~10 us launch)
+  constexpr bool EARLY_BIAS = !LDS_EPI && EPI != EPI_PARTIAL;
+  float4 bq[EARLY_BIAS ? T::FN : 1];
+  if constexpr (EARLY_BIAS) {
+    const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)args.N * 4 : 0);
+#pragma unroll
+    for (int jj = 0; jj < T::FN; ++jj) bq[jj] = epi_bias(rB, n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4);
   }
 
   // ---- loads: buffer_load ... lds with per-lane VGPR offsets fixed over K and the K advance in the
@@ -493,8 +508,9 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
     constexpr int D = NS - 1;
     for (int p = 0; p < D; ++p)
       if (p < nk) issue(kbeg + p, p);
-    if (nk > 1 && D > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW * (D - 1)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // tile 0 landed: the min(D, nk) - 1 tiles issued after it may stay in flight (a K shorter than the ring issues
+    // fewer; until round 5 a stamp's hidden vmcnt(0) covered the nk < D case this count used to get wrong)
+    vm_wait_rt<GPW*(D > 1 ? D - 1 : 0)>(GPW * (min(D, nk) - 1));
     __builtin_amdgcn_s_barrier();
     GEMM_STAMP(1);
     int stage = 0;
@@ -602,14 +618,11 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
     __syncthreads();
     LT::template drain<BM, T::NT, RPRE>(lds, g, args, m0, n0, M, rpre);
   } else {
-    const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)args.N * 4 : 0);
     const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
     // (the residual chunks of the 32-fragment tiles -- 256 x 256 tuning configs -- would need 128 more VGPRs:
     // those keep one fragment's residual at a time)
     constexpr bool RPRE_ALL = epi_has_r(EPI) && T::FM * T::FN <= 16;
-    float4 bq[T::FN], rq[RPRE_ALL ? T::FM : 1][RPRE_ALL ? T::FN : 1];
-#pragma unroll
-    for (int jj = 0; jj < T::FN; ++jj) bq[jj] = epi_bias(rB, n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4);
+    float4 rq[RPRE_ALL ? T::FM : 1][RPRE_ALL ? T::FN : 1];
     if constexpr (RPRE_ALL) {
 #pragma unroll
       for (int i = 0; i < T::FM; ++i)
@@ -1016,6 +1029,7 @@ static int num_cus() {
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm256_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 128 * 64];
+  GEMM_STAMP_DECL;
   const GemmGroup& g = args.g[blockIdx.z];
   const int M = args.M, K = args.K;
   const int tiles_m = (M + 255) / 256, tiles_n = args.N / 256, ntiles = tiles_m * tiles_n;
@@ -1225,7 +1239,21 @@ static void launch256_epi(const GemmArgs& a, int epi, hipStream_t s) {
 // one 128 x 128 quadrant: per wave 64 x 32 = 4 x 2 fragment pairs x 3 products = 24 MFMAs.
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
+#ifdef GEMM_PHASE_STAMPS
+  // tuning build: per phase, wave 0 and wave 4 stamp (before the counted wait, after the first barrier = MFMA start,
+  // after the second barrier) into an LDS tail of the one staging array; copied to mmt_gemm_stamps' buffer at the end
+  constexpr int PS_PH = 3 * 96;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 8192 + 2 * PS_PH * 4];
+  unsigned long long* const pst = reinterpret_cast<unsigned long long*>(smem + 8 * 8192);
+#define PSTAMP(slot)                                                                                          \
+  do {                                                                                                        \
+    if ((threadIdx.x & 255) == 0 && (slot) < PS_PH) pst[(threadIdx.x >> 8) * PS_PH + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
   __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 8192];
+#define PSTAMP(slot) do { } while (0)
+#endif
+  GEMM_STAMP_DECL;
   const GemmGroup& g = args.g[blockIdx.z];
   const int M = args.M, K = args.K;
   const int tiles_m = (M + 255) / 256, tiles_n = args.N / 256, ntiles = tiles_m * tiles_n;
@@ -1238,6 +1266,14 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   GEMM_STAMP(0);
+  // the lane's 4 bias chunks (2 column halves x 2), requested before the first half-tile loads (the prologue's
+  // counted wait retires them; the epilogue then starts without a dependent round trip)
+  const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)args.N * 4 : 0);
+  float4 bq[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) bq[h][jj] = epi_bias(rB, n0 + h * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4);
 
   // half-tile loads: a wave-instruction fills 16 rows x 64 B (swzk<32> image, source chunk pre-swizzled)
   const int chunk = ((lane & 3) ^ ((lane >> 4) & 2)) * 16;
@@ -1322,28 +1358,40 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
     const int P0 = 4 * kt;
     read_b(S + 8192, B0h, B0l);
     read_a(S);
+    PSTAMP(3 * P0);
     if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0, 0));
     if (STEADY || P0 + 6 < NL) issue(P0 + 6, std::integral_constant<int, 2>{});
     __builtin_amdgcn_s_barrier();
+    PSTAMP(3 * P0 + 1);
     mma(acc[0], B0h, B0l);
     __builtin_amdgcn_s_barrier();
+    PSTAMP(3 * P0 + 2);
     read_b(S + 2 * 8192, B1h, B1l);
+    PSTAMP(3 * P0 + 3);
     if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 1, 1));
     if (STEADY || P0 + 7 < NL) issue(P0 + 7, std::integral_constant<int, 3>{});
     __builtin_amdgcn_s_barrier();
+    PSTAMP(3 * P0 + 4);
     mma(acc[1], B1h, B1l);
     __builtin_amdgcn_s_barrier();
+    PSTAMP(3 * P0 + 5);
     read_a(S + 3 * 8192);
+    PSTAMP(3 * P0 + 6);
     if (STEADY) asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); else wait_vm(n_after(P0 + 2, 2));
     if (STEADY || P0 + 8 < NL) issue(P0 + 8, std::integral_constant<int, 0>{});
     __builtin_amdgcn_s_barrier();
+    PSTAMP(3 * P0 + 7);
     mma(acc[2], B1h, B1l);
     __builtin_amdgcn_s_barrier();
+    PSTAMP(3 * P0 + 8);
+    PSTAMP(3 * P0 + 9);
     if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 3, 3));
     if (STEADY || P0 + 9 < NL) issue(P0 + 9, std::integral_constant<int, 1>{});
     __builtin_amdgcn_s_barrier();
+    PSTAMP(3 * P0 + 10);
     mma(acc[3], B0h, B0l);
     __builtin_amdgcn_s_barrier();
+    PSTAMP(3 * P0 + 11);
   };
 
   issue(0, std::integral_constant<int, 0>{});
@@ -1368,14 +1416,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
   GEMM_STAMP(2);
 
   constexpr int QA[4] = {0, 0, 1, 1}, QB[4] = {0, 1, 1, 0};
-  // the lane's 4 bias chunks (2 column halves x 2) requested together; the residual epilogues (not used by the
-  // path's launches) keep the per-fragment store4
-  const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)args.N * 4 : 0);
-  float4 bq[2][2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) bq[h][jj] = epi_bias(rB, n0 + h * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4);
+  // (the residual epilogues, not used by the path's launches, keep the per-fragment store4)
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int qd = 0; qd < 4; ++qd)
@@ -1392,7 +1433,14 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
                              bq[QB[qd]][jj], zero4);
     }
   GEMM_STAMP(3);
+#ifdef GEMM_PHASE_STAMPS
+  __syncthreads();
+  if (gemm_stamps_ && blockIdx.x < 256)   // blocks' phase stamps after the [blocks][4] kernel stamps
+    for (int e = threadIdx.x; e < 2 * PS_PH; e += 512)
+      gemm_stamps_[65536 + (size_t)blockIdx.x * 2 * PS_PH + e] = pst[e];
+#endif
 }
+#undef PSTAMP
 
 template <int EPI>
 static void launch256s(const GemmArgs& a0, hipStream_t s) {

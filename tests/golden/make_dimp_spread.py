@@ -12,7 +12,14 @@ in variants that differ only in rounding:
 * ``clf64``     -- the classification feature block (clf conv + InstanceL2Norm, dimpnet.py:85-86) evaluated in
                    float64 and cast to float32: the clf features with their fp32 summation-order error removed;
 * ``opt64``     -- the whole classifier (filter initialiser, Gauss-Newton steepest descent, apply_filter) in
-                   float64: the optimiser's own fp32 rounding removed.
+                   float64: the optimiser's own fp32 rounding removed;
+* ``feat3e-6`` .. ``feat3e-5`` -- backbone noise at and around the HIP path's measured layer3 error;
+* ``bb64``      -- both ResNet-50 backbones in float64, cast to float32 after the max merge: the reference's own
+                   fp32 summation-order error of its features removed (an exact-arithmetic backbone);
+* ``all64``     -- bb64 + clf64 + opt64.
+Then, for the branch sequences of tracker_dimp_branches.npz with the most filter updates (long, low_score,
+uncertain_threshold, distractor_far): base, the backbone noise at 3e-6 / 1e-5 over four seeds, and bb64, stored as
+"<seq>:<variant>/...".
 For every variant the per-frame confidences, boxes and flags are stored; the spread of a variant is its largest
 relative confidence difference to ``base`` over the frames whose flags agree.
 
@@ -34,7 +41,19 @@ import make_golden_dimp as mgd  # noqa: E402
 from mmtrack_amd import synth  # noqa: E402
 
 
-def run_tracker(wnet, feat_noise=0.0, clf64=False, opt64=False, noise_seed=1234):
+class _Double(torch.nn.Module):
+    """A backbone evaluated in float64, its outputs cast to float32 (the reference's fp32 rounding removed)."""
+
+    def __init__(self, m):
+        super().__init__()
+        self.m = copy.deepcopy(m).double()
+
+    def forward(self, x, layers=None):
+        out = self.m(x.double(), layers) if layers is not None else self.m(x.double())
+        return {k: v.float() for k, v in out.items()}
+
+
+def run_tracker(wnet, feat_noise=0.0, clf64=False, opt64=False, noise_seed=1234, bb64=False, seq=None):
     from pytracking.parameter.dimp import DeT_DiMP50_Max as P
     from pytracking.tracker.dimp.dimp import DiMP
     net = wnet.net
@@ -56,6 +75,9 @@ def run_tracker(wnet, feat_noise=0.0, clf64=False, opt64=False, noise_seed=1234)
         return fe(x).float()
 
     net.extract_backbone_features = noisy_backbone
+    if bb64:
+        saved["bb"] = (net.feature_extractor, net.feature_extractor_depth)
+        net.feature_extractor, net.feature_extractor_depth = _Double(saved["bb"][0]), _Double(saved["bb"][1])
     if clf64:
         net.extract_classification_feat = clf_feat64
     if opt64:   # the classifier's filter initialiser / optimiser / classify in float64 on float64 features
@@ -88,6 +110,9 @@ def run_tracker(wnet, feat_noise=0.0, clf64=False, opt64=False, noise_seed=1234)
     try:
         params = P.parameters()
         params.use_gpu, params.device, params.use_iou_net, params.net = False, "cpu", False, wnet
+        events, over, nfr = ({}, {}, mgd.SEQ["n"]) if seq is None else mgd.BRANCH_SEQS[seq]
+        for k, v in over.items():
+            setattr(params, k, v)
         tr = DiMP(params)
         tr.features_initialized = True
         if opt64:   # the tracker's own filter updates call the optimiser directly on float32 tensors
@@ -100,11 +125,11 @@ def run_tracker(wnet, feat_noise=0.0, clf64=False, opt64=False, noise_seed=1234)
                 return (r[0].float(),) + tuple(r[1:])
             fo.forward = fwd64
         S = mgd.SEQ
-        frames, _ = synth.make_frames(S["seed"], S["n"], S["H"], S["W"], S["C"], box=S["box"])
+        frames, _ = synth.make_frames(S["seed"], nfr, S["H"], S["W"], S["C"], box=S["box"], **events)
         torch.manual_seed(mgd.TRACK_SEED)
         tr.initialize(frames[0], {"init_bbox": list(S["box"])})
         boxes, conf, flags = [list(S["box"])], [1.0], ["init"]
-        for t in range(1, S["n"]):
+        for t in range(1, nfr):
             o = tr.track(frames[t])
             boxes.append([float(v) for v in o["target_bbox"]])
             conf.append(float(o["confidence"]))
@@ -115,6 +140,8 @@ def run_tracker(wnet, feat_noise=0.0, clf64=False, opt64=False, noise_seed=1234)
         net.extract_classification_feat = ecf
         if "clf" in saved:
             net.classifier = saved["clf"]
+        if "bb" in saved:
+            net.feature_extractor, net.feature_extractor_depth = saved["bb"]
 
 
 def spread(base, other):
@@ -134,7 +161,18 @@ def main():
     gold = np.load(os.path.join(HERE, "tracker_dimp.npz"))
     variants = {"base": {}, "feat2e-7": dict(feat_noise=2e-7), "feat5e-7": dict(feat_noise=5e-7),
                 "feat1e-6": dict(feat_noise=1e-6), "feat5e-7_s2": dict(feat_noise=5e-7, noise_seed=99),
-                "clf64": dict(clf64=True), "opt64": dict(opt64=True)}
+                "clf64": dict(clf64=True), "opt64": dict(opt64=True),
+                # the HIP backbone's measured layer3 error on this sequence (test_gpu_dimp_stages: 1.2e-5 / 1.4e-5 of
+                # the map's maximum in f16x3 / fp32, i.e. ~3e-6 typical relative per element) and around it
+                "feat3e-6": dict(feat_noise=3e-6), "feat1e-5": dict(feat_noise=1e-5),
+                "feat1e-5_s2": dict(feat_noise=1e-5, noise_seed=99), "feat1e-5_s3": dict(feat_noise=1e-5, noise_seed=7),
+                "feat3e-5": dict(feat_noise=3e-5),
+                # the two backbones in float64 (then cast): the reference's own fp32 summation-order error of its
+                # features removed -- the spread an exact-arithmetic implementation would show against it
+                "bb64": dict(bb64=True), "all64": dict(bb64=True, clf64=True, opt64=True)}
+    only = sys.argv[1:]
+    if only:
+        variants = {k: v for k, v in variants.items() if k == "base" or k in only}
     out = {}
     res = {}
     for name, kw in variants.items():
@@ -149,6 +187,26 @@ def main():
         print(f"{name:12s} max rel confidence diff vs base {s:.3e}  flag flips {nflip}  "
               f"per frame {np.round(np.abs(c[1:] - res['base'][1][1:]) / res['base'][1][1:], 6).tolist()}", flush=True)
     out["names"] = np.array(list(variants))
+    # the branch sequences with the most Gauss-Newton updates / the largest HIP-vs-reference confidence drift in the
+    # round-4 runs (tracker_dimp_branches.npz): base + fp32-level backbone noise over several seeds + the exact backbone
+    bvars = {"base": {}, "feat3e-6": dict(feat_noise=3e-6), "feat1e-5": dict(feat_noise=1e-5),
+             "feat1e-5_s2": dict(feat_noise=1e-5, noise_seed=99), "feat1e-5_s3": dict(feat_noise=1e-5, noise_seed=7),
+             "feat1e-5_s4": dict(feat_noise=1e-5, noise_seed=4242), "bb64": dict(bb64=True)}
+    bgold = np.load(os.path.join(HERE, "tracker_dimp_branches.npz"))
+    for seq in (["long", "low_score", "uncertain_threshold", "distractor_far"] if not only else []):
+        bres = {}
+        for name, kw in bvars.items():
+            b, c, f = run_tracker(wnet, seq=seq, **kw)
+            bres[name] = (b, c, f)
+            key = f"{seq}:{name}"
+            out[key + "/confidence"], out[key + "/flags"] = c, f
+            if name == "base":
+                assert np.array_equal(c, bgold[f"{seq}/confidence"]), f"{seq} base != golden"
+            sp, nflip = spread(bres["base"], bres[name])
+            out[key + "/spread"], out[key + "/flag_flips"] = np.array(sp), np.array(nflip)
+            print(f"{key:32s} max rel confidence diff vs base {sp:.3e}  flag flips {nflip}", flush=True)
+    out["branch_seqs"] = np.array(["long", "low_score", "uncertain_threshold", "distractor_far"])
+    out["branch_variants"] = np.array(list(bvars))
     np.savez_compressed(os.path.join(HERE, "dimp_spread.npz"), **out)
 
 

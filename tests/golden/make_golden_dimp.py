@@ -370,6 +370,7 @@ def stages_fixture(wnet, n_frames=6):
     tr.features_initialized = True
     cap = {"bb_in": [], "bb_out": [], "clf": [], "scores": []}
     eb, gcf, ct = wnet.extract_backbone, tr.get_classification_features, tr.classify_target
+    ebf = tr.extract_backbone_features
     fi = net.classifier.filter_initializer
     fo = net.classifier.filter_optimizer
     fi_fwd, fo_fwd = fi.forward, fo.forward
@@ -383,6 +384,11 @@ def stages_fixture(wnet, n_frames=6):
     def clf_feat(f):
         r = gcf(f)
         cap["clf"].append(r.clone())
+        return r
+
+    def backbone_feat(*a, **k):
+        r = ebf(*a, **k)
+        cap.setdefault("coords", []).append(r[1][0].float().clone())
         return r
 
     def classify(x):
@@ -405,6 +411,7 @@ def stages_fixture(wnet, n_frames=6):
         return r
     wnet.extract_backbone = extract
     tr.get_classification_features, tr.classify_target = clf_feat, classify
+    tr.extract_backbone_features = backbone_feat
     fi.forward, fo.forward = init_fwd, opt_fwd
     try:
         frames, _ = synth.make_frames(SEQ["seed"], SEQ["n"], SEQ["H"], SEQ["W"], SEQ["C"], box=SEQ["box"])
@@ -433,6 +440,11 @@ def stages_fixture(wnet, n_frames=6):
             sc, fu = cap["scores"][t - 1]
             res[f"f{t}_scores"] = sc.numpy()
             res[f"f{t}_filter"] = fu.numpy()
+            # the sample the frame localised in and the state after it (dimp.py:107-131)
+            res[f"f{t}_coords"] = cap["coords"][t - 1].numpy()
+            res[f"f{t}_state"] = np.array([*tr.pos.tolist(), *tr.target_sz.tolist(), float(tr.target_scale)],
+                                          dtype=np.float64)
+            res[f"f{t}_flag"] = np.array(tr.debug_info["flag"])
         res["confidence"] = np.array(conf)
         gold = np.load(os.path.join(HERE, "tracker_dimp.npz"))
         assert np.array_equal(res["confidence"], gold["confidence"][1:n_frames + 1]), "stage run != tracker golden"

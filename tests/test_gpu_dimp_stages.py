@@ -20,6 +20,7 @@ def rel(a, b):
 
 def run_stages(precision, n_frames=6):
     """The HIP tracker on the golden sequence with its stages captured (monkeypatched hooks, same call order)."""
+    from mmtrack_amd import _lib
     from mmtrack_amd import dimp as mdimp
     from mmtrack_amd import synth
     from mmtrack_amd.dimp_tracker import DiMP, parameters
@@ -70,7 +71,17 @@ def run_stages(precision, n_frames=6):
     try:
         torch.manual_seed(tseed)
         tr.initialize(frames[0], {"init_bbox": list(gd["init_box"])})
-        conf = [tr.track(frames[t])["confidence"] for t in range(1, n_frames + 1)]
+        conf = []
+        for t in range(1, n_frames + 1):
+            conf.append(tr.track(frames[t])["confidence"])
+            pool = tr.pool
+            st = _lib.MmtDimpState.from_buffer_copy(bytes(
+                pool.states[tr.slot * pool.sbytes:(tr.slot + 1) * pool.sbytes].cpu().numpy()))
+            rr = _lib.MmtDimpResult.from_buffer_copy(bytes(
+                pool.results[tr.slot * pool.rbytes:(tr.slot + 1) * pool.rbytes].cpu().numpy()))
+            cap.setdefault("state", []).append([st.pos[0], st.pos[1], st.target_sz[0], st.target_sz[1],
+                                                st.target_scale])
+            cap.setdefault("sample", []).append([rr.sample_pos[0], rr.sample_pos[1], rr.sample_scale])
     finally:
         mdimp.apply_filter = af
     return cap, conf
@@ -104,6 +115,14 @@ def stage_errors(cap, conf, g, n_frames=6):
         out.append((f"frame {t} filter used", rel(fu, g[f"f{t}_filter"])))
         out.append((f"frame {t} scores", rel(sc.reshape(g[f"f{t}_scores"].shape), g[f"f{t}_scores"])))
         out.append((f"frame {t} confidence", rel(conf[t - 1], g["confidence"][t - 1])))
+        if f"f{t}_state" in g:
+            c = g[f"f{t}_coords"]   # the reference's sample: coords (y0, x0, y1, x1) -> centre and scale
+            ref_sp = [0.5 * (c[0] + c[2] - 1), 0.5 * (c[1] + c[3] - 1)]
+            out.append((f"frame {t} sample centre (px, abs)", float(np.abs(np.array(cap["sample"][t - 1][:2]) -
+                                                                            np.array(ref_sp)).max())))
+            out.append((f"frame {t} state pos (px, abs)", float(np.abs(np.array(cap["state"][t - 1][:2]) -
+                                                                        g[f"f{t}_state"][:2]).max())))
+            out.append((f"frame {t} state size / scale", rel(cap["state"][t - 1][2:], g[f"f{t}_state"][2:])))
     return out
 
 

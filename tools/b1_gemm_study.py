@@ -40,6 +40,43 @@ for name in os.environ.get("SHAPES", "qkv,fc1,fc2,proj").split(","):
                               C.data_ptr() if epi == 2 else None, N if epi == 2 else 0, M, N, K, epi, 1e-3, 1.0,
                               0, 0, s)
     st = torch.zeros(1 << 16, dtype=torch.int64, device="cuda")
+    scratch = torch.empty(2, device="cuda")
+    # "mall": each launch's weight copy read by another kernel (torch.sum, its own XCD placement) just before the
+    # GEMM, which then finds it in the Infinity Cache and mostly not in its XCD's L2 -- what a prefetch of the next
+    # GEMM's weights on a side stream would give; timed per launch with events around the GEMM alone
+    for mode in ("mall",):
+        for k in range(ncopy):
+            run(k)
+        flush.fill_(1)
+        ts = []
+        for i in range(2 * ncopy):
+            k = i % ncopy
+            scratch[0] = torch.sum(Wh[k], dtype=torch.float32)
+            scratch[1] = torch.sum(Wl[k], dtype=torch.float32)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            run(k)
+            e1.record()
+            ts.append((e0, e1))
+        torch.cuda.synchronize()
+        us = sorted(a.elapsed_time(b) * 1e3 for a, b in ts)
+        print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "mode": mode,
+                          "cfg": os.environ.get("MMT_SPLIT_CFG", "-1"), "us_median": round(us[len(us) // 2], 2),
+                          "us_min": round(us[0], 2)}), flush=True)
+        # the same single-launch event timing in the cold and warm states, for comparison
+        for sub in ("cold", "warm"):
+            ts = []
+            for i in range(2 * ncopy):
+                k = i % ncopy if sub == "cold" else 0
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                run(k)
+                e1.record()
+                ts.append((e0, e1))
+            torch.cuda.synchronize()
+            us = sorted(a.elapsed_time(b) * 1e3 for a, b in ts)
+            print(json.dumps({"shape": name, "mode": sub + "_single", "us_median": round(us[len(us) // 2], 2),
+                              "us_min": round(us[0], 2)}), flush=True)
     for mode in ("cold", "warm"):
         for k in range(ncopy):
             run(k)
