@@ -179,16 +179,6 @@ struct mmt_engine {
   std::map<std::tuple<int, int, std::string>, GraphEntry> graphs;
   std::unique_ptr<TimingProbe> probe;
 
-  // weight prefetch (launches of <= prefetch_max sequences): at the start of layer i a side stream reads layer
-  // i + 1's weights (at the last layer: the head's; at the head: the next frame's patch embedding and layer 0) so
-  // the GEMMs find them in the Infinity Cache instead of streaming them cold from HBM (the hi + lo weights, 372 MB,
-  // do not fit it: a frame-after-frame replay evicts every layer before its next use)
-  struct WRange { size_t off = 0, bytes = 0; };
-  WRange wr_layer[DEPTH], wr_head, wr_front;
-  int prefetch_max = 0, prefetch_blocks = 32;
-  hipStream_t pf_stream = nullptr;
-  hipEvent_t pf_ev[DEPTH + 1] = {}, pf_done = nullptr;
-
   int fail(int code, const std::string& m) {
     err = m;
     return code;
@@ -486,11 +476,9 @@ int pack_weights(mmt_engine* e) {
       TRY(upload_f32(e, &w.fold, f));
     }
   }
-  e->wr_front = {0, e->wused};
   for (int i = 0; i < DEPTH; ++i) {
     const std::string p = "backbone.blocks." + std::to_string(i) + ".";
     LayerW& w = e->lw[i];
-    const size_t layer0 = e->wused;
     TRY(upload_w(e, &w.qkv_w, &w.qkv_wl, H(e, p + "attn.qkv.weight"), &w.qkv_s));
     TRY(upload_f32(e, &w.qkv_b, H(e, p + "attn.qkv.bias")));
     TRY(upload_w(e, &w.proj_w, &w.proj_wl, H(e, p + "attn.proj.weight"), &w.proj_s));
@@ -513,9 +501,7 @@ int pack_weights(mmt_engine* e) {
     TRY(upload_f32(e, &w.n1b, H(e, p + "norm1.bias")));
     TRY(upload_f32(e, &w.n2w, H(e, p + "norm2.weight")));
     TRY(upload_f32(e, &w.n2b, H(e, p + "norm2.bias")));
-    e->wr_layer[i] = {layer0, e->wused - layer0};
   }
-  const size_t head0 = e->wused;
   TRY(upload_f32(e, &e->norm_w, H(e, "backbone.norm.weight")));
   TRY(upload_f32(e, &e->norm_b, H(e, "backbone.norm.bias")));
   // head
@@ -559,7 +545,6 @@ int pack_weights(mmt_engine* e) {
     TRY(upload_f32(e, &e->b5, b5));
   }
   TRY(upload_f32(e, &e->hann, H(e, "output_window")));
-  e->wr_head = {head0, e->wused - head0};
   return MMT_OK;
 }
 
@@ -794,14 +779,6 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
   const bool vipt = c.model == MMT_MODEL_VIPT;
   const bool prompted = vipt && c.prompt_type != MMT_PROMPT_NONE;
   const bool deep = vipt && c.prompt_type == MMT_PROMPT_DEEP;
-  // weight prefetch on the side stream, forked at event k of this launch (see mmt_engine::prefetch_max)
-  const bool pf = e->prefetch_max > 0 && n <= e->prefetch_max && e->pf_stream && e->split;
-  auto prefetch_at = [&](int k, const mmt_engine::WRange& r) {
-    if (!pf || !r.bytes) return;
-    hipEventRecord(e->pf_ev[k], s);
-    hipStreamWaitEvent(e->pf_stream, e->pf_ev[k], 0);
-    prefetch(static_cast<const char*>(e->warena) + r.off, r.bytes, e->prefetch_blocks, e->pf_stream);
-  };
   bf16_t* A_rgb = e->A_rgb + (size_t)b0 * L * C;
   bf16_t* A_aux = e->A_aux + (size_t)b0 * L * C;
   bf16_t* A_rgb_l = off(e->A_rgb_l, (size_t)b0 * L * C);
@@ -883,7 +860,6 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
     const LayerW& w = e->lw[i];
     const int Na = Lz + Ls;
     int ln_mode = (prompted && i == 0) ? 1 : 0;
-    prefetch_at(i, i + 1 < DEPTH ? e->wr_layer[i + 1] : e->wr_head);
     if (deep && i >= 1) {  // vit_ce_prompt.py:268-310
       set_prompt(i, i - 1);
       pa.srcA = X;
@@ -994,8 +970,6 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
   final_norm_recover(X, Lz + Ls, q_slot2pos, e->norm_w, e->norm_b, n, Lz, Lx, q_feat, q_feat_l, e->feat_s,
                      q_dbg_feat, s, pend);
 
-  // the next frame's patch embedding and layer 0 (the launches of a sequence follow each other)
-  prefetch_at(DEPTH, mmt_engine::WRange{0, e->wr_layer[0].off + e->wr_layer[0].bytes});
   // CENTER head: conv1 of the three branches fused (N = 3*hc), then per-branch grouped convs
   const int hc = c.head_channels, fs = e->fs, M = n * Lx;
   {
@@ -1064,10 +1038,6 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
     da.row0 = r0;
   }
   decode(da, s);
-  if (pf) {   // join the side stream (a captured graph must end on the origin stream)
-    hipEventRecord(e->pf_done, e->pf_stream);
-    hipStreamWaitEvent(s, e->pf_done, 0);
-  }
 }
 
 // crop geometry of processing_utils.py:32-41 in doubles with Python rounding (round half to even)
@@ -1250,12 +1220,6 @@ int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
     if (hipEventCreateWithFlags(&je, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
   if (hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming) != hipSuccess)
     return MMT_E_HIP;
-  if (hipStreamCreateWithFlags(&e->pf_stream, hipStreamNonBlocking) != hipSuccess) return MMT_E_HIP;
-  for (auto& ev : e->pf_ev)
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
-  if (hipEventCreateWithFlags(&e->pf_done, hipEventDisableTiming) != hipSuccess) return MMT_E_HIP;
-  if (const char* pv = std::getenv("MMT_PREFETCH")) e->prefetch_max = std::atoi(pv);
-  if (const char* pb = std::getenv("MMT_PREFETCH_BLOCKS")) e->prefetch_blocks = std::max(1, std::atoi(pb));
   // f16x3 GEMMs are 3x longer, so halves of 16 sequences still fill the chip and the two streams fill each
   // other's tile-quantisation tails (+8 % at 32 sequences; plain bf16 lost 4 % there)
   if (e->split) e->overlap_min = 32;
@@ -1306,13 +1270,6 @@ void mmt_destroy(mmt_engine* e) {
     if (ev) hipEventDestroy(ev);
   if (e->frame_ev) hipEventDestroy(e->frame_ev);
   if (e->fork_ev) hipEventDestroy(e->fork_ev);
-  if (e->pf_stream) {
-    hipStreamSynchronize(e->pf_stream);
-    hipStreamDestroy(e->pf_stream);
-  }
-  for (auto& ev : e->pf_ev)
-    if (ev) hipEventDestroy(ev);
-  if (e->pf_done) hipEventDestroy(e->pf_done);
   for (auto& je : e->join_ev)
     if (je) hipEventDestroy(je);
   delete e;

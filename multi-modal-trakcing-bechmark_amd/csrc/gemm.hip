@@ -617,6 +617,50 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
       }
     __syncthreads();
     LT::template drain<BM, T::NT, RPRE>(lds, g, args, m0, n0, M, rpre);
+  } else if constexpr (SPLIT && epi_is_bf16(EPI) && 2 * BM * BN * 2 <= T::NSTAGE * T::STAGE * 2) {
+    // split 16-bit outputs (one-sequence qkv / fc1, the head convs): the tile's hi and lo planes staged in the LDS,
+    // then whole 16-B row chunks per lane (fragment-shaped stores write 16 rows x 32 B per wave-instruction; the
+    // staged drain, whole 128-B lines: the 256 x 256 kernel's epilogue 35k -> see gemm256s_kernel).  Same bits.
+    using LT = LdsTile<EPI_BF16, BN>;
+    char* const planeH = reinterpret_cast<char*>(smem);
+    char* const planeL = planeH + BM * BN * 2;
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj) {
+        const int row = wm * T::WM + i * 16 + (lane & 15);
+        const int col = wn * T::WN + jj * 16 + (lane >> 4) * 4;
+        const f32x4& a = acc[i][jj];
+        const float4 bv = bq[jj];
+        float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
+        if (EPI == EPI_GELU_BF16)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+        if (EPI == EPI_RELU_BF16)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        uint16_t hh[4], ll[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split_h(v[e] * g.out_scale, hh[e], ll[e]);
+        const int o = LT::off(row, col);
+        *reinterpret_cast<uint2*>(planeH + o) =
+            make_uint2((uint32_t)hh[0] | ((uint32_t)hh[1] << 16), (uint32_t)hh[2] | ((uint32_t)hh[3] << 16));
+        *reinterpret_cast<uint2*>(planeL + o) =
+            make_uint2((uint32_t)ll[0] | ((uint32_t)ll[1] << 16), (uint32_t)ll[2] | ((uint32_t)ll[3] << 16));
+      }
+    __syncthreads();
+    const int rows = max(0, min(BM, M - m0));
+    const rsrc_t rC = make_rsrc(static_cast<bf16_t*>(g.C) + (int64_t)m0 * g.ldc, (int64_t)rows * g.ldc * 2);
+    const rsrc_t rCl = make_rsrc(static_cast<bf16_t*>(g.C_lo) + (int64_t)m0 * g.ldc, (int64_t)rows * g.ldc * 2);
+    static_assert((BM * LT::NCH) % T::NT == 0, "uniform drain");
+#pragma unroll
+    for (int it = 0; it < BM * LT::NCH / T::NT; ++it) {
+      const int idx = tid + it * T::NT, r = idx / LT::NCH, c = idx - r * LT::NCH;
+      const int lo = r * BN * 2 + ((c ^ (r & LT::MASK)) << 4);
+      const uint32_t go = r < rows ? (uint32_t)(((int64_t)r * g.ldc + n0 + c * 8) * 2) : kBufOob;
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(planeH + lo), rC, go, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(planeL + lo), rCl, go, 0, 0);
+    }
   } else {
     const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
     // (the residual chunks of the 32-fragment tiles -- 256 x 256 tuning configs -- would need 128 more VGPRs:
@@ -1416,6 +1460,70 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
   GEMM_STAMP(2);
 
   constexpr int QA[4] = {0, 0, 1, 1}, QB[4] = {0, 1, 1, 0};
+  if constexpr (epi_is_bf16(EPI)) {
+    // 16-bit outputs (qkv, fc1): per 128-row half, the hi and lo planes of the half go to the LDS (64 KB each, the
+    // whole staging array), then every lane stores whole 16-B row chunks, eight lanes per 128-B line.  Stored straight
+    // from the fragments, a wave-instruction wrote 16 rows x 32 B and the epilogue took ~35k of a tile's ~145k
+    // cycles (round-5 phase stamps, tools/gemm256s_phases.py); same values, same bits.
+    using LT = LdsTile<EPI_BF16, 256>;   // [128][256] 16-bit, 16-B chunks XOR-swizzled by row
+    char* const planeH = reinterpret_cast<char*>(smem);
+    char* const planeL = planeH + 128 * 256 * 2;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();   // h = 0: every wave's last fragment reads are done; h = 1: the first half is drained
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        if (QA[qd] != h) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int row = wr * 64 + i * 16 + (lane & 15);
+            const int col = QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4;
+            const f32x4& a = acc[qd][i][jj];
+            const float4 bv = bq[QB[qd]][jj];
+            float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
+            if (EPI == EPI_GELU_BF16)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+            if (EPI == EPI_RELU_BF16)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            uint16_t hh[4], ll[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) split_h(v[e] * g.out_scale, hh[e], ll[e]);
+            const int o = LT::off(row, col);
+            *reinterpret_cast<uint2*>(planeH + o) =
+                make_uint2((uint32_t)hh[0] | ((uint32_t)hh[1] << 16), (uint32_t)hh[2] | ((uint32_t)hh[3] << 16));
+            *reinterpret_cast<uint2*>(planeL + o) =
+                make_uint2((uint32_t)ll[0] | ((uint32_t)ll[1] << 16), (uint32_t)ll[2] | ((uint32_t)ll[3] << 16));
+          }
+      }
+      __syncthreads();
+      // 128 rows x 32 chunks per plane; rows past M fall outside the C resources (zero-sized tail) and are dropped
+      const int rows = max(0, min(128, M - (m0 + h * 128)));
+      const rsrc_t rC = make_rsrc(static_cast<bf16_t*>(g.C) + (int64_t)(m0 + h * 128) * g.ldc, (int64_t)rows * g.ldc * 2);
+      const rsrc_t rCl = make_rsrc(static_cast<bf16_t*>(g.C_lo) + (int64_t)(m0 + h * 128) * g.ldc,
+                                   (int64_t)rows * g.ldc * 2);
+#pragma unroll
+      for (int it = 0; it < 128 * 32 / 512; ++it) {
+        const int idx = tid + it * 512, r = idx >> 5, c = idx & 31;
+        const int lo = r * 512 + ((c ^ (r & 15)) << 4);
+        const uint32_t go = r < rows ? (uint32_t)(((int64_t)r * g.ldc + n0 + c * 8) * 2) : kBufOob;
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(planeH + lo), rC, go, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(planeL + lo), rCl, go, 0, 0);
+      }
+    }
+    GEMM_STAMP(3);
+#ifdef GEMM_PHASE_STAMPS
+    __syncthreads();
+    if (gemm_stamps_ && blockIdx.x < 256)
+      for (int e = threadIdx.x; e < 2 * PS_PH; e += 512)
+        gemm_stamps_[65536 + (size_t)blockIdx.x * 2 * PS_PH + e] = pst[e];
+#endif
+    return;
+  }
   // (the residual epilogues, not used by the path's launches, keep the per-fragment store4)
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll

@@ -340,30 +340,4 @@ void xcorr_nhwc(const float* Z, int64_t z_bstride, const float* X, float* out, i
                      z_bstride, X, out, C, hz, wz, hx, wx, scale, bias);
 }
 
-// ------------------------------------------------------------------ weight prefetch
-// Each thread streams 16-B chunks of [p, p + bytes) with eight loads in flight; the values go to an empty asm
-// sink (nothing is stored).  Plain (default-policy) loads: the lines stay in the Infinity Cache for the GEMMs of
-// the next layer, which run a few tens of microseconds later.
-__global__ __launch_bounds__(256) void prefetch_kernel(const void* __restrict__ p, uint32_t bytes) {
-  // raw buffer loads: a chunk past the end is an out-of-range offset that reads zeros, so no load sits behind a
-  // branch (the compiler would wait for each one in place)
-  const rsrc_t r = make_rsrc(p, bytes);
-  const uint32_t stride = gridDim.x * 256u * 16u;
-  for (uint32_t o = (blockIdx.x * 256u + threadIdx.x) * 16u; o < bytes; o += 8u * stride) {
-    u32x4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t ok = o + k * stride;
-      v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, ok < bytes ? ok : kBufOob, 0, 0));
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(v[k][0]));
-  }
-}
-
-void prefetch(const void* p, size_t bytes, int blocks, hipStream_t s) {
-  if (!p || bytes < 16 || blocks <= 0) return;
-  hipLaunchKernelGGL(prefetch_kernel, dim3(blocks), dim3(256), 0, s, p, (uint32_t)std::min<size_t>(bytes, 0xFFFF0000u));
-}
-
 }  // namespace mmt

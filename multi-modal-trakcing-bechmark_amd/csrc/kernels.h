@@ -243,9 +243,6 @@ struct DecodeArgs {
   int ring_pitch, row0;
 };
 void decode(const DecodeArgs& a, hipStream_t s);
-// reads [p, p + bytes) and discards it, so the next launches find those bytes in the Infinity Cache (one-sequence
-// frames: the 372 MB of hi + lo weights do not fit it and would otherwise stream cold from HBM); imaging.hip
-void prefetch(const void* p, size_t bytes, int blocks, hipStream_t s);
 
 // ---------------------------------------------------------------- SiamFC / DiMP correlation
 // out[b][y][x] = scale * sum_{c,i,j} X[b][c][y+i][x+j] * Z[b][c][i][j] + bias   (valid, fp32)
