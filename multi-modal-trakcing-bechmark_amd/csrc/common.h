@@ -139,6 +139,30 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return x >= 0.f ? x - xh : xh;
 }
 
+// gelu_erf on a pair, in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of FMA per instruction; the
+// reciprocal and exp2 stay per element): the same operations in the same order, element by element, for the
+// VALU-bound GELU epilogue of fc1 (half the FMA issue slots)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 u = __builtin_elementwise_abs(x) * (f32x2)0.70710678118654752440f;
+  const f32x2 d = __builtin_elementwise_fma((f32x2)0.5f, u, (f32x2)1.0f);
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 q = (f32x2)0.246517298f;
+  q = __builtin_elementwise_fma(q, t, (f32x2)-1.18611495f);
+  q = __builtin_elementwise_fma(q, t, (f32x2)2.14747446f);
+  q = __builtin_elementwise_fma(q, t, (f32x2)-1.63775315f);
+  q = __builtin_elementwise_fma(q, t, (f32x2)0.402321582f);
+  q = __builtin_elementwise_fma(q, t, (f32x2)-0.26875686f);
+  q = __builtin_elementwise_fma(q, t, (f32x2)0.139630057f);
+  q = __builtin_elementwise_fma(q, t, (f32x2)0.539700616f);
+  q = __builtin_elementwise_fma(q, t, (f32x2)1.4427292f);
+  q = __builtin_elementwise_fma(q, t, (f32x2)-2.82574822f);
+  const f32x2 a = __builtin_elementwise_fma((f32x2)-1.44269504f * u, u, q);
+  const f32x2 h = t * f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  const f32x2 xh = x * h;
+  return f32x2{x.x >= 0.f ? x.x - xh.x : xh.x, x.y >= 0.f ? x.y - xh.y : xh.y};
+}
+
 // bf16-output GELU: the same erf GELU with erfc from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 on
 // erf, five coefficients; 1/2 and log2(e) folded as above), written as
 //   GELU(x) = relu(x) - |x| * h(|x|),   h(a) = t p(t) 2^(-x^2 log2(e) / 2),  t = 1 / (1 + 0.3275911 a / sqrt2)

@@ -633,9 +633,13 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
         const f32x4& a = acc[i][jj];
         const float4 bv = bq[jj];
         float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
-        if (EPI == EPI_GELU_BF16)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+        if (EPI == EPI_GELU_BF16) {
+          const f32x2 g0 = gelu_erf2(f32x2{v[0], v[1]}), g1 = gelu_erf2(f32x2{v[2], v[3]});
+          v[0] = g0.x;
+          v[1] = g0.y;
+          v[2] = g1.x;
+          v[3] = g1.y;
+        }
         if (EPI == EPI_RELU_BF16)
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -1484,9 +1488,13 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
             const f32x4& a = acc[qd][i][jj];
             const float4 bv = bq[QB[qd]][jj];
             float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
-            if (EPI == EPI_GELU_BF16)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+            if (EPI == EPI_GELU_BF16) {
+              const f32x2 g0 = gelu_erf2(f32x2{v[0], v[1]}), g1 = gelu_erf2(f32x2{v[2], v[3]});
+              v[0] = g0.x;
+              v[1] = g0.y;
+              v[2] = g1.x;
+              v[3] = g1.y;
+            }
             if (EPI == EPI_RELU_BF16)
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);

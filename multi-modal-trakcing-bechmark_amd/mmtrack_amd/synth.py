@@ -253,7 +253,14 @@ def make_frames(seed: int, n: int, H: int = 480, W: int = 640, C: int = 6,
     gts = np.empty((n, 4), dtype=np.float64)
     yy = np.arange(H, dtype=np.float32)[:, None]
     xx = np.arange(W, dtype=np.float32)[None, :]
-    x, y, w, h = box
+    # Python floats: a NumPy float64 box (e.g. read back from a golden .npz) would turn the float32 mask arithmetic
+    # below into float64 (NEP 50 promotion) and move a few pixels of some frames by one level -- the goldens were made
+    # from Python floats, so every caller must see these frames (round 5: the DiMP tests had compared the tracker on
+    # frames that differed from the reference's at a few pixels of frames 2+)
+    x, y, w, h = (float(v) for v in box)
+    drift = (float(drift[0]), float(drift[1]))
+    if distractor is not None:
+        distractor = tuple(float(v) for v in distractor)
     for t in range(n):
         cx = x + 0.5 * w + drift[0] * t + 6.0 * math.sin(0.21 * t)
         cy = y + 0.5 * h + drift[1] * t + 4.0 * math.cos(0.17 * t)
