@@ -327,6 +327,24 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
 #pragma unroll
     for (int jj = 0; jj < T::FN; ++jj) bq[jj] = epi_bias(rB, n0 + wn * T::WN + jj * 16 + (lane >> 4) * 4);
   }
+  // split fp32 outputs (fc2 / proj residual updates, the patch embedding, the head's last conv): the tile goes through
+  // the LDS and leaves as whole 16-B row chunks, the residual chunks of that drain requested here (raw buffer loads,
+  // rows past M read zeros) so their round trip hides under the main loop instead of opening the epilogue
+  constexpr bool SF32 = SPLIT && (EPI == EPI_RESID_F32 || EPI == EPI_F32 || EPI == EPI_POS_F32 || EPI == EPI_RELU_F32) &&
+                        BM * BN * 4 <= T::NSTAGE * T::STAGE * 2 && (BM * (BN / 4)) % T::NT == 0;
+  constexpr int SF_N = SF32 ? BM * (BN / 4) / T::NT : 1;   // drain chunks per thread
+  constexpr bool SF_R = SF32 && epi_has_r(EPI);
+  u32x4 rsf[SF_R ? SF_N : 1];
+  if constexpr (SF_R) {
+    const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
+#pragma unroll
+    for (int k = 0; k < SF_N; ++k) {
+      const int idx = tid + k * T::NT, r = idx / (BN / 4), c = idx - r * (BN / 4), m = m0 + r;
+      const int row = EPI == EPI_POS_F32 ? m % args.pos_rows : m;
+      const uint32_t o = m < M ? (uint32_t)(((int64_t)row * g.ldr + n0 + 4 * c) * 4) : kBufOob;
+      rsf[k] = __builtin_amdgcn_raw_buffer_load_b128(rR, o, 0, 0);
+    }
+  }
 
   // ---- loads: buffer_load ... lds with per-lane VGPR offsets fixed over K and the K advance in the
   // SGPR soffset; rows past M fall outside the A resource and read as zero.  Row block i of the
@@ -617,6 +635,32 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
       }
     __syncthreads();
     LT::template drain<BM, T::NT, RPRE>(lds, g, args, m0, n0, M, rpre);
+  } else if constexpr (SF32) {
+    using LF = LdsTile<EPI_F32, BN>;   // fp32 [BM][BN], 16-B chunks XOR-swizzled by row
+    char* const lds = reinterpret_cast<char*>(smem);
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < T::FN; ++jj) {
+        const f32x4& a = acc[i][jj];
+        const float4 bv = bq[jj];
+        float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
+        if (EPI == EPI_RELU_F32)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        LF::put(lds, wm * T::WM + i * 16 + (lane & 15), wn * T::WN + jj * 16 + (lane >> 4) * 4, v);
+      }
+    __syncthreads();
+    const int rows = max(0, min(BM, M - m0));
+    const rsrc_t rC = make_rsrc(static_cast<float*>(g.C) + (int64_t)m0 * g.ldc, (int64_t)rows * g.ldc * 4);
+#pragma unroll
+    for (int k = 0; k < SF_N; ++k) {
+      const int idx = tid + k * T::NT, r = idx / (BN / 4), c = idx - r * (BN / 4);
+      f32x4 v = *reinterpret_cast<const f32x4*>(lds + r * BN * 4 + ((c ^ (r & LF::MASK)) << 4));
+      if constexpr (SF_R) v = __builtin_bit_cast(f32x4, rsf[k]) + v;   // R + (acc * inv + bias), as store4v
+      const uint32_t go = r < rows ? (uint32_t)(((int64_t)r * g.ldc + n0 + 4 * c) * 4) : kBufOob;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rC, go, 0, 0);
+    }
   } else if constexpr (SPLIT && epi_is_bf16(EPI) && 2 * BM * BN * 2 <= T::NSTAGE * T::STAGE * 2) {
     // split 16-bit outputs (one-sequence qkv / fc1, the head convs): the tile's hi and lo planes staged in the LDS,
     // then whole 16-B row chunks per lane (fragment-shaped stores write 16 rows x 32 B per wave-instruction; the
@@ -1378,12 +1422,22 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
       Bl[jj] = *reinterpret_cast<const bf16x8*>(S + 4096 + swzk<32>(row, c));
     }
   };
-  auto mma = [&](f32x4 (&C)[4][2], const bf16x8 (&Bh)[2], const bf16x8 (&Bl)[2]) {
+#ifndef GEMM256S_DMA_IN_MFMA
+#define GEMM256S_DMA_IN_MFMA 0
+#endif
+  // mid(): GEMM256S_DMA_IN_MFMA (tuning build) issues the phase's half-tile loads after the first eight MFMAs instead
+  // of before the phase barrier, so their issue cost leaves the fragment-read side of the ping-pong
+  auto mma = [&](f32x4 (&C)[4][2], const bf16x8 (&Bh)[2], const bf16x8 (&Bl)[2], auto mid) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bh[jj], Ah[i], C[i][jj]);
+    if constexpr (GEMM256S_DMA_IN_MFMA) {
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1408,36 +1462,48 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
     read_a(S);
     PSTAMP(3 * P0);
     if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0, 0));
-    if (STEADY || P0 + 6 < NL) issue(P0 + 6, std::integral_constant<int, 2>{});
+    auto ld0 = [&]() {
+      if (STEADY || P0 + 6 < NL) issue(P0 + 6, std::integral_constant<int, 2>{});
+    };
+    if constexpr (!GEMM256S_DMA_IN_MFMA) ld0();
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 1);
-    mma(acc[0], B0h, B0l);
+    mma(acc[0], B0h, B0l, ld0);
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 2);
     read_b(S + 2 * 8192, B1h, B1l);
     PSTAMP(3 * P0 + 3);
     if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 1, 1));
-    if (STEADY || P0 + 7 < NL) issue(P0 + 7, std::integral_constant<int, 3>{});
+    auto ld1 = [&]() {
+      if (STEADY || P0 + 7 < NL) issue(P0 + 7, std::integral_constant<int, 3>{});
+    };
+    if constexpr (!GEMM256S_DMA_IN_MFMA) ld1();
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 4);
-    mma(acc[1], B1h, B1l);
+    mma(acc[1], B1h, B1l, ld1);
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 5);
     read_a(S + 3 * 8192);
     PSTAMP(3 * P0 + 6);
     if (STEADY) asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); else wait_vm(n_after(P0 + 2, 2));
-    if (STEADY || P0 + 8 < NL) issue(P0 + 8, std::integral_constant<int, 0>{});
+    auto ld2 = [&]() {
+      if (STEADY || P0 + 8 < NL) issue(P0 + 8, std::integral_constant<int, 0>{});
+    };
+    if constexpr (!GEMM256S_DMA_IN_MFMA) ld2();
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 7);
-    mma(acc[2], B1h, B1l);
+    mma(acc[2], B1h, B1l, ld2);
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 8);
     PSTAMP(3 * P0 + 9);
     if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 3, 3));
-    if (STEADY || P0 + 9 < NL) issue(P0 + 9, std::integral_constant<int, 1>{});
+    auto ld3 = [&]() {
+      if (STEADY || P0 + 9 < NL) issue(P0 + 9, std::integral_constant<int, 1>{});
+    };
+    if constexpr (!GEMM256S_DMA_IN_MFMA) ld3();
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 10);
-    mma(acc[3], B0h, B0l);
+    mma(acc[3], B0h, B0l, ld3);
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 11);
   };

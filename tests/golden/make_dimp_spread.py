@@ -17,9 +17,8 @@ in variants that differ only in rounding:
 * ``bb64``      -- both ResNet-50 backbones in float64, cast to float32 after the max merge: the reference's own
                    fp32 summation-order error of its features removed (an exact-arithmetic backbone);
 * ``all64``     -- bb64 + clf64 + opt64.
-Then, for the branch sequences of tracker_dimp_branches.npz with the most filter updates (long, low_score,
-uncertain_threshold, distractor_far): base, the backbone noise at 3e-6 / 1e-5 over four seeds, and bb64, stored as
-"<seq>:<variant>/...".
+Then, for every branch sequence of tracker_dimp_branches.npz: base, bb64, and the backbone noise at 3e-6 / 1e-5
+(two seeds), stored as "<seq>:<variant>/...".
 For every variant the per-frame confidences, boxes and flags are stored; the spread of a variant is its largest
 relative confidence difference to ``base`` over the frames whose flags agree.
 
@@ -189,11 +188,10 @@ def main():
     out["names"] = np.array(list(variants))
     # the branch sequences with the most Gauss-Newton updates / the largest HIP-vs-reference confidence drift in the
     # round-4 runs (tracker_dimp_branches.npz): base + fp32-level backbone noise over several seeds + the exact backbone
-    bvars = {"base": {}, "feat3e-6": dict(feat_noise=3e-6), "feat1e-5": dict(feat_noise=1e-5),
-             "feat1e-5_s2": dict(feat_noise=1e-5, noise_seed=99), "feat1e-5_s3": dict(feat_noise=1e-5, noise_seed=7),
-             "feat1e-5_s4": dict(feat_noise=1e-5, noise_seed=4242), "bb64": dict(bb64=True)}
+    bvars = {"base": {}, "bb64": dict(bb64=True), "feat3e-6": dict(feat_noise=3e-6), "feat1e-5": dict(feat_noise=1e-5),
+             "feat1e-5_s2": dict(feat_noise=1e-5, noise_seed=99)}
     bgold = np.load(os.path.join(HERE, "tracker_dimp_branches.npz"))
-    for seq in (["long", "low_score", "uncertain_threshold", "distractor_far"] if not only else []):
+    for seq in (list(mgd.BRANCH_SEQS) if not only else []):
         bres = {}
         for name, kw in bvars.items():
             b, c, f = run_tracker(wnet, seq=seq, **kw)
@@ -205,7 +203,7 @@ def main():
             sp, nflip = spread(bres["base"], bres[name])
             out[key + "/spread"], out[key + "/flag_flips"] = np.array(sp), np.array(nflip)
             print(f"{key:32s} max rel confidence diff vs base {sp:.3e}  flag flips {nflip}", flush=True)
-    out["branch_seqs"] = np.array(["long", "low_score", "uncertain_threshold", "distractor_far"])
+    out["branch_seqs"] = np.array(list(mgd.BRANCH_SEQS))
     out["branch_variants"] = np.array(list(bvars))
     np.savez_compressed(os.path.join(HERE, "dimp_spread.npz"), **out)
 

@@ -9,6 +9,10 @@ tail -1 $O/gpu_suite.txt
 grep -E "max confidence rel|relative confidence differences|teacher-forced per-step|per-frame IoU" $O/gpu_suite.txt | cut -c1-300
 grep -E "^\[(f16x3|fp32)\] (filter after (7|8|10)|frame [1-6] confidence)" $O/gpu_suite.txt
 rm -f gpurun_out/ab.log
-LIBDIR=abx2 ROUNDS=3 STEPS=60 bash tools/ab_bench.sh > $O/ab_b32.txt 2>&1 || { tail -5 $O/ab_b32.txt; exit 1; }
-cp gpurun_out/ab.log $O/ab_b32.log
+LIBDIR=abx3 ROUNDS=3 STEPS=60 bash tools/ab_bench.sh > $O/ab_b32.txt 2>&1 || { tail -5 $O/ab_b32.txt; exit 1; }
+cp gpurun_out/ab.log $O/ab_b32.log; rm -f gpurun_out/ab.log
+LIBDIR=abx3 ROUNDS=3 STEPS=300 ARGS="--batch 1" bash tools/ab_bench.sh > $O/ab_b1.txt 2>&1 || { tail -5 $O/ab_b1.txt; exit 1; }
+cp gpurun_out/ab.log $O/ab_b1.log
+cat $O/ab_b1.log
+
 cat $O/ab_b32.log
