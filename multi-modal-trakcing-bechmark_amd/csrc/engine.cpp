@@ -130,7 +130,7 @@ struct mmt_engine {
   // next layer re-forms the fovea output s8 from the half it did not write)
   float *tok_rgb = nullptr, *tok_aux = nullptr, *X = nullptr, *X2 = nullptr,
         *a8 = nullptr,
-        *c8 = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
+        *c8 = nullptr, *fstat = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
   int *gidx0 = nullptr, *gidx1 = nullptr, *slot2pos = nullptr, *gather = nullptr, *removed = nullptr;
   float* splitk_ws = nullptr;   // [kMaxParts launch parts][kSplitKWsElems] fp32 split-K partials (few-tile GEMMs)
@@ -557,7 +557,7 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->A_rgb, (size_t)B * L * C * 2},      {(void**)&e->A_aux, (size_t)B * L * C * 2},
       {(void**)&e->tok_rgb, (size_t)B * L * C * 4},    {(void**)&e->tok_aux, (size_t)B * L * C * 4},
       {(void**)&e->X, (size_t)B * L * C * 4},          {(void**)&e->X2, (size_t)B * L * C * 4},
-      {(void**)&e->a8, (size_t)2 * B * L * 8 * 4},
+      {(void**)&e->a8, (size_t)2 * B * L * 8 * 4},     {(void**)&e->fstat, (size_t)B * 32 * 4},
       {(void**)&e->c8, (size_t)2 * B * L * 8 * 4},         {(void**)&e->Hn, (size_t)B * L * C * 2},
       {(void**)&e->QKV, (size_t)B * L * 3 * C * 2},    {(void**)&e->O, (size_t)B * L * C * 2},
       {(void**)&e->Hm, (size_t)B * L * MLPD * 2},      {(void**)&e->feat, (size_t)B * Lx * C * 2},
@@ -828,6 +828,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
     pa.a8p = i ? q_a8(i - 1) : nullptr;
     pa.c8p = i ? q_c8(i - 1) : nullptr;
     pa.smooth_p = i ? e->pw[i - 1].smooth : 0.f;
+    pa.fstat_p = i ? e->fstat + (size_t)r0 * 32 : nullptr;   // written by layer i-1's LN1 (prompt_expand_ln)
     pa.lnA_w = e->pw[lnA].nw;
     pa.lnA_b = e->pw[lnA].nb;
     pa.lnB_w = e->pw[i].nw;
@@ -882,6 +883,7 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
       la.a8 = q_a8(i);
       la.c8 = q_c8(i);
       la.smooth = e->pw[i].smooth;
+      la.fstat = deep ? e->fstat + (size_t)r0 * 32 : nullptr;
       la.w1 = e->pw[i].w1;   // conv1x1 of the prompt block that ran for this layer
       la.b1 = e->pw[i].b1;
       la.tok_rgb = q_tok_rgb;

@@ -1914,7 +1914,9 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // few 64 x 64 tiles and a long K (small batches): split K over workgroups (fp32 partials in the
     // workspace, fixed-order reduction with the epilogue), at least 4 K-tiles per split
     const int tiles = t64 * (a.N / 64) * a.groups, nk = a.K / 64;
-    static const int sk_tiles = getenv("MMT_SPLITK_TILES") ? atoi(getenv("MMT_SPLITK_TILES")) : 128;
+    // (100, not 128: qkv of the 129..192-row CE layers at one sequence -- 108 tiles -- runs unsplit without its
+    // reduce launch, 1092 -> 1100 frames/s, profiles/r05_ab_splitk_tiles_b1.txt)
+    static const int sk_tiles = getenv("MMT_SPLITK_TILES") ? atoi(getenv("MMT_SPLITK_TILES")) : 100;
     static const int sk_target = getenv("MMT_SPLITK_TARGET") ? atoi(getenv("MMT_SPLITK_TARGET")) : 256;
     static const int sk_minkt = getenv("MMT_SPLITK_MINKT") ? atoi(getenv("MMT_SPLITK_MINKT")) : 4;
     static const int sk_max = getenv("MMT_SPLITK_MAX") ? atoi(getenv("MMT_SPLITK_MAX")) : 8;

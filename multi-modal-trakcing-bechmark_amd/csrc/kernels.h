@@ -118,6 +118,9 @@ struct PromptArgs {
   // per-(sequence, part) softmax statistics computed in this block (fovea_stats) -- s8 is never stored
   const float* a8p; const float* c8p;
   float smooth_p;
+  // deep layers: those statistics as the previous layer's LN1 formed them ([B][32], LnPromptArgs::fstat): the
+  // same bits, loaded instead of re-reduced; null: computed here (fovea_stats)
+  const float* fstat_p;
   RowReduce rr;              // deep layers: the previous block's fc2 split-K update of X, applied here
 };
 // PromptFold (float[160]) for deep layer i, from prompt_norms[i] (g, b), conv0_1 of block i (W, w0)
@@ -135,6 +138,7 @@ struct LnPromptArgs {
   float* X;
   const float* a8; const float* c8;   // [B][Lz+Lx][8] this prompt block's branches; s8 = fovea(a8) + c8
   float smooth;
+  float* fstat;              // non-null: the sequence's fovea statistics written here ([B][32], block x = 0)
   const float* w1; const float* b1;         // conv1x1 channel-major [8][768] -> the prompt P = w1^T s8 + b1
   const float* tok_rgb;      // mode 1
   const float* pos;          // mode 1: [Lz+Lx][768]

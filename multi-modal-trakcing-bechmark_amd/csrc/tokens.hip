@@ -320,7 +320,11 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
   extern __shared__ __attribute__((aligned(16))) float va[];   // [L][8] (dynamic: sized by the launch)
   __shared__ float red[64], st[32];
   const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, b = blockIdx.y;
-  const FoveaStage fsg = fovea_stage(a.a8p + (int64_t)b * L * 8, L);
+  // the previous a8's fovea statistics: as the previous LN1 wrote them (32 floats), else reduced here
+  const bool pre = a.fstat_p != nullptr;
+  FoveaStage fsg;
+  if (!pre) fsg = fovea_stage(a.a8p + (int64_t)b * L * 8, L);
+  const float stv = pre && threadIdx.x < 32 ? a.fstat_p[b * 32 + threadIdx.x] : 0.f;
   int sv[R], posv[R];
   int64_t xrowv[R];
   Row12 xv[R];
@@ -346,7 +350,12 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
 #pragma unroll
   for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[threadIdx.x + TOK_THREADS * k] = wst[k];
   if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
-  fovea_stats(fsg, a.Lz, a.Lx, a.smooth_p, va, red, st);   // ends with a barrier
+  if (pre) {
+    if (threadIdx.x < 32) st[threadIdx.x] = stv;
+    __syncthreads();
+  } else {
+    fovea_stats(fsg, a.Lz, a.Lx, a.smooth_p, va, red, st);   // ends with a barrier
+  }
 #pragma unroll
   for (int rr = 0; rr < R; ++rr) {
   const int s = sv[rr], pos = posv[rr];
@@ -415,7 +424,7 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
     // of two, so the 640 blocks of a 16-sequence half run in one round
     const int R = a.rr.ws ? 1 : tok_rows_per_wave(a.B);   // the slab-holding variant keeps one slot per wave
     const dim3 grid((L + TOK_ROWS * R - 1) / (TOK_ROWS * R), a.B);
-    const size_t va_bytes = (size_t)L * 8 * sizeof(float);
+    const size_t va_bytes = a.fstat_p ? 0 : (size_t)L * 8 * sizeof(float);
     if (a.rr.ws)
       hipLaunchKernelGGL((prompt_reduce_deep_kernel<true, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
     else if (R == 4)
@@ -491,6 +500,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
     if (e < 3 * C768) cst[e] = cs[k];
   }
   fovea_stats(fsg, a.Lz, a.Lx, a.smooth, va, red, st);   // ends with a barrier
+  if (a.fstat && blockIdx.x == 0 && threadIdx.x < 32) a.fstat[b * 32 + threadIdx.x] = st[threadIdx.x];
 #pragma unroll
   for (int rr = 0; rr < R; ++rr) {
   if (tv[rr] >= a.rows_per_seq) break;   // wave-uniform; later rows of the wave lie further out

@@ -54,6 +54,8 @@ def run_stages(precision, n_frames=6):
 
     def optimize(w, feat, bb, num_iter=None, **k):
         its = [w.detach().cpu()]
+        cap["opt_in"] = (feat.detach().cpu(), torch.as_tensor(bb).detach().cpu(),
+                         {kk: (v.detach().cpu() if torch.is_tensor(v) else v) for kk, v in k.items()})
         cur = w
         for _ in range(num_iter):
             cur = opt(cur, feat, bb, num_iter=1, **k)

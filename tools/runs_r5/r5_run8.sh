@@ -11,3 +11,6 @@ head -45 $O/b1_steady.txt
 rm -rf $O/prof1
 ROUNDS=3 STEPS=300 ARGS="--batch 1" timeout -k 10 400 bash tools/ab_envs.sh "" "MMT_SPLITK_TILES=100" > $O/ab_splitk_tiles_b1.txt 2>&1 || { tail -5 $O/ab_splitk_tiles_b1.txt; exit 1; }
 cat $O/ab_splitk_tiles_b1.txt
+# gemm256s with the next half-tile's DMA issued inside the MFMA cluster (GEMM256S_DMA_IN_MFMA=1) vs default, B=32
+ROUNDS=3 LIBDIR=abx4 timeout -k 10 500 bash tools/ab_bench.sh > $O/ab_dmamfma_b32.txt 2>&1 || { tail -5 $O/ab_dmamfma_b32.txt; exit 1; }
+cat $O/ab_dmamfma_b32.txt
