@@ -238,6 +238,22 @@ size_t mmt_conv2d_f16x3_ws_bytes(int N, int H, int W, int Cin, int Cout, int kh,
 int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int n_groups, int N, int H, int W, int Cin, int Kp,
                             int Cout, int kh, int kw, int stride, int pad, void* ws, size_t ws_bytes,
                             void* hip_stream);
+/* ResNet's Bottleneck tail with a downsample (resnet.py:76-95: relu(bn3(conv3(b)) + bn_d(conv_d(x)))) as ONE
+ * GEMM over concatenated K: conv3 (1 x 1 over b [N][H][W][Cin]) and the downsample (1 x 1 / stride2 over the block
+ * input x2 [N][H2][W2][Cin2], (H2 - 1) / stride2 + 1 == H) accumulate into the same fp32 registers, so the
+ * downsample's output is never written nor read back (replaces a mmt_conv2d_f16x3_groups launch of the downsample
+ * plus the conv3 launch that read it as resid).  groups[i].w_hi / w_lo: [Cout][Kp] with Kp = Cin + Cin2 -- conv3's
+ * K then the downsample's, both split at the common w_scale --, bias = b3 + b_d, resid NULL; ds[i] the second
+ * source (x2_max: its sharded max words, or x2_scale); the two sources are split at the smaller of their scales.
+ * Cin % 32 == Cin2 % 32 == 0; workspace sized by mmt_conv2d_f16x3_ws_bytes(N, H, W, Kp, Cout, 1, 1, 1, 0, G). */
+typedef struct mmt_conv_ds {
+  const float* x2;
+  const float* x2_max;
+  float x2_scale;
+} mmt_conv_ds;
+int mmt_conv2d_f16x3_ds_groups(const mmt_conv_group* groups, const mmt_conv_ds* ds, int n_groups, int N, int H, int W,
+                               int Cin, int H2, int W2, int Cin2, int stride2, int Kp, int Cout, void* ws,
+                               size_t ws_bytes, void* hip_stream);
 /* nn.MaxPool2d(k, stride, pad) over NHWC                                                           */
 int mmt_maxpool2d_f32(const float* x, int N, int H, int W, int C, int k, int stride, int pad, float* y,
                       void* hip_stream);
@@ -350,6 +366,13 @@ typedef struct mmt_dimp_result {  /* per sequence, per frame                    
 size_t mmt_dimp_state_bytes(void);
 int mmt_dimp_track_sample(mmt_dimp_state* states, const mmt_dimp_frame* frames, int n, const mmt_dimp_track_params* p,
                           int out_h, int out_w, float* patches, void* hip_stream);
+/* the same patches written as the f16x3 backbones read them: each 6-channel pixel's two halves normalised
+ * (((v / 255) - mean) / std, net_wrappers.py:62-72, the arithmetic of mmt_image_normalize4) into out_a / out_b
+ * [n][out_h][out_w][4] (zero fourth channel) -- one launch and one patch round trip fewer than
+ * mmt_dimp_track_sample + mmt_image_normalize4, the same bits.  Frames must have C == 6.               */
+int mmt_dimp_track_sample_norm4(mmt_dimp_state* states, const mmt_dimp_frame* frames, int n,
+                                const mmt_dimp_track_params* p, int out_h, int out_w, const float mean[3],
+                                const float std_[3], float* out_a, float* out_b, void* hip_stream);
 int mmt_dimp_track_update(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
                           const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
                           mmt_dimp_result* results, void* hip_stream);

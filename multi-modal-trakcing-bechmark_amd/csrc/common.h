@@ -163,6 +163,40 @@ __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
   return f32x2{x.x >= 0.f ? x.x - xh.x : xh.x, x.y >= 0.f ? x.y - xh.y : xh.y};
 }
 
+// gelu_erf2 on two pairs.  GELU_INTERLEAVE (tuning build): the two Horner chains interleaved statement by statement
+// and fenced in lockstep -- the fc1 epilogue's 256 x 256 tile drops 32.8k -> 30.0k cycles, but the 32-sequence line
+// measured 6 327 -> 6 307 frames/s (three alternating rounds, profiles/r05_ab_gelu_interleave_b32_rejected.txt), so the
+// default runs the pairs one after the other; same operations per element, same bits either way
+__device__ __forceinline__ void gelu_erf4(f32x2& x0, f32x2& x1) {
+#ifndef GELU_INTERLEAVE
+  x0 = gelu_erf2(x0);
+  x1 = gelu_erf2(x1);
+  return;
+#endif
+  const f32x2 u0 = __builtin_elementwise_abs(x0) * (f32x2)0.70710678118654752440f;
+  const f32x2 u1 = __builtin_elementwise_abs(x1) * (f32x2)0.70710678118654752440f;
+  const f32x2 d0 = __builtin_elementwise_fma((f32x2)0.5f, u0, (f32x2)1.0f);
+  const f32x2 d1 = __builtin_elementwise_fma((f32x2)0.5f, u1, (f32x2)1.0f);
+  const f32x2 t0 = {__builtin_amdgcn_rcpf(d0.x), __builtin_amdgcn_rcpf(d0.y)};
+  const f32x2 t1 = {__builtin_amdgcn_rcpf(d1.x), __builtin_amdgcn_rcpf(d1.y)};
+  f32x2 q0 = (f32x2)0.246517298f, q1 = (f32x2)0.246517298f;
+  constexpr float C[9] = {-1.18611495f, 2.14747446f, -1.63775315f, 0.402321582f, -0.26875686f,
+                          0.139630057f, 0.539700616f, 1.4427292f, -2.82574822f};
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    q0 = __builtin_elementwise_fma(q0, t0, (f32x2)C[k]);
+    q1 = __builtin_elementwise_fma(q1, t1, (f32x2)C[k]);
+    asm volatile("" : "+v"(q0), "+v"(q1));   // lockstep: the scheduler otherwise serialises the two chains again
+  }
+  const f32x2 a0 = __builtin_elementwise_fma((f32x2)-1.44269504f * u0, u0, q0);
+  const f32x2 a1 = __builtin_elementwise_fma((f32x2)-1.44269504f * u1, u1, q1);
+  const f32x2 h0 = t0 * f32x2{__builtin_amdgcn_exp2f(a0.x), __builtin_amdgcn_exp2f(a0.y)};
+  const f32x2 h1 = t1 * f32x2{__builtin_amdgcn_exp2f(a1.x), __builtin_amdgcn_exp2f(a1.y)};
+  const f32x2 xh0 = x0 * h0, xh1 = x1 * h1;
+  x0 = f32x2{x0.x >= 0.f ? x0.x - xh0.x : xh0.x, x0.y >= 0.f ? x0.y - xh0.y : xh0.y};
+  x1 = f32x2{x1.x >= 0.f ? x1.x - xh1.x : xh1.x, x1.y >= 0.f ? x1.y - xh1.y : xh1.y};
+}
+
 // bf16-output GELU: the same erf GELU with erfc from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 on
 // erf, five coefficients; 1/2 and log2(e) folded as above), written as
 //   GELU(x) = relu(x) - |x| * h(|x|),   h(a) = t p(t) 2^(-x^2 log2(e) / 2),  t = 1 / (1 + 0.3275911 a / sqrt2)

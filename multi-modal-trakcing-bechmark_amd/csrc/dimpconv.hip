@@ -56,6 +56,9 @@ struct ConvGroupArgs {            // one convolution of a grouped launch (the RG
   float xscale;                   // static input scale (power of two) when xmax is null
   float inv_w;                    // 1 / s_w
   int flags;
+  const float* x2;                // Cin2 > 0: the block input the fused downsample reads ([N][H2][W2][Cin2])
+  const float* x2max;             // its sharded max words, or null: x2scale
+  float x2scale;
 };
 
 struct ConvF16Args {
@@ -63,6 +66,9 @@ struct ConvF16Args {
   float* part;                    // split-K partials [ks][G][M][Cout] (ks > 1)
   int N, H, W, Cin, Cout, kh, kw, stride, pad, Ho, Wo, Kp, ks;
   int xcd_order;                  // conv_f16x3_deep_kernel: XCD-aware tile order (else M tiles fastest)
+  // a downsample fused into a 1 x 1 conv3 (conv_f16x3_deep_kernel only): K-tiles from Cin / 32 on read x2 at
+  // output pixel (oy, ox) * stride2; 0: none
+  int Cin2, H2, W2, stride2;
 };
 
 __device__ __forceinline__ int cswz(int r, int c) { return r * 32 + ((c ^ ((r >> 2) & 2)) << 3); }   // gemm.hip swzk<32>
@@ -827,18 +833,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
     const float mx = wave_max(g.xmax[lane * kShardStride]);
     sa = mx > 0.f ? pow2_scale(mx) : 1.0f;
   }
+  // fused downsample: both sources split at the smaller scale, so one accumulator holds both sums
+  const bool ds = a.Cin2 > 0;
+  if (ds) {
+    float sb = g.x2scale;
+    if (g.x2max) {
+      const float mx = wave_max(g.x2max[lane * kShardStride]);
+      sb = mx > 0.f ? pow2_scale(mx) : 1.0f;
+    }
+    sa = fminf(sa, sb);
+  }
   const float inv = g.inv_w / sa;
 
   const int ac = t & 3;   // slot s: row (t >> 2) + 128 s, K chunk ac (8 values)
   bool mval[SL];
   int iy0[SL], ix0[SL];
-  uint32_t xrow[SL];
+  uint32_t xrow[SL], xrow2[SL];
 #pragma unroll
   for (int sl = 0; sl < SL; ++sl) {
     const int m = m0 + (t >> 2) + 128 * sl;
     mval[sl] = m < M;
     iy0[sl] = ix0[sl] = 0;
-    xrow[sl] = 0;
+    xrow[sl] = xrow2[sl] = 0;
     if (mval[sl]) {
       const int nimg = m / (a.Ho * a.Wo);
       const int r = m - nimg * a.Ho * a.Wo;
@@ -846,9 +862,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
       iy0[sl] = oy * a.stride - a.pad;
       ix0[sl] = ox * a.stride - a.pad;
       xrow[sl] = (uint32_t)(nimg * a.H * a.W * a.Cin);
+      // the downsample's input pixel (1 x 1, no padding): its float offset, channel 0
+      if (ds) xrow2[sl] = (uint32_t)(((nimg * a.H2 + oy * a.stride2) * a.W2 + ox * a.stride2) * a.Cin2);
     }
   }
   const u32x4 qX = make_rsrc_words(g.x, (int64_t)a.N * a.H * a.W * a.Cin * 4);
+  const u32x4 qX2 = make_rsrc_words(ds ? g.x2 : g.x, ds ? (int64_t)a.N * a.H2 * a.W2 * a.Cin2 * 4 : 0);
+  const int nk1 = ds ? a.Cin / BK : 1 << 30;   // K-tiles of the first source (1 x 1 conv3: its Cin)
   const int nk = a.Kp / BK;
   const int kt0 = (int)((int64_t)slice * nk / a.ks), nt = (int)((int64_t)(slice + 1) * nk / a.ks) - kt0;
   const int cpt = a.Cin / BK;
@@ -876,13 +896,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
         ++a_ky;
       }
     }
+    // the fused downsample's K-tiles (wave-uniform; selects, not a branch, so the loads stay straight-line code for
+    // tools/isa_audit.py): x2 at the output pixel's stride2 position
+    const bool second = kt0 + i >= nk1;
+    const int c2 = (kt0 + i - nk1) * BK + ac * 8;
+    const u32x4 qA = second ? qX2 : qX;
 #pragma unroll
     for (int sl = 0; sl < SL; ++sl) {
       const int iy = iy0[sl] + ky, ix = ix0[sl] + kx;
-      const bool ok = i < nt && mval[sl] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      const uint32_t vo = ok ? (xrow[sl] + (uint32_t)((iy * a.W + ix) * a.Cin + c0)) * 4 : kBufOob;
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(set.a[2 * sl]) : "v"(vo), "s"(qX) : "memory");
-      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:16" : "=v"(set.a[2 * sl + 1]) : "v"(vo), "s"(qX)
+      // (bitwise, not short-circuit: no control flow around the loads)
+      const bool inb = (iy >= 0) & (iy < a.H) & (ix >= 0) & (ix < a.W);
+      const bool ok = (i < nt) & mval[sl] & (second | inb);
+      const uint32_t off1 = xrow[sl] + (uint32_t)((iy * a.W + ix) * a.Cin + c0), off2 = xrow2[sl] + (uint32_t)c2;
+      const uint32_t vo = ok ? (second ? off2 : off1) * 4 : kBufOob;
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(set.a[2 * sl]) : "v"(vo), "s"(qA) : "memory");
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:16" : "=v"(set.a[2 * sl + 1]) : "v"(vo), "s"(qA)
                    : "memory");
     }
   };
@@ -1527,7 +1555,7 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
         ((c.flags & MMT_CONV_POOL) && ((c.flags & MMT_CONV_MAX) || c.resid)))
       return MMT_E_ARG;
     a.g[i] = ConvGroupArgs{c.x, c.w_hi, c.w_lo, c.bias, c.resid, c.y, c.x_max, c.y_max, c.x_scale, 1.0f / c.w_scale,
-                           c.flags};
+                           c.flags, nullptr, nullptr, 0.f};
   }
   // the twin layers of a grouped launch write disjoint outputs unless they merge (a MAX layer reads y)
   if (G == 2 && (a.g[0].y == a.g[1].y || (a.g[0].flags | a.g[1].flags) & MMT_CONV_MAX)) return MMT_E_ARG;
@@ -1632,6 +1660,52 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
     }
   }
 #endif
+  if (ks > 1) {
+    const int64_t q = M * Cout / 4;
+    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((q + 255) / 256), G), dim3(256), 0, s, a);
+  }
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_conv2d_f16x3_ds_groups(const mmt_conv_group* groups, const mmt_conv_ds* ds, int G, int N, int H, int W,
+                               int Cin, int H2, int W2, int Cin2, int stride2, int Kp, int Cout, void* ws,
+                               size_t ws_bytes, void* stream) {
+  int Ho, Wo, K;
+  // conv3 is 1 x 1 / stride 1 over [N][H][W][Cin]; the downsample 1 x 1 / stride2 over [N][H2][W2][Cin2] lands on
+  // the same H x W grid; the weights hold both K ranges
+  if (!groups || !ds || G < 1 || G > kMaxGroups || Cin < 32 || Cin % 32 || Cin2 < 32 || Cin2 % 32 || stride2 < 1 ||
+      H2 <= 0 || W2 <= 0 || (H2 - 1) / stride2 + 1 != H || (W2 - 1) / stride2 + 1 != W || Kp != Cin + Cin2 ||
+      conv_shape(N, H, W, Kp, Cout, 1, 1, 1, 0, Ho, Wo, K) != MMT_OK ||
+      (int64_t)N * H2 * W2 * Cin2 > ((int64_t)1 << 29))   // 32-bit buffer offsets into x2
+    return MMT_E_ARG;
+  ConvF16Args a{};
+  for (int i = 0; i < G; ++i) {
+    const mmt_conv_group& c = groups[i];
+    if (!c.x || !c.w_hi || !c.w_lo || !c.y || !(c.w_scale > 0) || c.resid ||
+        (c.flags & ~(MMT_CONV_RELU | MMT_CONV_MAX)) || (!c.x_max && !(c.x_scale > 0)) || !ds[i].x2 ||
+        (!ds[i].x2_max && !(ds[i].x2_scale > 0)))
+      return MMT_E_ARG;
+    a.g[i] = ConvGroupArgs{c.x, c.w_hi, c.w_lo, c.bias, nullptr, c.y, c.x_max, c.y_max, c.x_scale, 1.0f / c.w_scale,
+                           c.flags, ds[i].x2, ds[i].x2_max, ds[i].x2_scale};
+  }
+  if (G == 2 && (a.g[0].y == a.g[1].y || (a.g[0].flags | a.g[1].flags) & MMT_CONV_MAX)) return MMT_E_ARG;
+  a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.kh = 1; a.kw = 1; a.stride = 1; a.pad = 0;
+  a.Ho = H; a.Wo = W; a.Kp = Kp;
+  a.Cin2 = Cin2; a.H2 = H2; a.W2 = W2; a.stride2 = stride2;
+  const int64_t M = (int64_t)N * H * W;
+  int ks = (int)conv_ks_for(N, H, W, H, W, Kp, Cout, 1, 1, 1, 0, Kp, G);
+  if (ks > 1 && (!ws || ws_bytes < (size_t)(ks * G * M * (int64_t)Cout * 4))) ks = 1;
+  a.ks = ks;
+  a.part = static_cast<float*>(ws);
+  static const int xcd_env = getenv("MMT_CONV_XCD") ? atoi(getenv("MMT_CONV_XCD")) : -1;
+  a.xcd_order = xcd_env != 0;
+  const int bn = conv_bn((M + 127) / 128, Kp, Cout, G);
+  const dim3 dgrid((unsigned)((M + 127) / 128 * (Cout / bn)), 1, G * ks);
+  const hipStream_t s = (hipStream_t)stream;
+  if (bn == 128)
+    hipLaunchKernelGGL((conv_f16x3_deep_kernel<128, 3, 128, true>), dgrid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_f16x3_deep_kernel<64, 3, 128, true>), dgrid, dim3(512), 0, s, a);
   if (ks > 1) {
     const int64_t q = M * Cout / 4;
     hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3((unsigned)((q + 255) / 256), G), dim3(256), 0, s, a);

@@ -97,19 +97,49 @@ __device__ __forceinline__ float frame_at(const uint8_t* f, int64_t rs, int C, c
 // grid (pixel blocks, sequences): patch [n][C][oh][ow] from the sequence's frame; block 0 stores the sample
 // coordinates.  Pixels as sample_patch_kernel (dimpnet.hip): replicate padding, ATen's CPU bilinear with its
 // fma contraction.
+// NORM4 (6-channel frames): instead of the NCHW patch, each pixel's two 3-channel halves normalised as
+// normalize_kernel does (dimpnet.hip, oc = 4: v / 255, - mean, / std, zero fourth channel) into outa / outb
+// [n][oh][ow][4] -- the same values, so the same bits as the two launches
+struct NormArgs {
+  float mean[3], sd[3];
+  float* outa;
+  float* outb;
+};
+template <bool NORM4>
 __global__ __launch_bounds__(256) void dimp_sample_kernel(mmt_dimp_state* states, const mmt_dimp_frame* frames,
-                                                          mmt_dimp_track_params p, int oh, int ow, float* out) {
+                                                          mmt_dimp_track_params p, int oh, int ow, float* out,
+                                                          NormArgs na) {
   const int s = blockIdx.y;
   const mmt_dimp_frame fr = frames[s];
   const Geom g = dimp_geometry(states[s], p, fr.H, fr.W);
   if (blockIdx.x == 0 && threadIdx.x < 4) states[s].coords[threadIdx.x] = g.coords[threadIdx.x];
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)oh * ow) return;
-  const int C = fr.C;
+  const int C = NORM4 ? 6 : fr.C;
   float* o = out + (int64_t)s * C * oh * ow;
+  float v6[6];
+  auto put = [&](int c, float v) {
+    if constexpr (NORM4) v6[c] = v;
+    else o[(int64_t)c * oh * ow + i] = v;
+  };
+  auto flush = [&]() {
+    if constexpr (NORM4) {
+      float n[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        float v = v6[c] / 255.f;
+        v = v - na.mean[c % 3];
+        n[c] = v / na.sd[c % 3];
+      }
+      const int64_t q = (int64_t)s * oh * ow + i;
+      reinterpret_cast<float4*>(na.outa)[q] = make_float4(n[0], n[1], n[2], 0.f);
+      reinterpret_cast<float4*>(na.outb)[q] = make_float4(n[3], n[4], n[5], 0.f);
+    }
+  };
   const int oy = (int)(i / ow), ox = (int)(i - (int64_t)oy * ow);
   if (g.sz_h == oh && g.sz_w == ow) {
-    for (int c = 0; c < C; ++c) o[(int64_t)c * oh * ow + i] = frame_at(fr.data, fr.stride, C, g, oy, ox, c);
+    for (int c = 0; c < C; ++c) put(c, frame_at(fr.data, fr.stride, C, g, oy, ox, c));
+    flush();
     return;
   }
   const float sy = (float)g.sz_h / (float)oh, sx = (float)g.sz_w / (float)ow;
@@ -124,8 +154,9 @@ __global__ __launch_bounds__(256) void dimp_sample_kernel(mmt_dimp_state* states
                                     frame_at(fr.data, fr.stride, C, g, y0, x0, c) * lx0);
     const float t1 = __builtin_fmaf(frame_at(fr.data, fr.stride, C, g, y1, x1, c), lx1,
                                     frame_at(fr.data, fr.stride, C, g, y1, x0, c) * lx0);
-    o[(int64_t)c * oh * ow + i] = __builtin_fmaf(t1, ly1, t0 * ly0);
+    put(c, __builtin_fmaf(t1, ly1, t0 * ly0));
   }
+  flush();
 }
 
 // pytracking dcf.max2d over an h x w map in LDS: the maximum and its (row, col) as torch.max(dim=-2) then
@@ -400,8 +431,20 @@ int mmt_dimp_track_sample(mmt_dimp_state* states, const mmt_dimp_frame* frames, 
                           const mmt_dimp_track_params* p, int out_h, int out_w, float* patches, void* stream) {
   if (!states || !frames || !p || !patches || n <= 0 || out_h <= 0 || out_w <= 0) return MMT_E_ARG;
   const dim3 grid((unsigned)(((int64_t)out_h * out_w + 255) / 256), n);
-  hipLaunchKernelGGL(dimp_sample_kernel, grid, dim3(256), 0, (hipStream_t)stream, states, frames, *p, out_h, out_w,
-                     patches);
+  hipLaunchKernelGGL(dimp_sample_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, states, frames, *p, out_h,
+                     out_w, patches, NormArgs{});
+  return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_dimp_track_sample_norm4(mmt_dimp_state* states, const mmt_dimp_frame* frames, int n,
+                                const mmt_dimp_track_params* p, int out_h, int out_w, const float mean[3],
+                                const float std_[3], float* out_a, float* out_b, void* stream) {
+  if (!states || !frames || !p || !mean || !std_ || !out_a || !out_b || n <= 0 || out_h <= 0 || out_w <= 0)
+    return MMT_E_ARG;
+  NormArgs na{{mean[0], mean[1], mean[2]}, {std_[0], std_[1], std_[2]}, out_a, out_b};
+  const dim3 grid((unsigned)(((int64_t)out_h * out_w + 255) / 256), n);
+  hipLaunchKernelGGL(dimp_sample_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, states, frames, *p, out_h,
+                     out_w, nullptr, na);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 

@@ -678,7 +678,8 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
         const float4 bv = bq[jj];
         float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
         if (EPI == EPI_GELU_BF16) {
-          const f32x2 g0 = gelu_erf2(f32x2{v[0], v[1]}), g1 = gelu_erf2(f32x2{v[2], v[3]});
+          f32x2 g0 = {v[0], v[1]}, g1 = {v[2], v[3]};
+          gelu_erf4(g0, g1);
           v[0] = g0.x;
           v[1] = g0.y;
           v[2] = g1.x;
@@ -1555,7 +1556,8 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
             const float4 bv = bq[QB[qd]][jj];
             float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
             if (EPI == EPI_GELU_BF16) {
-              const f32x2 g0 = gelu_erf2(f32x2{v[0], v[1]}), g1 = gelu_erf2(f32x2{v[2], v[3]});
+              f32x2 g0 = {v[0], v[1]}, g1 = {v[2], v[3]};
+              gelu_erf4(g0, g1);
               v[0] = g0.x;
               v[1] = g0.y;
               v[2] = g1.x;

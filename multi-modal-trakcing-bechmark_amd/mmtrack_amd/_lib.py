@@ -104,6 +104,10 @@ class MmtConvGroup(ctypes.Structure):
                 ("x_scale", ctypes.c_float), ("y_max", ctypes.c_void_p), ("flags", ctypes.c_int)]
 
 
+class MmtConvDs(ctypes.Structure):
+    _fields_ = [("x2", ctypes.c_void_p), ("x2_max", ctypes.c_void_p), ("x2_scale", ctypes.c_float)]
+
+
 class MmtDimpResult(ctypes.Structure):
     _fields_ = [("box", ctypes.c_float * 4), ("max_score", ctypes.c_float), ("flag", ctypes.c_int),
                 ("num_iter", ctypes.c_int), ("n_samples", ctypes.c_int), ("replace_ind", ctypes.c_int),
@@ -157,6 +161,7 @@ SIGNATURES = {
     "mmt_conv2d_f16x3": (_I, [_P, _I, _I, _I, _I, _P, _P, _F, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _I, _P]),
     "mmt_conv2d_f16x3_ws_bytes": (ctypes.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "mmt_conv2d_f16x3_groups": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, ctypes.c_size_t, _P]),
+    "mmt_conv2d_f16x3_ds_groups": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, ctypes.c_size_t, _P]),
     "mmt_maxpool2d_f32": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "mmt_image_normalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "mmt_image_normalize4": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
@@ -178,6 +183,7 @@ SIGNATURES = {
     "mmt_dimp_track_optimize": (_I, [_P, _I, _P, _P, _I, _I, _I, _P, _I, _I, ctypes.POINTER(MmtDimpParams), _I, _P,
                                      ctypes.c_size_t, _P]),
     "mmt_dimp_track_sample": (_I, [_P, _P, _I, ctypes.POINTER(MmtDimpTrackParams), _I, _I, _P, _P]),
+    "mmt_dimp_track_sample_norm4": (_I, [_P, _P, _I, ctypes.POINTER(MmtDimpTrackParams), _I, _I, _P, _P, _P, _P, _P]),
     "mmt_dimp_track_update": (_I, [_P, _I, _P, _I, _I, ctypes.POINTER(MmtDimpTrackParams), _P, _I64, _P, _P, _P]),
     "mmt_gemm_stamps": (_I, [_P]),
     "mmt_op_gemm": (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _I, _I, _P]),

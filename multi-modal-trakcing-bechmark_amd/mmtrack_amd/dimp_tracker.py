@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -311,6 +312,9 @@ class DiMP:
         return {'target_bbox': [float(v) for v in res.box], 'confidence': float(res.max_score)}
 
 FLAGS = ('normal', 'not_found', 'uncertain', 'hard_negative')
+# f16x3 pools sample 6-channel frames straight into the backbones' normalised 4-channel inputs
+# (mmt_dimp_track_sample_norm4); MMT_DIMP_FUSED_SAMPLE=0 (tuning A/B, stage tests): the NCHW patch + normalise
+FUSED_SAMPLE = os.environ.get("MMT_DIMP_FUSED_SAMPLE", "1") != "0"
 
 
 class DimpPool:
@@ -433,15 +437,28 @@ class DimpPool:
         self._copy_ev[(first, buf)] = cev
         sz = [int(v) for v in self.tparams.img_sample_sz]
         C = fr[0].shape[2]
-        patches = torch.empty(n, C, sz[0], sz[1], dtype=torch.float32, device=self.dev)
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
-        rc = lib.mmt_dimp_track_sample(ctypes.c_void_p(self.state_ptr(first)),
-                                       ctypes.c_void_p(self.frames.data_ptr() + first * fb), n,
-                                       ctypes.byref(self.tparams), sz[0], sz[1], ctypes.c_void_p(patches.data_ptr()),
-                                       stream)
-        if rc != 0:
-            raise RuntimeError(f"mmt_dimp_track_sample failed ({rc})")
-        test_x = net.extract_classification_feat(net.extract_backbone(patches))
+        if net.precision == "f16x3" and C == 6 and FUSED_SAMPLE:
+            # the sampler writes the backbones' normalised 4-channel halves itself (same bits as sample + normalise)
+            xa, xb = net.norm4_buffers(n, sz[0], sz[1])
+            rc = lib.mmt_dimp_track_sample_norm4(ctypes.c_void_p(self.state_ptr(first)),
+                                                 ctypes.c_void_p(self.frames.data_ptr() + first * fb), n,
+                                                 ctypes.byref(self.tparams), sz[0], sz[1], net._mean, net._std,
+                                                 ctypes.c_void_p(xa.data_ptr()), ctypes.c_void_p(xb.data_ptr()),
+                                                 stream)
+            if rc != 0:
+                raise RuntimeError(f"mmt_dimp_track_sample_norm4 failed ({rc})")
+            layer3 = net.extract_backbone_norm4(n, sz[0], sz[1])
+        else:
+            patches = torch.empty(n, C, sz[0], sz[1], dtype=torch.float32, device=self.dev)
+            rc = lib.mmt_dimp_track_sample(ctypes.c_void_p(self.state_ptr(first)),
+                                           ctypes.c_void_p(self.frames.data_ptr() + first * fb), n,
+                                           ctypes.byref(self.tparams), sz[0], sz[1],
+                                           ctypes.c_void_p(patches.data_ptr()), stream)
+            if rc != 0:
+                raise RuntimeError(f"mmt_dimp_track_sample failed ({rc})")
+            layer3 = net.extract_backbone(patches)
+        test_x = net.extract_classification_feat(layer3)
         from .dimp import apply_filter
         scores = apply_filter(test_x.unsqueeze(0), self.filters[first:first + n])[0].contiguous()
         F_ = test_x[0].numel()

@@ -120,6 +120,47 @@ class _Conv:
         return out
 
 
+class _ConvDs:
+    """A Bottleneck's conv3 (1 x 1) and its downsample (1 x 1 / stride) as one f16x3 GEMM over concatenated K
+    (mmt_conv2d_f16x3_ds_groups, resnet.py:76-95): weights [Cout][Cin3 + Cin_d] -- conv3's BN-folded K then the
+    downsample's -- split at one common scale, bias b3 + b_d; the downsample's output is never materialised."""
+
+    def __init__(self, c3, ds, dev):
+        w3 = c3.w.double().reshape(c3.cout, -1)     # [Cout][1][1][Cin] fp32 (BN folded) -> [Cout][Cin]
+        wd = ds.w.double().reshape(ds.cout, -1)
+        wq = torch.cat([w3, wd], dim=1).float()
+        self.cout, self.cin3, self.cin_d, self.stride = c3.cout, c3.cin, ds.cin, ds.stride
+        self.kp = wq.shape[1]
+        self.w_scale = range_scale(float(wq.abs().max()))
+        v = wq.to(dev) * self.w_scale
+        hi = v.half()
+        self.wh, self.wl = hi.contiguous(), (v - hi.float()).half().contiguous()
+        self.b = (c3.b.double() + ds.b.double()).float().to(dev)
+
+    def group(self, x, out, relu=True, x_max=None, y_max=None):
+        ptr = (lambda t: t.data_ptr() if t is not None else None)
+        return _lib.MmtConvGroup(x.data_ptr(), self.wh.data_ptr(), self.wl.data_ptr(), self.w_scale, ptr(self.b),
+                                 None, out.data_ptr(), ptr(x_max), 0.0, ptr(y_max), 1 if relu else 0)
+
+    def run(self, lib, groups, ds, N, H, W, H2, W2, ws, stream):
+        """groups: conv3's operands per backbone (x = conv2's output [N][H][W][Cin3]); ds: (x2 = the block input
+        [N][H2][W2][Cin_d], its max words) per backbone."""
+        G = len(groups)
+        need = lib.mmt_conv2d_f16x3_ws_bytes(N, H, W, self.kp, self.cout, 1, 1, 1, 0, G)
+        buf = ws(need) if (need and ws is not None) else None
+        arr = (_lib.MmtConvGroup * G)(*groups)
+        darr = (_lib.MmtConvDs * G)(*[_lib.MmtConvDs(x2.data_ptr(), x2m.data_ptr() if x2m is not None else None, 0.0)
+                                      for x2, x2m in ds])
+        _rc(lib.mmt_conv2d_f16x3_ds_groups(arr, darr, G, N, H, W, self.cin3, H2, W2, self.cin_d, self.stride, self.kp,
+                                           self.cout, _p(buf), need if buf is not None else 0, stream),
+            "mmt_conv2d_f16x3_ds_groups")
+
+
+# f16x3: each stage's first Bottleneck runs conv3 + downsample as one GEMM (_ConvDs); MMT_DIMP_DSFUSE=0 (tuning A/B):
+# the downsample conv writes its map and conv3 adds it as a residual
+DS_FUSE = os.environ.get("MMT_DIMP_DSFUSE", "1") != "0"
+
+
 def run_f16x3(lib, conv, groups, N, H, W, ws, stream, cin=None):
     """One mmt_conv2d_f16x3_groups launch of conv's shape over groups (the twin layers of the two backbones, or
     one); split-K partials in ws(nbytes) when the library asks for a split.  cin=4: the stem over an image
@@ -173,7 +214,7 @@ class DiMPNet:
                     c3 = _Conv(sd[pre + ".conv3.weight"], bn(pre + ".bn3"), dev=self.dev, f16x3=f16)
                     ds = _Conv(sd[pre + ".downsample.0.weight"], bn(pre + ".downsample.1"), stride=s, dev=self.dev,
                                f16x3=f16) if b == 0 else None
-                    blocks.append((c1, c2, c3, ds))
+                    blocks.append((c1, c2, c3, ds, _ConvDs(c3, ds, self.dev) if (f16 and ds is not None) else None))
             self.backbones.append((stem, blocks))
         self.clf = _Conv(sd["classifier.feature_extractor.0.weight"], pad=1, dev=self.dev, f16x3=f16)
         self.fconv = _Conv(sd["classifier.filter_initializer.filter_conv.weight"], pad=1,
@@ -248,7 +289,7 @@ class DiMPNet:
         nxt_name = "pong"
         nblocks = len(self.backbones[0][1])
         for i in range(nblocks):
-            c1s, c2s, c3s, dss = zip(*[bb[1][i] for bb in self.backbones])
+            c1s, c2s, c3s, dss, fus = zip(*[bb[1][i] for bb in self.backbones])
             Ho, Wo = c2s[0].out_hw(H, W)
             a = [self._buf(f"a{k}", N * H * W * c1s[0].cout) for k in K]
             a_max = [self._slot() for k in K]
@@ -258,13 +299,22 @@ class DiMPNet:
             b_max = [self._slot() for k in K]
             self._layer(c2s, [dict(x=a[k], out=b[k], relu=True, x_max=a_max[k], y_max=b_max[k]) for k in K],
                         N, H, W, s)
+            last = i == nblocks - 1
+            fused = fus[0] is not None and DS_FUSE and not last
+            if fused:   # conv3 + downsample in one GEMM: relu(conv3(b) + ds(cur) + b3 + b_d)
+                o = [self._buf(f"{nxt_name}{k}", N * Ho * Wo * c3s[0].cout) for k in K]
+                o_max = [self._slot() for k in K]
+                fus[0].run(lib, [fu.group(b[k], o[k], x_max=b_max[k], y_max=o_max[k]) for k, fu in zip(K, fus)],
+                           [(cur[k], cur_max[k]) for k in K], N, Ho, Wo, H, W, self._ws, s)
+                cur, cur_max, nxt_name = o, o_max, ("ping" if nxt_name == "pong" else "pong")
+                H, W = Ho, Wo
+                continue
             if dss[0] is not None:
                 res = [self._buf(f"res{k}", N * Ho * Wo * dss[0].cout) for k in K]
                 # only ever a residual operand: no max words
                 self._layer(dss, [dict(x=cur[k], out=res[k], x_max=cur_max[k]) for k in K], N, H, W, s)
             else:
                 res = cur
-            last = i == nblocks - 1
             if last:
                 o, o_max = [out] * len(K), [out_max] * len(K)
                 for k in K:   # the RGB map first, then the aux map merged into it
@@ -286,7 +336,7 @@ class DiMPNet:
             h, w = stem.out_hw(H, W)
             total += 2 * h * w * stem.cout * stem.kh * stem.kw * stem.cin
             h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
-            for c1, c2, c3, ds in blocks:
+            for c1, c2, c3, ds, _ in blocks:
                 ho, wo = c2.out_hw(h, w)
                 total += 2 * h * w * c1.cout * c1.cin
                 total += 2 * ho * wo * c2.cout * 9 * c2.cin
@@ -301,7 +351,8 @@ class DiMPNet:
         [6, H, W] image: each layer's input read once, its output written once (and read back by the MAX merge),
         the residual read, fp32 activations, f16x3 weights (hi + lo, read once per launch -- amortised over
         the batch, so not counted per image).  The per-layer roofline of a batch is the sum over layers of
-        max(FLOPs / matrix peak, bytes / HBM bandwidth)."""
+        max(FLOPs / matrix peak, bytes / HBM bandwidth).  (The reference's layers as the yardstick: the fused
+        conv3 + downsample of the f16x3 path moves fewer bytes than the two layers it replaces.)"""
         out = []
         for bi, (stem, blocks) in enumerate(self.backbones):
             h, w = stem.out_hw(H, W)
@@ -309,7 +360,7 @@ class DiMPNet:
             h2, w2 = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
             out.append((0, 4 * (h * w * 64 + h2 * w2 * 64)))   # max-pool
             h, w, cin = h2, w2, 64
-            for k, (c1, c2, c3, ds) in enumerate(blocks):
+            for k, (c1, c2, c3, ds, _) in enumerate(blocks):
                 ho, wo = c2.out_hw(h, w)
                 out.append((2 * h * w * c1.cout * c1.cin, 4 * (h * w * cin + h * w * c1.cout)))
                 out.append((2 * ho * wo * c2.cout * 9 * c2.cin, 4 * (h * w * c2.cin + ho * wo * c2.cout)))
@@ -341,6 +392,21 @@ class DiMPNet:
         xb = self._buf("xb", N * H * W * pc)
         norm = self.lib.mmt_image_normalize4 if f16 else self.lib.mmt_image_normalize
         _rc(norm(_p(im), N, 6, H, W, self._mean, self._std, _p(xa), _p(xb), s), "mmt_image_normalize")
+        return self._backbones(xa, xb, N, H, W, s)
+
+    def norm4_buffers(self, N, H, W):
+        """f16x3: the two normalised 4-channel NHWC halves [N*H*W*4] that extract_backbone_norm4 reads (a sampler
+        that normalises, mmt_dimp_track_sample_norm4, writes them directly)."""
+        if self.precision != "f16x3":
+            raise ValueError("norm4 buffers: f16x3 only")
+        return self._buf("xa", N * H * W * 4), self._buf("xb", N * H * W * 4)
+
+    def extract_backbone_norm4(self, N, H, W):
+        """extract_backbone on the patches already normalised into norm4_buffers(N, H, W)."""
+        xa, xb = self.norm4_buffers(N, H, W)
+        return self._backbones(xa, xb, N, H, W, self._stream())
+
+    def _backbones(self, xa, xb, N, H, W, s):
         Hf, Wf = (H + 15) // 16, (W + 15) // 16
         out = torch.empty(N, Hf, Wf, 1024, dtype=torch.float32, device=self.dev)
         if self._max_words is not None:

@@ -22,8 +22,12 @@ def run_stages(precision, n_frames=6):
     """The HIP tracker on the golden sequence with its stages captured (monkeypatched hooks, same call order)."""
     from mmtrack_amd import _lib
     from mmtrack_amd import dimp as mdimp
+    from mmtrack_amd import dimp_tracker as mdt
     from mmtrack_amd import synth
     from mmtrack_amd.dimp_tracker import DiMP, parameters
+    # frames through the NCHW patch + extract_backbone (the hooked entry point); the normalising sampler the pools
+    # use by default gives the same bits (test_gpu_dimpnet.py test_fused_sampler_bits)
+    mdt.FUSED_SAMPLE = False
     from mmtrack_amd.dimpnet import DiMPNet
     gd = np.load(os.path.join(GOLDEN, "tracker_dimp.npz"))
     seed, n, H, W, C, tseed = [int(v) for v in gd["meta"]]
@@ -86,6 +90,7 @@ def run_stages(precision, n_frames=6):
             cap.setdefault("sample", []).append([rr.sample_pos[0], rr.sample_pos[1], rr.sample_scale])
     finally:
         mdimp.apply_filter = af
+        mdt.FUSED_SAMPLE = True
     return cap, conf
 
 

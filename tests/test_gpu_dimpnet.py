@@ -158,6 +158,54 @@ def test_conv2d_f16x3_groups_and_splitk(N, C, H, W, Co, k, s, p):
     assert lib.mmt_conv2d_f16x3_groups(bad, 2, N, H, W, C, convs[0].kp, Co, k, k, s, p, None, 0, stream) == -1
 
 
+@pytest.mark.parametrize("N,Cin3,Cin2,H2,W2,Co,s2,G", [(3, 64, 64, 18, 18, 256, 1, 2), (2, 128, 256, 36, 36, 512, 2, 2),
+                                                     (1, 256, 512, 35, 33, 1024, 2, 1), (32, 64, 64, 18, 18, 256, 1, 2)])
+def test_conv2d_f16x3_fused_downsample(N, Cin3, Cin2, H2, W2, Co, s2, G):
+    """conv3 + the block's downsample as one GEMM over concatenated K (mmt_conv2d_f16x3_ds_groups, resnet.py:76-95):
+    relu(conv3(b) + b3 + downsample(x2) + b_d) against float64 within 1e-5 of the output's scale for each of G
+    groups (their own inputs of different ranges, so the two sources' scales differ), split-K shapes included; the
+    max words hold exactly max|y|; a residual operand, a wrong Kp and an inconsistent strided geometry are refused."""
+    import ctypes
+    from mmtrack_amd import _lib, dimpnet
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(N + Cin3 + Cin2 + Co + s2)
+    H, W = (H2 - 1) // s2 + 1, (W2 - 1) // s2 + 1
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    w3 = torch.randn(Co, Cin3, 1, 1, generator=g) / math.sqrt(Cin3)
+    wd = torch.randn(Co, Cin2, 1, 1, generator=g) / math.sqrt(Cin2) * 3.0
+    b3, bd = torch.randn(Co, generator=g) * 0.1, torch.randn(Co, generator=g) * 0.1
+    fu = dimpnet._ConvDs(dimpnet._Conv(w3, bias=b3, dev="cuda", f16x3=True),
+                         dimpnet._Conv(wd, bias=bd, stride=s2, dev="cuda", f16x3=True), "cuda")
+    nw = lib.mmt_conv_max_words()
+    groups, ds, outs, words, refs, keep = [], [], [], [], [], []
+    for i in range(G):
+        b = torch.relu(torch.randn(N, Cin3, H, W, generator=g)) * (1.0 + i)
+        x2 = torch.relu(torch.randn(N, Cin2, H2, W2, generator=g)) * (4.0 - i)
+        refs.append(F.relu(F.conv2d(b.double(), w3.double(), b3.double())
+                           + F.conv2d(x2.double(), wd.double(), bd.double(), stride=s2)))
+        bdev, xdev = b.permute(0, 2, 3, 1).contiguous().cuda(), x2.permute(0, 2, 3, 1).contiguous().cuda()
+        bm = torch.full((nw,), float(b.abs().max()), device="cuda")
+        xm = torch.full((nw,), float(x2.abs().max()), device="cuda")
+        outs.append(torch.empty(N, H, W, Co, device="cuda"))
+        words.append(torch.zeros(nw, device="cuda"))
+        groups.append(fu.group(bdev, outs[i], x_max=bm, y_max=words[i]))
+        ds.append((xdev, xm))
+        keep += [bdev, bm]
+    fu.run(lib, groups, ds, N, H, W, H2, W2, lambda n: torch.empty((n + 3) // 4, device="cuda"), stream)
+    for i in range(G):
+        got = outs[i].permute(0, 3, 1, 2).cpu()
+        close(got, refs[i], 1e-5)
+        assert float(words[i].max()) == float(got.abs().max())
+    arr = (_lib.MmtConvGroup * 1)(groups[0])
+    darr = (_lib.MmtConvDs * 1)(_lib.MmtConvDs(ds[0][0].data_ptr(), ds[0][1].data_ptr(), 0.0))
+    call = lambda h, kp: lib.mmt_conv2d_f16x3_ds_groups(arr, darr, 1, N, h, W, Cin3, H2, W2, Cin2, s2, kp, Co, None, 0,
+                                                        stream)
+    assert call(H, fu.kp + 32) == -1 and call(H + 1, fu.kp) == -1
+    r = torch.zeros(N, H, W, Co, device="cuda")
+    arr[0].resid = r.data_ptr()
+    assert call(H, fu.kp) == -1
+
+
 def test_conv2d_f16x3_stem_padded_input_bitwise():
     """The f16x3 stem over the image padded to 4 channels (mmt_image_normalize4 layout, one 16-B load per tap)
     gives the bits of the stem over the 3-channel image (the same K order, the pad channel's weight is 0)."""
@@ -439,6 +487,35 @@ def test_dimp_tracker_matches_reference_sequence(precision):
         assert dconf[-1] < bar, (t, out["confidence"], gd["confidence"][t], bar)
     print("relative confidence differences per frame:", np.round(dconf, 5).tolist(),
           f"bar {bar:.2e} (2 x the reference's fp32-order spread {reference_spread()})")
+
+
+def test_fused_sampler_bits():
+    """The pools' normalising sampler (mmt_dimp_track_sample_norm4: the 6-channel patch written as the two
+    normalised 4-channel halves the f16x3 backbones read) against the NCHW patch + mmt_image_normalize4 path: the
+    tracker_dimp.npz sequence tracked both ways gives identical boxes, confidences and flags, bit for bit."""
+    from mmtrack_amd import dimp_tracker as mdt
+    from mmtrack_amd import synth
+    from mmtrack_amd.dimp_tracker import DiMP, parameters
+    from mmtrack_amd.dimpnet import DiMPNet
+    gd = np.load(os.path.join(GOLDEN, "tracker_dimp.npz"))
+    seed, n, H, W, C, tseed = [int(v) for v in gd["meta"]]
+    frames, _ = synth.make_frames(seed, 8, H, W, C, box=tuple(gd["init_box"]))
+    net = DiMPNet(synth.make_dimp_state_dict(0), precision="f16x3")
+    runs = []
+    try:
+        for fused in (True, False):
+            mdt.FUSED_SAMPLE = fused
+            tr = DiMP(parameters(), net=net)
+            torch.manual_seed(tseed)
+            tr.initialize(frames[0], {"init_bbox": list(gd["init_box"])})
+            out = []
+            for t in range(1, 8):
+                o = tr.track(frames[t])
+                out.append((list(o["target_bbox"]), o["confidence"], tr.debug_info["flag"]))
+            runs.append(out)
+    finally:
+        mdt.FUSED_SAMPLE = True
+    assert runs[0] == runs[1]
 
 
 @pytest.mark.parametrize("groups", [1, 2])
