@@ -87,6 +87,11 @@ const char* mmt_version(void);
  * instead of silently reading sample 0 everywhere). */
 #define MMT_ABI_VERSION 5
 int mmt_abi_version(void);
+/* pinned host memory that kernels read and write in place (mapped + coherent: a kernel sees the host's latest
+ * writes and the host sees the kernel's after an event, with no copy launch) -- the DiMP pool's frame descriptors
+ * and result records; NULL on failure.  mmt_host_free(NULL) is a no-op.                                     */
+void* mmt_host_alloc(size_t bytes);
+void mmt_host_free(void* p);
 
 /* weights: every reference state_dict key, fp32, row-major (load_state_dict(strict=True)) */
 int mmt_set_tensor(mmt_engine* e, const char* key, const float* data, const int64_t* shape, int ndim);
@@ -369,13 +374,21 @@ int mmt_dimp_track_sample(mmt_dimp_state* states, const mmt_dimp_frame* frames, 
 /* the same patches written as the f16x3 backbones read them: each 6-channel pixel's two halves normalised
  * (((v / 255) - mean) / std, net_wrappers.py:62-72, the arithmetic of mmt_image_normalize4) into out_a / out_b
  * [n][out_h][out_w][4] (zero fourth channel) -- one launch and one patch round trip fewer than
- * mmt_dimp_track_sample + mmt_image_normalize4, the same bits.  Frames must have C == 6.               */
+ * mmt_dimp_track_sample + mmt_image_normalize4, the same bits.  Frames must have C == 6; `frames` may be
+ * device-visible pinned host memory (read in place, no copy launch).  zero_words / n_zero (optional): floats the
+ * launch clears as well (the backbones' sharded max words, cleared before their first producer).          */
 int mmt_dimp_track_sample_norm4(mmt_dimp_state* states, const mmt_dimp_frame* frames, int n,
                                 const mmt_dimp_track_params* p, int out_h, int out_w, const float mean[3],
-                                const float std_[3], float* out_a, float* out_b, void* hip_stream);
+                                const float std_[3], float* out_a, float* out_b, float* zero_words, int64_t n_zero,
+                                void* hip_stream);
 int mmt_dimp_track_update(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
                           const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
                           mmt_dimp_result* results, void* hip_stream);
+/* the same, the records also written straight into host_results (device-visible pinned host memory) by the
+ * kernel that forms them -- the host reads them after an event, without a device-to-host copy launch      */
+int mmt_dimp_track_update_pinned(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
+                                 const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
+                                 mmt_dimp_result* results, mmt_dimp_result* host_results, void* hip_stream);
 /* the filter updates the frame's records ask for, decided on the device: for each of the n sequences (slots
  * of states / results / filters, memory [n][MMT_DIMP_MEMORY][C][H][W]) results[s].num_iter Gauss-Newton steps
  * over its first results[s].n_samples memory samples with its state's boxes and sample weights, in one

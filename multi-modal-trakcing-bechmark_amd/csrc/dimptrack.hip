@@ -104,12 +104,19 @@ struct NormArgs {
   float mean[3], sd[3];
   float* outa;
   float* outb;
+  float* zero;     // optional: words to clear (the backbones' max words)
+  int64_t nzero;
 };
 template <bool NORM4>
 __global__ __launch_bounds__(256) void dimp_sample_kernel(mmt_dimp_state* states, const mmt_dimp_frame* frames,
                                                           mmt_dimp_track_params p, int oh, int ow, float* out,
                                                           NormArgs na) {
   const int s = blockIdx.y;
+  if (NORM4 && na.zero) {   // the backbones' max words cleared here, before their first producer (no fill launch)
+    const int64_t nt = (int64_t)gridDim.x * gridDim.y * 256;
+    for (int64_t k = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x; k < na.nzero; k += nt)
+      na.zero[k] = 0.f;
+  }
   const mmt_dimp_frame fr = frames[s];
   const Geom g = dimp_geometry(states[s], p, fr.H, fr.W);
   if (blockIdx.x == 0 && threadIdx.x < 4) states[s].coords[threadIdx.x] = g.coords[threadIdx.x];
@@ -236,7 +243,8 @@ __device__ int update_sample_weights(float* sw, int num_samp, int num_init, int 
 
 // one workgroup (256 threads) per sequence: scores [n][sh][sw] of this frame -> the tracker's update
 __global__ __launch_bounds__(256) void dimp_localize_kernel(mmt_dimp_state* states, const float* scores, int sh, int sw_,
-                                                            mmt_dimp_track_params p, mmt_dimp_result* results) {
+                                                            mmt_dimp_track_params p, mmt_dimp_result* results,
+                                                            mmt_dimp_result* host_results) {
   __shared__ float sm[1024];
   __shared__ float red_v[64];
   __shared__ int red_i[64];
@@ -405,6 +413,7 @@ __global__ __launch_bounds__(256) void dimp_localize_kernel(mmt_dimp_state* stat
   res.box[2] = st.target_sz[1];
   res.box[3] = st.target_sz[0];
   results[s] = res;
+  if (host_results) host_results[s] = res;   // the record straight into the caller's pinned buffer (no copy launch)
 }
 
 // the frame's features into the memory slot update_sample_weights chose (training_samples[replace_ind] = x)
@@ -438,28 +447,38 @@ int mmt_dimp_track_sample(mmt_dimp_state* states, const mmt_dimp_frame* frames, 
 
 int mmt_dimp_track_sample_norm4(mmt_dimp_state* states, const mmt_dimp_frame* frames, int n,
                                 const mmt_dimp_track_params* p, int out_h, int out_w, const float mean[3],
-                                const float std_[3], float* out_a, float* out_b, void* stream) {
-  if (!states || !frames || !p || !mean || !std_ || !out_a || !out_b || n <= 0 || out_h <= 0 || out_w <= 0)
+                                const float std_[3], float* out_a, float* out_b, float* zero_words, int64_t n_zero,
+                                void* stream) {
+  if (!states || !frames || !p || !mean || !std_ || !out_a || !out_b || n <= 0 || out_h <= 0 || out_w <= 0 ||
+      n_zero < 0 || (n_zero && !zero_words))
     return MMT_E_ARG;
-  NormArgs na{{mean[0], mean[1], mean[2]}, {std_[0], std_[1], std_[2]}, out_a, out_b};
+  NormArgs na{{mean[0], mean[1], mean[2]}, {std_[0], std_[1], std_[2]}, out_a, out_b, zero_words, n_zero};
   const dim3 grid((unsigned)(((int64_t)out_h * out_w + 255) / 256), n);
   hipLaunchKernelGGL(dimp_sample_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, states, frames, *p, out_h,
                      out_w, nullptr, na);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
 }
 
-int mmt_dimp_track_update(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
-                          const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
-                          mmt_dimp_result* results, void* stream) {
+int mmt_dimp_track_update_pinned(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
+                                 const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
+                                 mmt_dimp_result* results, mmt_dimp_result* host_results, void* stream) {
   if (!states || !scores || !p || !feat || !memory || !results || n <= 0 || sh <= 0 || sw <= 0 || sh * sw > 1024 ||
       sw > 64 || feat_elems <= 0 || feat_elems % 4 || p->sample_memory_size != kMem || p->train_skipping <= 0 ||
       p->train_sample_interval <= 0)
     return MMT_E_ARG;
   const hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(dimp_localize_kernel, dim3(n), dim3(256), 0, s, states, scores, sh, sw, *p, results);
+  hipLaunchKernelGGL(dimp_localize_kernel, dim3(n), dim3(256), 0, s, states, scores, sh, sw, *p, results,
+                     host_results);
   hipLaunchKernelGGL(dimp_memory_kernel, dim3((unsigned)((feat_elems / 4 + 255) / 256), n), dim3(256), 0, s, results,
                      feat, feat_elems, memory);
   return hipGetLastError() == hipSuccess ? MMT_OK : MMT_E_HIP;
+}
+
+int mmt_dimp_track_update(mmt_dimp_state* states, int n, const float* scores, int sh, int sw,
+                          const mmt_dimp_track_params* p, const float* feat, int64_t feat_elems, float* memory,
+                          mmt_dimp_result* results, void* stream) {
+  return mmt_dimp_track_update_pinned(states, n, scores, sh, sw, p, feat, feat_elems, memory, results, nullptr,
+                                      stream);
 }
 
 }  // extern "C"

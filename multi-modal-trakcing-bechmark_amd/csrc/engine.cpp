@@ -735,7 +735,7 @@ inline T* off(T* p, size_t o) {
   return p ? p + o : nullptr;
 }
 
-void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int part) {
+void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int part, bool fuse_geom) {
   const auto& c = e->cfg;
   const int Lz = e->Lz, Lx = e->Lx, L = e->L;
   // per-launch activation views: this launch covers launch-relative sequences [r0, r0 + n)
@@ -797,6 +797,16 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
   ca.rows_per_seq = L;
   ca.row0 = Lz;
   ca.dbg_patch = q_dbg_patch;
+  if (fuse_geom) {   // a launch not split into stream parts: the geometry kernel's work done by the crop itself
+    ca.geom.state = e->state_dev + b0;
+    ca.geom.factor = c.search_factor;
+    ca.geom.ring = e->hring;
+    ca.geom.use_ring = e->ring_handoff ? 1 : 0;
+    ca.geom.gidx = q_gidx0;
+    ca.geom.slot2pos = q_slot2pos;
+    ca.geom.Lz = Lz;
+    ca.geom.Lx = Lx;
+  }
   crop_patchify(ca, s);
 
   // 2. patch embedding (template rows were written at initialize)
@@ -948,11 +958,14 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
       ce_a.forced = (e->force_ce && e->ce_forced) ? e->ce_forced + (size_t)b0 * nce * Lx + (size_t)ce_stage * Lx
                                                   : nullptr;
       ++ce_stage;
-      ce_select(ce_a, s);
+      if (!ce_layernorm(ce_a, X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, Na, X2, s, pend)) {
+        ce_select(ce_a, s);
+        layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * (Lz + keep), Lz + keep, q_gather, Na, X2, s,
+                  pend);
+      }
       removed_off += Ls - keep;
       std::swap(gin, gout);
       Ls = keep;
-      layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * (Lz + Ls), Lz + Ls, q_gather, Na, X2, s, pend);
       std::swap(X, X2);
     } else {
       layernorm(X, w.n2w, w.n2b, q_Hn, q_Hn_l, w.ln2_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s, pend);
@@ -1038,6 +1051,10 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
     da.ring_cur = e->hring.cur;
     da.ring_pitch = e->hring.pitch;
     da.row0 = r0;
+    if (fuse_geom) {
+      da.ring_ctr = e->hring.ctr;
+      da.ring_kring = e->hring.kring;
+    }
   }
   decode(da, s);
 }
@@ -1088,18 +1105,23 @@ int stage_frame(mmt_engine* e, int slot, int ring, const uint8_t* frame, int Hh,
 void enqueue_split(mmt_engine* e, int b0, int n) {
   // crop geometry of all n sequences from their device-resident state (and, ring hand-off, their frame
   // parameters from the host ring), once per launch before any part starts
-  crop_geometry(e->params_dev, e->state_dev + b0, n, e->cfg.search_factor, e->cfg.search_size,
-                e->ring_handoff ? &e->hring : nullptr, e->gidx0, e->slot2pos, e->Lz, e->Lx, e->stream);
   if (e->overlap_min <= 0 || n < e->overlap_min || e->probe) {
-    enqueue_forward(e, b0, 0, n, e->stream, 0);
+    // one stream: the crop forms the geometry itself (MMT_GEOM_KERNEL, tuning: the separate geometry kernel)
+    static const bool geom_kernel = getenv("MMT_GEOM_KERNEL") != nullptr;
+    if (geom_kernel)
+      crop_geometry(e->params_dev, e->state_dev + b0, n, e->cfg.search_factor, e->cfg.search_size,
+                    e->ring_handoff ? &e->hring : nullptr, e->gidx0, e->slot2pos, e->Lz, e->Lx, e->stream);
+    enqueue_forward(e, b0, 0, n, e->stream, 0, !geom_kernel);
     return;
   }
+  crop_geometry(e->params_dev, e->state_dev + b0, n, e->cfg.search_factor, e->cfg.search_size,
+                e->ring_handoff ? &e->hring : nullptr, e->gidx0, e->slot2pos, e->Lz, e->Lx, e->stream);
   const int P = std::min(e->nparts, n);
   hipEventRecord(e->fork_ev, e->stream);
   for (int p = 1; p < P; ++p) hipStreamWaitEvent(e->xstream[p - 1], e->fork_ev, 0);
   for (int p = 0; p < P; ++p) {
     const int r0 = n * p / P, r1 = n * (p + 1) / P;
-    enqueue_forward(e, b0 + r0, r0, r1 - r0, p ? e->xstream[p - 1] : e->stream, p);
+    enqueue_forward(e, b0 + r0, r0, r1 - r0, p ? e->xstream[p - 1] : e->stream, p, false);
   }
   for (int p = 1; p < P; ++p) {
     hipEventRecord(e->join_ev[p - 1], e->xstream[p - 1]);
@@ -1176,6 +1198,14 @@ extern "C" {
 
 const char* mmt_version(void) { return "mmtrack-mi355x 0.1 (gfx950)"; }
 int mmt_abi_version(void) { return MMT_ABI_VERSION; }
+void* mmt_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (!bytes || hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+  return p;
+}
+void mmt_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
 
 int mmt_create(const mmt_config* cfg, int device, mmt_engine** out) {
   if (!cfg || !out) return MMT_E_ARG;

@@ -22,9 +22,62 @@ __device__ __forceinline__ int crop_px(const CropParam& p, int r, int x, int c) 
   return p.frame[(int64_t)yy * p.stride + (int64_t)xx * p.C + c];
 }
 
+// processing_utils.py:32-41: crop_sz = ceil(sqrt(w h) factor) ('Too small bounding box.' if < 1),
+// x1 = round(x + w/2 - crop_sz/2) with python's round (half to even)
+__device__ void geometry_of(const double box[4], double factor, int out_sz, CropParam& p, double& rf, int& err) {
+#pragma clang fp contract(off)
+  const double x = box[0], y = box[1], w = box[2], h = box[3];
+  const double cs = ceil(sqrt(w * h) * factor);
+  err = 0;
+  if (!(cs >= 1.0)) err = -5;           // MMT_E_BOX
+  else if (cs > 1e6) err = -1;          // MMT_E_ARG
+  if (err) {                            // a harmless crop; the frame's result is discarded
+    p.x1 = p.y1 = 0;
+    p.crop_sz = 1;
+    rf = 1.0;
+  } else {
+    p.crop_sz = (int)cs;
+    p.x1 = (int)rint(x + 0.5 * w - cs * 0.5);
+    p.y1 = (int)rint(y + 0.5 * h - cs * 0.5);
+    rf = (double)out_sz / cs;
+  }
+}
+// FUSED_GEOM (launches that are not split into stream parts: the one-sequence frame): the geometry kernel's work
+// done here -- every workgroup derives its sequence's crop from the device state (and the frame from the host ring
+// entry) itself; workgroup 0 of each sequence stores the parameters, rf / err and the token index reset, and
+// records the ring entry for decode, which advances the counter (g.ring_advance) -- one launch fewer
+template <bool FUSED_GEOM>
 __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
   const int b = blockIdx.y;
-  const CropParam p = a.params[b];
+  CropParam p = a.params[b];
+  if constexpr (FUSED_GEOM) {
+    const GeomArgs& g = a.geom;
+    const int e = g.use_ring ? *g.ring.ctr : 0;
+    if (g.use_ring) {
+      const CropParam h = g.ring.params[(int64_t)e * g.ring.pitch + b];
+      p.frame = h.frame;
+      p.stride = h.stride;
+      p.H = h.H;
+      p.W = h.W;
+      p.C = h.C;
+    }
+    double rf;
+    int err;
+    geometry_of(g.state[b].box, g.factor, a.out_sz, p, rf, err);
+    if (blockIdx.x == 0) {
+      if (threadIdx.x == 0) {
+        const_cast<CropParam*>(a.params)[b] = p;
+        g.state[b].rf = rf;
+        g.state[b].err = err;
+        if (g.use_ring && b == 0) *g.ring.cur = e;
+      }
+      if (g.gidx)
+        for (int j = threadIdx.x; j < g.Lx; j += blockDim.x) {
+          g.gidx[b * g.Lx + j] = j;
+          g.slot2pos[b * g.Lx + j] = g.Lz + j;
+        }
+    }
+  }
   const int O = a.out_sz;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= O * O) return;
@@ -52,7 +105,11 @@ __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
 }
 
 void crop_patchify(const CropArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(crop_kernel, dim3((a.out_sz * a.out_sz + 255) / 256, a.B), dim3(256), 0, s, a);
+  const dim3 grid((a.out_sz * a.out_sz + 255) / 256, a.B);
+  if (a.geom.state)
+    hipLaunchKernelGGL(crop_kernel<true>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(crop_kernel<false>, grid, dim3(256), 0, s, a);
 }
 
 // ------------------------------------------------------------------ decode
@@ -62,32 +119,18 @@ __device__ __forceinline__ float sigmoid_clamp(float x) {
 }
 
 // ------------------------------------------------------------------ tracker state on the device
-// No FMA contraction in these two functions (pragma at the top of each body): every product and sum
+// No FMA contraction in update_state and geometry_of (pragma at the top of each body): every product and sum
 // rounds as in the reference's python doubles (and float32 tensor ops where it computes on tensors).
 __device__ __forceinline__ double dmax(double a, double b) { return a < b ? b : a; }   // std::max / python max
 __device__ __forceinline__ double dmin(double a, double b) { return b < a ? b : a; }   // std::min / python min
 
-// processing_utils.py:32-41: crop_sz = ceil(sqrt(w h) factor) ('Too small bounding box.' if < 1),
-// x1 = round(x + w/2 - crop_sz/2) with python's round (half to even)
+// geometry_of into the device parameters and state (geometry_kernel)
 __device__ void geometry_one(CropParam* params, SeqState* state, int i, double factor, int out_sz) {
-#pragma clang fp contract(off)
   SeqState& st = state[i];
-  const double x = st.box[0], y = st.box[1], w = st.box[2], h = st.box[3];
-  const double cs = ceil(sqrt(w * h) * factor);
-  int err = 0;
-  if (!(cs >= 1.0)) err = -5;           // MMT_E_BOX
-  else if (cs > 1e6) err = -1;          // MMT_E_ARG
-  CropParam& p = params[i];
-  if (err) {                            // a harmless crop; the frame's result is discarded
-    p.x1 = p.y1 = 0;
-    p.crop_sz = 1;
-    st.rf = 1.0;
-  } else {
-    p.crop_sz = (int)cs;
-    p.x1 = (int)rint(x + 0.5 * w - cs * 0.5);
-    p.y1 = (int)rint(y + 0.5 * h - cs * 0.5);
-    st.rf = (double)out_sz / cs;
-  }
+  double rf;
+  int err;
+  geometry_of(st.box, factor, out_sz, params[i], rf, err);
+  st.rf = rf;
   st.err = err;
 }
 
@@ -176,6 +219,11 @@ __global__ __launch_bounds__(256) void decode_kernel(const DecodeArgs a) {
   __shared__ int si[256];
   __shared__ float sw[5 * 32 + 5];
   const int b = blockIdx.x, tid = threadIdx.x, n = a.fs * a.fs;
+  // (a crop with the geometry fused in read the ring counter; the launch's last kernel advances it)
+  if (a.ring_ctr && b == 0 && tid == 0) {
+    const int e = *a.ring_cur;
+    *a.ring_ctr = e + 1 == a.ring_kring ? 0 : e + 1;
+  }
   if (tid < 165) sw[tid] = tid < 160 ? a.w5[tid] : a.b5[tid - 160];
   __syncthreads();
   float best = -INFINITY;

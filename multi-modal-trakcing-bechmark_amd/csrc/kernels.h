@@ -168,6 +168,10 @@ struct CEArgs {
   int keys_pitch;         // floats between sequences of forced / keys_out
 };
 void ce_select(const CEArgs& a, hipStream_t s);
+// ce_select + the LN2 that gathers the survivors (layernorm with a.gather), one launch for few sequences; false:
+// not taken (the caller launches the two)
+bool ce_layernorm(const CEArgs& a, const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo,
+                  float out_scale, int in_rows_per_seq, float* xcopy, hipStream_t s, const RowReduce& rr);
 
 // final norm + token recovery (zeros at pruned slots) -> head input NHWC bf16 [B][Lx][768]
 // feat_lo non-null: feat / feat_lo are the f16x3 halves of the normed rows * feat_scale
@@ -189,6 +193,22 @@ struct CropParam {                 // one per sequence (device memory, rewritten
   int x1, y1, crop_sz;             // processing_utils.py:32-41
   int pad_;
 };
+struct SeqState;
+struct RingArgs {
+  const CropParam* params;   // device-visible pinned [kring][pitch]
+  TrackOut* outs;            // device-visible pinned [kring][pitch] (decode writes the launch's results)
+  int* ctr;                  // launches so far mod kring (device; the ring entry of the next launch)
+  int* cur;                  // ring entry of the launch in flight (device)
+  int kring, pitch;
+};
+struct GeomArgs {                  // crop_kernel<FUSED_GEOM>: the geometry kernel's operands (state null: not fused)
+  SeqState* state;
+  double factor;
+  RingArgs ring;
+  int use_ring;
+  int* gidx; int* slot2pos;
+  int Lz, Lx;
+};
 struct CropArgs {
   const CropParam* params;         // [B]
   int B, out_sz, C;                // C = 6 (RGB+aux) or 3
@@ -197,6 +217,7 @@ struct CropArgs {
                                        // normalised pixel * kPixScale
   int rows_per_seq, row0;          // patch rows land at row0 + patch index
   uint8_t* dbg_patch;              // optional [B][out][out][C]
+  GeomArgs geom;                   // state non-null: the crop geometry formed in this launch (no geometry_kernel)
 };
 void crop_patchify(const CropArgs& a, hipStream_t s);
 constexpr float kPixScale = 4096.0f;   // |(p/255 - mean) / std| <= 2.64: 2^12 keeps the f16x3 halves below 2^14
@@ -218,13 +239,6 @@ struct SeqState {                  // one per slot
 // Ring hand-off (ring non-null): the frame fields of params[i] are first read from the host's pinned
 // ring entry ring->params[(ctr % kring) * pitch + i] (no copy launch), then *cur <- that entry and
 // ctr advances -- one per launch, in the same order as the host's tickets.
-struct RingArgs {
-  const CropParam* params;   // device-visible pinned [kring][pitch]
-  TrackOut* outs;            // device-visible pinned [kring][pitch] (decode writes the launch's results)
-  int* ctr;                  // launches so far mod kring (device; the ring entry of the next launch)
-  int* cur;                  // ring entry of the launch in flight (device)
-  int kring, pitch;
-};
 // (gidx / slot2pos non-null: also the launch's token index arrays, [n][Lx] each, as before any elimination)
 void crop_geometry(CropParam* params, SeqState* state, int n, double factor, int out_sz, const RingArgs* ring,
                    int* gidx, int* slot2pos, int Lz, int Lx, hipStream_t s);
@@ -245,6 +259,8 @@ struct DecodeArgs {
   TrackOut* ring_outs;             // ring hand-off (or null): out rows also go to ring_outs[*ring_cur * pitch + row0 + b]
   const int* ring_cur;
   int ring_pitch, row0;
+  int* ring_ctr;                   // non-null (the crop formed the geometry): advance the ring counter, mod ring_kring
+  int ring_kring;
 };
 void decode(const DecodeArgs& a, hipStream_t s);
 

@@ -627,6 +627,90 @@ void ce_select(const CEArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(ce_select_kernel, dim3(a.B), dim3(CE_THREADS), 0, s, a);
 }
 
+// Candidate elimination and the LN2 that gathers its survivors in one launch (few sequences: the one-sequence
+// frame, where the select kernel is a latency-bound launch of its own).  Grid (row blocks of one sequence, B): every
+// workgroup forms the sequence's head-mean keys and ranks (the arithmetic of ce_select_kernel: the same sums in the
+// same order, and a rank is an integer count whatever order it is counted in), keeps the inverse (rank -> token) map
+// in LDS and LayerNorms its four compact rows from their gathered source rows, as ln_kernel with the gather would;
+// workgroup 0 of each sequence also writes the index arrays ce_select_kernel writes.  Ls <= 1024.
+template <bool RR>
+__global__ __launch_bounds__(256) void ce_ln_kernel(const CEArgs a, const float* x, const float* w, const float* b,
+                                                    bf16_t* ob, bf16_t* olo, float oscale, int in_rows_per_seq,
+                                                    float* xcopy, const RowReduce rr) {
+  __shared__ float key[1024];
+  __shared__ int inv[1024];
+  const int bs = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const float* prob = a.prob + (int64_t)bs * a.heads * a.Ls;
+  for (int i = tid; i < a.Ls; i += 256) {
+    float v[CE_MAX_HEADS];
+#pragma unroll
+    for (int h = 0; h < CE_MAX_HEADS; ++h) v[h] = h < a.heads ? prob[h * a.Ls + i] : 0.f;
+    float sum = 0.f;
+#pragma unroll
+    for (int h = 0; h < CE_MAX_HEADS; ++h)
+      if (h < a.heads) sum += v[h];
+    for (int h = CE_MAX_HEADS; h < a.heads; ++h) sum += prob[h * a.Ls + i];
+    sum = sum / (float)a.heads;
+    if (a.keys_out || a.forced) {   // parity diagnostics only
+      const int slot = a.gidx_in[bs * a.Ls + i];
+      if (a.keys_out && blockIdx.x == 0) a.keys_out[(int64_t)bs * a.keys_pitch + slot] = sum;
+      if (a.forced) sum = a.forced[(int64_t)bs * a.keys_pitch + slot];
+    }
+    key[i] = sum;
+  }
+  __syncthreads();
+  const int Ln = a.Lz + a.keep;
+  for (int i = tid; i < a.Ls; i += 256) {
+    const float ki = key[i];
+    int rank = 0;
+    for (int j = 0; j < a.Ls; ++j) rank += before(key[j], j, ki, i) ? 1 : 0;
+    if (rank < a.keep) inv[rank] = i;
+    if (blockIdx.x == 0) {
+      const int slot = a.gidx_in[bs * a.Ls + i];
+      if (rank < a.keep) {
+        a.gidx_out[bs * a.keep + rank] = slot;
+        a.gather[bs * Ln + a.Lz + rank] = a.Lz + i;
+        a.slot2pos[bs * a.Lx + slot] = a.Lz + rank;
+      } else {
+        a.removed[bs * a.Lx + a.removed_off + (rank - a.keep)] = slot;
+        a.slot2pos[bs * a.Lx + slot] = -1;
+      }
+    }
+  }
+  if (blockIdx.x == 0)
+    for (int t = tid; t < a.Lz; t += 256) a.gather[bs * Ln + t] = t;
+  __syncthreads();
+  const int p = blockIdx.x * 4 + (tid >> 6);   // compact row of the sequence
+  if (p >= Ln) return;
+  const int64_t r = (int64_t)bs * Ln + p;
+  const int64_t src = (int64_t)bs * in_rows_per_seq + (p < a.Lz ? p : a.Lz + inv[p - a.Lz]);
+  Row12 xv = load_row(x + src * C768, lane);
+  if (RR && rr.ws) {
+    xv = apply_reduce(xv, rr, src, lane);
+    if (!xcopy) store_f32(const_cast<float*>(x) + src * C768, xv, lane);
+  }
+  if (xcopy) store_f32(xcopy + r * C768, xv, lane);
+  const Row12 y = ln_row(xv, w, b, lane);
+  if (olo) store_split(ob + r * C768, olo + r * C768, y, oscale, lane);
+  else if (ob) store_bf16(ob + r * C768, y, lane);
+}
+
+bool ce_layernorm(const CEArgs& a, const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo,
+                  float out_scale, int in_rows_per_seq, float* xcopy, hipStream_t s, const RowReduce& rr) {
+  // MMT_CE_FUSED (tuning): 0 never, else the largest batch that takes the fused launch (default 0 until the bf16
+  // batch-vs-single mismatch it showed is understood, tools/runs_r5/r5_run14.sh)
+  static const int maxb = getenv("MMT_CE_FUSED") ? atoi(getenv("MMT_CE_FUSED")) : 0;
+  if (a.B > maxb || a.Ls > 1024) return false;
+  const dim3 grid((a.Lz + a.keep + 3) / 4, a.B);
+  if (rr.ws)
+    hipLaunchKernelGGL(ce_ln_kernel<true>, grid, dim3(256), 0, s, a, x, w, b, out_bf16, out_lo, out_scale,
+                       in_rows_per_seq, xcopy, rr);
+  else
+    hipLaunchKernelGGL(ce_ln_kernel<false>, grid, dim3(256), 0, s, a, x, w, b, out_bf16, out_lo, out_scale,
+                       in_rows_per_seq, xcopy, rr);
+  return true;
+}
+
 // ------------------------------------------------------------------ final norm + recover_tokens
 // vit_ce_prompt.py:318-339: LN over the surviving tokens, then scatter the search tokens back
 // to their 16x16 slots; pruned slots are exact zeros.

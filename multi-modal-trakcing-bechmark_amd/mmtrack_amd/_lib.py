@@ -183,8 +183,13 @@ SIGNATURES = {
     "mmt_dimp_track_optimize": (_I, [_P, _I, _P, _P, _I, _I, _I, _P, _I, _I, ctypes.POINTER(MmtDimpParams), _I, _P,
                                      ctypes.c_size_t, _P]),
     "mmt_dimp_track_sample": (_I, [_P, _P, _I, ctypes.POINTER(MmtDimpTrackParams), _I, _I, _P, _P]),
-    "mmt_dimp_track_sample_norm4": (_I, [_P, _P, _I, ctypes.POINTER(MmtDimpTrackParams), _I, _I, _P, _P, _P, _P, _P]),
+    "mmt_dimp_track_sample_norm4": (_I, [_P, _P, _I, ctypes.POINTER(MmtDimpTrackParams), _I, _I, _P, _P, _P, _P, _P,
+                                         ctypes.c_int64, _P]),
     "mmt_dimp_track_update": (_I, [_P, _I, _P, _I, _I, ctypes.POINTER(MmtDimpTrackParams), _P, _I64, _P, _P, _P]),
+    "mmt_dimp_track_update_pinned": (_I, [_P, _I, _P, _I, _I, ctypes.POINTER(MmtDimpTrackParams), _P, _I64, _P, _P, _P,
+                                          _P]),
+    "mmt_host_alloc": (_P, [ctypes.c_size_t]),
+    "mmt_host_free": (None, [_P]),
     "mmt_gemm_stamps": (_I, [_P]),
     "mmt_op_gemm": (_I, [_P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _I, _I, _I, _I, _I, _P]),
     "mmt_gemm_force_config": (_I, [_I]),

@@ -371,13 +371,22 @@ class DimpPool:
         # frame descriptors: one pinned host copy per record parity, copied to the device without a stream sync;
         # a parity's pinned rows (descriptors and staged host frames) are rewritten only after the copies of its
         # previous launch have run (its event, normally long complete when the host is one frame behind)
+        # frame descriptors and result records in mapped, coherent pinned memory (mmt_host_alloc) that the kernels
+        # read and write in place: no copy launches (the sampler reads a launch's descriptors, the localisation
+        # kernel writes its records); two parities, so frame k + 1 may be launched before frame k's records are read
         fb = ctypes.sizeof(_lib.MmtDimpFrame)
-        self.desc_host = [torch.zeros(capacity * fb, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
-        self.frames = torch.empty(capacity * fb, dtype=torch.uint8, device=self.dev)
+        self._host_ptrs = []
+
+        def host_buffer(nbytes):
+            ptr = self.lib.mmt_host_alloc(nbytes)
+            if not ptr:
+                raise RuntimeError("mmt_host_alloc failed")
+            self._host_ptrs.append(ptr)
+            return torch.frombuffer((ctypes.c_uint8 * nbytes).from_address(ptr), dtype=torch.uint8)
+        self.desc_host = [host_buffer(capacity * fb) for _ in range(2)]
         self._stage = {}      # (slot, parity) -> pinned host staging of a numpy frame
-        self._copy_ev = {}    # (first slot, parity) -> event after the launch's host-to-device copies
-        # two pinned record buffers: frame k + 1 may be launched (its records copied) before frame k's are read
-        self.res_host = [torch.empty(capacity * self.rbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self._copy_ev = {}    # (first slot, parity) -> event after the launch's reads of its descriptors / staging
+        self.res_host = [host_buffer(capacity * self.rbytes) for _ in range(2)]
         self._parity = {}   # per first slot: the record buffer its next launch uses
         self.max_iter = max(p.net_opt_update_iter, p.net_opt_hn_iter, p.net_opt_low_iter) if p.update_classifier else 0
         self._opt_ws = None
@@ -426,49 +435,49 @@ class DimpPool:
             prev.synchronize()   # this parity's pinned rows are still being read by the launch two frames back
         fr = [self._device_frame(first + i, buf, f) for i, f in enumerate(frames)]
         fb = ctypes.sizeof(_lib.MmtDimpFrame)
-        desc = (_lib.MmtDimpFrame * n).from_address(self.desc_host[buf].data_ptr() + first * fb)
+        desc_ptr = self.desc_host[buf].data_ptr() + first * fb
+        desc = (_lib.MmtDimpFrame * n).from_address(desc_ptr)
         for i, f in enumerate(fr):
             d = desc[i]
             d.data, d.stride, d.H, d.W, d.C = f.data_ptr(), f.stride(0), f.shape[0], f.shape[1], f.shape[2]
-        self.frames[first * fb:(first + n) * fb].copy_(self.desc_host[buf][first * fb:(first + n) * fb],
-                                                        non_blocking=True)
-        cev = torch.cuda.Event()
-        cev.record()
-        self._copy_ev[(first, buf)] = cev
         sz = [int(v) for v in self.tparams.img_sample_sz]
         C = fr[0].shape[2]
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
         if net.precision == "f16x3" and C == 6 and FUSED_SAMPLE:
             # the sampler writes the backbones' normalised 4-channel halves itself (same bits as sample + normalise)
+            # (and clears the backbones' max words: no fill launch)
             xa, xb = net.norm4_buffers(n, sz[0], sz[1])
-            rc = lib.mmt_dimp_track_sample_norm4(ctypes.c_void_p(self.state_ptr(first)),
-                                                 ctypes.c_void_p(self.frames.data_ptr() + first * fb), n,
+            words = net.max_words()
+            rc = lib.mmt_dimp_track_sample_norm4(ctypes.c_void_p(self.state_ptr(first)), ctypes.c_void_p(desc_ptr), n,
                                                  ctypes.byref(self.tparams), sz[0], sz[1], net._mean, net._std,
                                                  ctypes.c_void_p(xa.data_ptr()), ctypes.c_void_p(xb.data_ptr()),
-                                                 stream)
+                                                 ctypes.c_void_p(words.data_ptr()), words.numel(), stream)
             if rc != 0:
                 raise RuntimeError(f"mmt_dimp_track_sample_norm4 failed ({rc})")
-            layer3 = net.extract_backbone_norm4(n, sz[0], sz[1])
+            self._descriptors_read(first, buf)
+            layer3 = net.extract_backbone_norm4(n, sz[0], sz[1], words_cleared=True)
         else:
             patches = torch.empty(n, C, sz[0], sz[1], dtype=torch.float32, device=self.dev)
-            rc = lib.mmt_dimp_track_sample(ctypes.c_void_p(self.state_ptr(first)),
-                                           ctypes.c_void_p(self.frames.data_ptr() + first * fb), n,
+            rc = lib.mmt_dimp_track_sample(ctypes.c_void_p(self.state_ptr(first)), ctypes.c_void_p(desc_ptr), n,
                                            ctypes.byref(self.tparams), sz[0], sz[1],
                                            ctypes.c_void_p(patches.data_ptr()), stream)
             if rc != 0:
                 raise RuntimeError(f"mmt_dimp_track_sample failed ({rc})")
+            self._descriptors_read(first, buf)
             layer3 = net.extract_backbone(patches)
         test_x = net.extract_classification_feat(layer3)
         from .dimp import apply_filter
         scores = apply_filter(test_x.unsqueeze(0), self.filters[first:first + n])[0].contiguous()
         F_ = test_x[0].numel()
-        rc = lib.mmt_dimp_track_update(ctypes.c_void_p(self.state_ptr(first)), n, ctypes.c_void_p(scores.data_ptr()),
-                                       scores.shape[-2], scores.shape[-1], ctypes.byref(self.tparams),
-                                       ctypes.c_void_p(test_x.data_ptr()), F_,
-                                       ctypes.c_void_p(self.memory[first].data_ptr()),
-                                       ctypes.c_void_p(self.results.data_ptr() + first * self.rbytes), stream)
+        rc = lib.mmt_dimp_track_update_pinned(ctypes.c_void_p(self.state_ptr(first)), n,
+                                              ctypes.c_void_p(scores.data_ptr()), scores.shape[-2], scores.shape[-1],
+                                              ctypes.byref(self.tparams), ctypes.c_void_p(test_x.data_ptr()), F_,
+                                              ctypes.c_void_p(self.memory[first].data_ptr()),
+                                              ctypes.c_void_p(self.results.data_ptr() + first * self.rbytes),
+                                              ctypes.c_void_p(self.res_host[buf].data_ptr() + first * self.rbytes),
+                                              stream)
         if rc != 0:
-            raise RuntimeError(f"mmt_dimp_track_update failed ({rc})")
+            raise RuntimeError(f"mmt_dimp_track_update_pinned failed ({rc})")
         # update_classifier's Gauss-Newton steps where the records ask for them (dimp.py:555-570), decided on
         # the device: one launch sequence over the batch, no host round trip
         if self.max_iter > 0:
@@ -487,11 +496,24 @@ class DimpPool:
             if rc != 0:
                 raise RuntimeError(f"mmt_dimp_track_optimize failed ({rc})")
         self._parity[first] = buf ^ 1
-        self.res_host[buf][first * self.rbytes:(first + n) * self.rbytes].copy_(
-            self.results[first * self.rbytes:(first + n) * self.rbytes], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return ev, buf
+
+    def _descriptors_read(self, first, buf):
+        """An event behind the kernel that read this parity's descriptors (and host-staged frames): they are
+        rewritten two frames later only once it has passed."""
+        cev = torch.cuda.Event()
+        cev.record()
+        self._copy_ev[(first, buf)] = cev
+
+    def __del__(self):
+        for p in getattr(self, "_host_ptrs", []):
+            try:
+                self.lib.mmt_host_free(p)
+            except Exception:
+                pass
+        self._host_ptrs = []
 
     def _device_frame(self, slot, buf, image):
         """A frame on the device without a blocking copy: device tensors as they are, host frames through a

@@ -401,16 +401,22 @@ class DiMPNet:
             raise ValueError("norm4 buffers: f16x3 only")
         return self._buf("xa", N * H * W * 4), self._buf("xb", N * H * W * 4)
 
-    def extract_backbone_norm4(self, N, H, W):
-        """extract_backbone on the patches already normalised into norm4_buffers(N, H, W)."""
-        xa, xb = self.norm4_buffers(N, H, W)
-        return self._backbones(xa, xb, N, H, W, self._stream())
+    def max_words(self):
+        """f16x3: the device words of every tensor's sharded max|y| (zeroed before each extract_backbone)."""
+        return self._max_words
 
-    def _backbones(self, xa, xb, N, H, W, s):
+    def extract_backbone_norm4(self, N, H, W, words_cleared=False):
+        """extract_backbone on the patches already normalised into norm4_buffers(N, H, W); words_cleared: the
+        max words were zeroed by an earlier launch on the stream (the normalising sampler)."""
+        xa, xb = self.norm4_buffers(N, H, W)
+        return self._backbones(xa, xb, N, H, W, self._stream(), words_cleared)
+
+    def _backbones(self, xa, xb, N, H, W, s, words_cleared=False):
         Hf, Wf = (H + 15) // 16, (W + 15) // 16
         out = torch.empty(N, Hf, Wf, 1024, dtype=torch.float32, device=self.dev)
         if self._max_words is not None:
-            self._max_words.zero_()
+            if not words_cleared:
+                self._max_words.zero_()
             self._nslot = 0
         out_max = self._slot()
         h, w = self._resnets([xa, xb], N, H, W, out, s, out_max)

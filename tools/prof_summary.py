@@ -1,9 +1,10 @@
 """Per-step kernel time breakdown from a rocprofv3 --stats kernel_stats.csv (tuning tool).
 
 usage: prof_summary.py kernel_stats.csv [steps|auto] [rows]
-Steps default to 'auto': the number of geometry_kernel dispatches, which the engine issues exactly once per
-mmt_track_batch launch (before the stream halves fork), so every launched step -- warm-up and timed alike --
-is counted once and per-step figures are exact for runs whose launches all have one shape (--probe none)."""
+Steps default to 'auto': the number of geometry_kernel dispatches (once per mmt_track_batch launch split into stream
+halves, before they fork) plus crop_kernel<true> dispatches (a one-stream launch forms its geometry in the crop, once
+per launch), so every launched step -- warm-up and timed alike -- is counted once and per-step figures are exact for
+runs whose launches all have one shape (--probe none)."""
 import csv
 import sys
 
@@ -11,7 +12,8 @@ path = sys.argv[1]
 rows = list(csv.DictReader(open(path)))
 arg = sys.argv[2] if len(sys.argv) > 2 else "auto"
 if arg == "auto":
-    steps = float(sum(float(r["Calls"]) for r in rows if "geometry_kernel" in r["Name"]))
+    steps = float(sum(float(r["Calls"]) for r in rows
+                      if "geometry_kernel" in r["Name"] or "crop_kernel<true>" in r["Name"]))
     if not steps:   # the mfDiMP path: one dimp_localize_kernel per tracked frame of the batch
         steps = float(sum(float(r["Calls"]) for r in rows if "dimp_localize_kernel" in r["Name"]))
 else:
