@@ -24,45 +24,58 @@ __device__ __forceinline__ Row12 zero_row() {
   return r;
 }
 
-// LayerNorm over 768 (F.layer_norm semantics: biased variance, eps inside sqrt)
+// LayerNorm over 768 (F.layer_norm semantics: biased variance, eps inside sqrt).  The arithmetic is spelled out
+// (contraction off, the fused multiply-adds written as fmaf) so that every kernel inlining it rounds the same way:
+// left to the compiler, ln_kernel and the fused CE + LN2 kernel contracted different products and their rows
+// differed in the last bits (tools/runs_r5/r5_run15.sh)
+__device__ __forceinline__ float sumsq4(float4 d, float acc) {
+#pragma clang fp contract(off)
+  float t = d.x * d.x;
+  t = __builtin_fmaf(d.y, d.y, t);
+  t = __builtin_fmaf(d.z, d.z, t);
+  t = __builtin_fmaf(d.w, d.w, t);
+  return acc + t;
+}
 __device__ __forceinline__ Row12 ln_row(const Row12& x, const float* w, const float* b, int lane) {
+#pragma clang fp contract(off)
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) s += x.v[i].x + x.v[i].y + x.v[i].z + x.v[i].w;
+  for (int i = 0; i < 3; ++i) s += ((x.v[i].x + x.v[i].y) + x.v[i].z) + x.v[i].w;
   const float mean = wave_sum(s) * (1.0f / C768);
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const float4 d = make_float4(x.v[i].x - mean, x.v[i].y - mean, x.v[i].z - mean, x.v[i].w - mean);
-    q += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
-  }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / C768) + LN_EPS);
+  for (int i = 0; i < 3; ++i)
+    q = sumsq4(make_float4(x.v[i].x - mean, x.v[i].y - mean, x.v[i].z - mean, x.v[i].w - mean), q);
+  const float rstd = 1.0f / sqrtf(__builtin_fmaf(wave_sum(q), 1.0f / C768, LN_EPS));
   Row12 y;
   const float4* w4 = reinterpret_cast<const float4*>(w);
   const float4* b4 = reinterpret_cast<const float4*>(b);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float4 ww = w4[lane + 64 * i], bb = b4[lane + 64 * i];
-    y.v[i] = make_float4((x.v[i].x - mean) * rstd * ww.x + bb.x, (x.v[i].y - mean) * rstd * ww.y + bb.y,
-                         (x.v[i].z - mean) * rstd * ww.z + bb.z, (x.v[i].w - mean) * rstd * ww.w + bb.w);
+    y.v[i] = make_float4(__builtin_fmaf((x.v[i].x - mean) * rstd, ww.x, bb.x),
+                         __builtin_fmaf((x.v[i].y - mean) * rstd, ww.y, bb.y),
+                         __builtin_fmaf((x.v[i].z - mean) * rstd, ww.z, bb.z),
+                         __builtin_fmaf((x.v[i].w - mean) * rstd, ww.w, bb.w));
   }
   return y;
 }
 
 // (x - mean) * rstd, the affine applied by the caller (or folded into the consumer's weights)
 __device__ __forceinline__ Row12 ln_hat(const Row12& x) {
+#pragma clang fp contract(off)
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) s += x.v[i].x + x.v[i].y + x.v[i].z + x.v[i].w;
+  for (int i = 0; i < 3; ++i) s += ((x.v[i].x + x.v[i].y) + x.v[i].z) + x.v[i].w;
   const float mean = wave_sum(s) * (1.0f / C768);
   float q = 0.f;
   Row12 d;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     d.v[i] = make_float4(x.v[i].x - mean, x.v[i].y - mean, x.v[i].z - mean, x.v[i].w - mean);
-    q += d.v[i].x * d.v[i].x + d.v[i].y * d.v[i].y + d.v[i].z * d.v[i].z + d.v[i].w * d.v[i].w;
+    q = sumsq4(d.v[i], q);
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / C768) + LN_EPS);
+  const float rstd = 1.0f / sqrtf(__builtin_fmaf(wave_sum(q), 1.0f / C768, LN_EPS));
 #pragma unroll
   for (int i = 0; i < 3; ++i) d.v[i] = make_float4(d.v[i].x * rstd, d.v[i].y * rstd, d.v[i].z * rstd, d.v[i].w * rstd);
   return d;
@@ -119,7 +132,9 @@ __device__ __forceinline__ Row12 apply_reduce(const Row12& x, const RowReduce& r
       if (sl < rr.ks) acc += p[sl][i];
     const float4 bv = reinterpret_cast<const float4*>(rr.bias)[lane + 64 * i];
     const float sc = rr.inv;
-    const float v[4] = {acc[0] * sc + bv.x, acc[1] * sc + bv.y, acc[2] * sc + bv.z, acc[3] * sc + bv.w};
+    // (explicit fmaf: the same rounding in every consumer kernel, see ln_row)
+    const float v[4] = {__builtin_fmaf(acc[0], sc, bv.x), __builtin_fmaf(acc[1], sc, bv.y),
+                        __builtin_fmaf(acc[2], sc, bv.z), __builtin_fmaf(acc[3], sc, bv.w)};
     const float4 r = x.v[i];
     o.v[i] = make_float4(r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]);
   }
@@ -697,9 +712,8 @@ __global__ __launch_bounds__(256) void ce_ln_kernel(const CEArgs a, const float*
 
 bool ce_layernorm(const CEArgs& a, const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo,
                   float out_scale, int in_rows_per_seq, float* xcopy, hipStream_t s, const RowReduce& rr) {
-  // MMT_CE_FUSED (tuning): 0 never, else the largest batch that takes the fused launch (default 0 until the bf16
-  // batch-vs-single mismatch it showed is understood, tools/runs_r5/r5_run14.sh)
-  static const int maxb = getenv("MMT_CE_FUSED") ? atoi(getenv("MMT_CE_FUSED")) : 0;
+  // MMT_CE_FUSED (tuning): 0 never, else the largest batch that takes the fused launch (default 2)
+  static const int maxb = getenv("MMT_CE_FUSED") ? atoi(getenv("MMT_CE_FUSED")) : 2;
   if (a.B > maxb || a.Ls > 1024) return false;
   const dim3 grid((a.Lz + a.keep + 3) / 4, a.B);
   if (rr.ws)
