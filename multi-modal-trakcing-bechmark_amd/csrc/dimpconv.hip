@@ -69,6 +69,7 @@ struct ConvF16Args {
   // a downsample fused into a 1 x 1 conv3 (conv_f16x3_deep_kernel only): K-tiles from Cin / 32 on read x2 at
   // output pixel (oy, ox) * stride2; 0: none
   int Cin2, H2, W2, stride2;
+  int staged_epi;                 // conv_f16x3_deep_kernel (BM 128): the LDS-staged epilogue
 };
 
 __device__ __forceinline__ int cswz(int r, int c) { return r * 32 + ((c ^ ((r >> 2) & 2)) << 3); }   // gemm.hip swzk<32>
@@ -84,13 +85,18 @@ __device__ __forceinline__ ConvGroupArgs pick_group(const ConvF16Args& a, int gr
   return grp ? a.g[1] : a.g[0];   // a select, not a dynamic index (which would copy the arguments to scratch)
 }
 
-// the epilogue arithmetic shared by the one-pass and the split-K paths: v (= acc / (s_w s_a)) + bias (+ residual),
-// ReLU, the backbones' running max; returns the stored value
-__device__ __forceinline__ f32x4 conv_out(const ConvGroupArgs& g, f32x4 v, int64_t mo, int no, int Cout) {
-  if (g.bias) {
-    const float4 b = *reinterpret_cast<const float4*>(g.bias + no);
-    v += f32x4{b.x, b.y, b.z, b.w};
-  }
+// the epilogue arithmetic shared by every conv kernel, spelled out (contraction off, the bias added by an explicit
+// fused multiply-add) so that each kernel rounds the same way whatever the compiler would contract:
+// conv_lin = acc / (s_w s_a) + bias; conv_tail = + residual, ReLU, the backbones' running max, store
+__device__ __forceinline__ f32x4 conv_lin(const ConvGroupArgs& g, const f32x4& acc, float inv, int no) {
+#pragma clang fp contract(off)
+  if (!g.bias) return acc * inv;
+  const float4 b = *reinterpret_cast<const float4*>(g.bias + no);
+  return f32x4{__builtin_fmaf(acc[0], inv, b.x), __builtin_fmaf(acc[1], inv, b.y), __builtin_fmaf(acc[2], inv, b.z),
+               __builtin_fmaf(acc[3], inv, b.w)};
+}
+__device__ __forceinline__ f32x4 conv_tail(const ConvGroupArgs& g, f32x4 v, int64_t mo, int no, int Cout) {
+#pragma clang fp contract(off)
   if (g.resid) {
     const float4 r = *reinterpret_cast<const float4*>(g.resid + mo * Cout + no);
     v += f32x4{r.x, r.y, r.z, r.w};
@@ -106,6 +112,15 @@ __device__ __forceinline__ f32x4 conv_out(const ConvGroupArgs& g, f32x4 v, int64
   *dst = make_float4(v[0], v[1], v[2], v[3]);
   return v;
 }
+// the split-K path: v = the slices' sum (each slice already scaled) + bias, then the tail
+__device__ __forceinline__ f32x4 conv_out(const ConvGroupArgs& g, f32x4 v, int64_t mo, int no, int Cout) {
+#pragma clang fp contract(off)
+  if (g.bias) {
+    const float4 b = *reinterpret_cast<const float4*>(g.bias + no);
+    v += f32x4{b.x, b.y, b.z, b.w};
+  }
+  return conv_tail(g, v, mo, no, Cout);
+}
 
 // a wave's FM x FN output fragments (rows mo[i] where mv[i], columns nb + 16 j .. + 3) through conv_out's arithmetic
 // in its order, the operands requested together before any is used (the FN bias groups, every fragment's residual)
@@ -116,14 +131,15 @@ template <int FM, int FN>
 __device__ __forceinline__ float conv_store_tile(const ConvGroupArgs& g, const f32x4 (&acc)[FM][FN], float inv,
                                                  const int64_t (&mo)[FM], const bool (&mv)[FM], int nb, int Cout,
                                                  int64_t rows) {
-  if (rows * Cout * 4 >= ((int64_t)1 << 31)) {   // past a 32-bit buffer offset: conv_out's plain loads
+#pragma clang fp contract(off)
+  if (rows * Cout * 4 >= ((int64_t)1 << 31)) {   // past a 32-bit buffer offset: conv_tail's plain loads
     float ymx = 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       if (!mv[i]) continue;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const f32x4 v = conv_out(g, acc[i][j] * inv, mo[i], nb + 16 * j, Cout);
+        const f32x4 v = conv_tail(g, conv_lin(g, acc[i][j], inv, nb + 16 * j), mo[i], nb + 16 * j, Cout);
 #pragma unroll
         for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
       }
@@ -150,7 +166,9 @@ __device__ __forceinline__ float conv_store_tile(const ConvGroupArgs& g, const f
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       f32x4 v = acc[i][j] * inv;
-      if (g.bias) v += bv[j];
+      if (g.bias)
+        v = f32x4{__builtin_fmaf(acc[i][j][0], inv, bv[j][0]), __builtin_fmaf(acc[i][j][1], inv, bv[j][1]),
+                  __builtin_fmaf(acc[i][j][2], inv, bv[j][2]), __builtin_fmaf(acc[i][j][3], inv, bv[j][3])};
       if (g.resid) v += rv[i][j];
       if (g.flags & MMT_CONV_RELU)
 #pragma unroll
@@ -165,6 +183,74 @@ __device__ __forceinline__ float conv_store_tile(const ConvGroupArgs& g, const f
       for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
     }
   }
+  return ymx;
+}
+
+// conv_store_tile through the LDS: the workgroup's 128-pixel x BN tile (8 waves: 4 row quarters x 2 column halves,
+// FM = 2) goes to `lds` (>= 128 x BN floats; 16-B chunk q of row r at q ^ (r & 7)) as conv_lin's values, then every
+// thread takes whole 16-B row chunks -- 32 lanes cover a pixel's 512 B of a 128-wide tile -- adds the residual,
+// ReLU and the merge and stores them: full 128-B lines for the output and the residual instead of a fragment's 16
+// rows x 16 B per wave instruction (the HBM-bound 1 x 1 convs of layers 1 / 2 spend most of their time here).  Same
+// arithmetic, same order as conv_store_tile, so the same bits.  Rows r valid below row_end (row0 + r = the pixel).
+template <int FN, int BN>
+__device__ __forceinline__ float conv_store_tile_staged(const ConvGroupArgs& g, const f32x4 (&acc)[2][FN], float inv,
+                                                        float* lds, int wm, int wn, int lane, int64_t row0,
+                                                        int64_t row_end, int n0, int Cout, int64_t rows) {
+#pragma clang fp contract(off)
+  constexpr int WN = BN / 2, NCH = BN / 4, PER = 128 * NCH / 512;
+  const int li = lane & 15, lk = lane >> 4, t = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every LDS-DMA of the K loop has landed
+  __syncthreads();                                   // and every wave is past its last fragment read
+  const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)Cout * 4 : 0);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int c = wn * WN + j * 16 + 4 * lk;
+    const f32x4 bv = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, (uint32_t)((n0 + c) * 4), 0, 0));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = wm * 32 + i * 16 + li;
+      f32x4 v = acc[i][j] * inv;
+      if (g.bias)
+        v = f32x4{__builtin_fmaf(acc[i][j][0], inv, bv[0]), __builtin_fmaf(acc[i][j][1], inv, bv[1]),
+                  __builtin_fmaf(acc[i][j][2], inv, bv[2]), __builtin_fmaf(acc[i][j][3], inv, bv[3])};
+      *reinterpret_cast<f32x4*>(lds + r * BN + (((c >> 2) ^ (r & 7)) << 2)) = v;
+    }
+  }
+  __syncthreads();
+  const rsrc_t rR = make_rsrc(g.resid, g.resid ? rows * Cout * 4 : 0);
+  const rsrc_t rY = make_rsrc(g.y, rows * Cout * 4);
+  const bool mx = g.flags & MMT_CONV_MAX;
+  constexpr int GRP = PER < 4 ? PER : 4;   // residual chunks requested together (registers: 4 x 4 per thread)
+  float ymx = 0.f;
+#pragma unroll
+  for (int k0 = 0; k0 < PER; k0 += GRP) {
+    f32x4 res[GRP];
+#pragma unroll
+    for (int k = 0; k < GRP; ++k) {
+      const int idx = t + 512 * (k0 + k), r = idx / NCH, q = idx - r * NCH;
+      const uint32_t off = row0 + r < row_end ? (uint32_t)(((row0 + r) * Cout + n0 + 4 * q) * 4) : kBufOob;
+      res[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rR, off, 0, 0));
+    }
+#pragma unroll
+    for (int k = 0; k < GRP; ++k) {
+      const int idx = t + 512 * (k0 + k), r = idx / NCH, q = idx - r * NCH;
+      if (row0 + r >= row_end) continue;
+      const uint32_t off = (uint32_t)(((row0 + r) * Cout + n0 + 4 * q) * 4);
+      f32x4 v = *reinterpret_cast<const f32x4*>(lds + r * BN + ((q ^ (r & 7)) << 2));
+      if (g.resid) v += res[k];
+      if (g.flags & MMT_CONV_RELU)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      if (mx) {   // torch.max(color, depth) (dimpnet.py:103): the RGB map already in y
+        const f32x4 o = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rY, off, 0, 0));
+        v = f32x4{fmaxf(o[0], v[0]), fmaxf(o[1], v[1]), fmaxf(o[2], v[2]), fmaxf(o[3], v[3])};
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rY, off, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
+    }
+  }
+  __syncthreads();   // the LDS is free again (the caller's max fold uses it)
   return ymx;
 }
 
@@ -429,7 +515,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int no = n0 + wn * WN + j * 16 + 4 * lk;
-      const f32x4 v = conv_out(g, acc[i][j] * inv, mo, no, a.Cout);
+      const f32x4 v = conv_tail(g, conv_lin(g, acc[i][j], inv, no), mo, no, a.Cout);
 #pragma unroll
       for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
     }
@@ -564,7 +650,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int no = wn * WN + j * 16 + 4 * lk;
-      const f32x4 v = conv_out(g, acc[i][j] * inv, mo, no, a.Cout);
+      const f32x4 v = conv_tail(g, conv_lin(g, acc[i][j], inv, no), mo, no, a.Cout);
 #pragma unroll
       for (int e = 0; e < 4; ++e) ymx = fmaxf(ymx, fabsf(v[e]));
     }
@@ -729,11 +815,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int no = wn * WN + j * 16 + 4 * lk;
-      f32x4 v = acc[i][j] * inv;
-      if (g.bias) {
-        const float4 b = *reinterpret_cast<const float4*>(g.bias + no);
-        v += f32x4{b.x, b.y, b.z, b.w};
-      }
+      f32x4 v = conv_lin(g, acc[i][j], inv, no);   // (the stem kernel's arithmetic: bit-identical to stem + pool)
       if (g.flags & MMT_CONV_RELU)
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -800,8 +882,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
   constexpr int WAIT_W = 2 * NA + NW;          // ... when W(j + 1) is (A(j + NR - 1), W(j + 2), A(j + NR))
   constexpr int WAIT_AE = (NR - 2) * (NW + NA); // OVL: ... when A(j + 1) is, before step j's loads
   static_assert(NR == 2 || NR == 3, "register sets");
-  __shared__ __attribute__((aligned(16))) uint16_t sA[2][2][BM * BK];
-  __shared__ __attribute__((aligned(16))) uint16_t sW[NWS][2][BN * BK];
+  // one LDS array (the operand rings, then the epilogue's staged tile: 128 x BN floats <= its size)
+  __shared__ __attribute__((aligned(16))) uint16_t smem_dk[2 * 2 * BM * BK + NWS * 2 * BN * BK];
+  auto& sA = *reinterpret_cast<uint16_t(*)[2][2][BM * BK]>(smem_dk);
+  auto& sW = *reinterpret_cast<uint16_t(*)[NWS][2][BN * BK]>(smem_dk + 2 * 2 * BM * BK);
+  static_assert(BM != 128 || 128 * BN * 4 <= (int)sizeof(smem_dk), "staged epilogue tile");
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int grp = blockIdx.z / a.ks, slice = blockIdx.z - grp * a.ks;
@@ -1148,6 +1233,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
     }
     return;
   }
+  float ymx;
+  if constexpr (BM == 128) {
+    if (a.staged_epi && (int64_t)M * a.Cout * 4 < ((int64_t)1 << 31)) {
+      ymx = conv_store_tile_staged<FN, BN>(g, acc, inv, reinterpret_cast<float*>(smem_dk), wm, wn, lane, m0, M, n0,
+                                           a.Cout, M);
+      if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.y * 7 + blockIdx.z * 13, reinterpret_cast<float*>(smem_dk));
+      return;
+    }
+  }
   int64_t mo[FM];
   bool mv[FM];
 #pragma unroll
@@ -1155,7 +1249,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BM == 128 ?
     mo[i] = m0 + wm * (BM / 4) + i * 16 + li;
     mv[i] = mo[i] < M;
   }
-  const float ymx = conv_store_tile<FM, FN>(g, acc, inv, mo, mv, n0 + wn * WN + 4 * lk, a.Cout, M);
+  ymx = conv_store_tile<FM, FN>(g, acc, inv, mo, mv, n0 + wn * WN + 4 * lk, a.Cout, M);
   if (g.ymax) fold_max<8>(g.ymax, ymx, blockIdx.x + blockIdx.y * 7 + blockIdx.z * 13, reinterpret_cast<float*>(&sA[0][0][0]));
 }
 
@@ -1371,6 +1465,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     }
     return;
   }
+  // (fragment-shaped stores: the LDS-staged epilogue of the deep kernel pushed this kernel past 128 VGPRs into
+  // scratch; the 3 x 3 layers are MFMA-bound, not store-bound)
   int64_t mo[FM];
   bool mv[FM];
 #pragma unroll
@@ -1584,6 +1680,9 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   const dim3 dgrid(gm * (Cout / bn), 1, G * ks);   // the deep kernel: M x N tiles flattened
   static const int xcd_env = getenv("MMT_CONV_XCD") ? atoi(getenv("MMT_CONV_XCD")) : -1;   // tuning: 0 / 1 force
   a.xcd_order = xcd_env != 0;
+  // the LDS-staged conv epilogue (opt-in until measured: MMT_CONV_STAGED=1)
+  static const bool staged_env = getenv("MMT_CONV_STAGED") && atoi(getenv("MMT_CONV_STAGED")) != 0;
+  a.staged_epi = staged_env ? 1 : 0;
   // the stem on a 4-channel image: 2-D tiles from an LDS input patch (MMT_CONV_STEM_OLD: the gather kernel, tuning)
   static const bool stem_old = getenv("MMT_CONV_STEM_OLD") != nullptr;
   static const int stem_th = getenv("MMT_CONV_STEM_TH") ? atoi(getenv("MMT_CONV_STEM_TH")) : 16;   // tuning: 8
@@ -1699,6 +1798,9 @@ int mmt_conv2d_f16x3_ds_groups(const mmt_conv_group* groups, const mmt_conv_ds* 
   a.part = static_cast<float*>(ws);
   static const int xcd_env = getenv("MMT_CONV_XCD") ? atoi(getenv("MMT_CONV_XCD")) : -1;
   a.xcd_order = xcd_env != 0;
+  // the LDS-staged conv epilogue (opt-in until measured: MMT_CONV_STAGED=1)
+  static const bool staged_env = getenv("MMT_CONV_STAGED") && atoi(getenv("MMT_CONV_STAGED")) != 0;
+  a.staged_epi = staged_env ? 1 : 0;
   const int bn = conv_bn((M + 127) / 128, Kp, Cout, G);
   const dim3 dgrid((unsigned)((M + 127) / 128 * (Cout / bn)), 1, G * ks);
   const hipStream_t s = (hipStream_t)stream;
