@@ -1680,8 +1680,9 @@ int mmt_conv2d_f16x3_groups(const mmt_conv_group* groups, int G, int N, int H, i
   const dim3 dgrid(gm * (Cout / bn), 1, G * ks);   // the deep kernel: M x N tiles flattened
   static const int xcd_env = getenv("MMT_CONV_XCD") ? atoi(getenv("MMT_CONV_XCD")) : -1;   // tuning: 0 / 1 force
   a.xcd_order = xcd_env != 0;
-  // the LDS-staged conv epilogue (opt-in until measured: MMT_CONV_STAGED=1)
-  static const bool staged_env = getenv("MMT_CONV_STAGED") && atoi(getenv("MMT_CONV_STAGED")) != 0;
+  // the LDS-staged conv epilogue (mfDiMP 7 396 -> 7 531 frames/s, profiles/r05_ab_conv_staged_epilogue.txt;
+  // MMT_CONV_STAGED=0, tuning: fragment-shaped stores)
+  static const bool staged_env = !getenv("MMT_CONV_STAGED") || atoi(getenv("MMT_CONV_STAGED")) != 0;
   a.staged_epi = staged_env ? 1 : 0;
   // the stem on a 4-channel image: 2-D tiles from an LDS input patch (MMT_CONV_STEM_OLD: the gather kernel, tuning)
   static const bool stem_old = getenv("MMT_CONV_STEM_OLD") != nullptr;
@@ -1798,8 +1799,9 @@ int mmt_conv2d_f16x3_ds_groups(const mmt_conv_group* groups, const mmt_conv_ds* 
   a.part = static_cast<float*>(ws);
   static const int xcd_env = getenv("MMT_CONV_XCD") ? atoi(getenv("MMT_CONV_XCD")) : -1;
   a.xcd_order = xcd_env != 0;
-  // the LDS-staged conv epilogue (opt-in until measured: MMT_CONV_STAGED=1)
-  static const bool staged_env = getenv("MMT_CONV_STAGED") && atoi(getenv("MMT_CONV_STAGED")) != 0;
+  // the LDS-staged conv epilogue (mfDiMP 7 396 -> 7 531 frames/s, profiles/r05_ab_conv_staged_epilogue.txt;
+  // MMT_CONV_STAGED=0, tuning: fragment-shaped stores)
+  static const bool staged_env = !getenv("MMT_CONV_STAGED") || atoi(getenv("MMT_CONV_STAGED")) != 0;
   a.staged_epi = staged_env ? 1 : 0;
   const int bn = conv_bn((M + 127) / 128, Kp, Cout, G);
   const dim3 dgrid((unsigned)((M + 127) / 128 * (Cout / bn)), 1, G * ks);
