@@ -4,7 +4,7 @@ set -e
 OUT=${OUT:-gpurun_out/pmc_bench}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-ARGS=${ARGS:---steps 5 --warmup 2 --no-cpu-baseline --probe none --host-frames 0}
+ARGS=${ARGS:---steps 5 --warmup 2 --no-cpu-baseline --no-extras --probe none --host-frames 0}
 # the timing probe's launch shapes: two-stream halves off (pmc_traffic.py assigns classes by layer order)
 export MMT_OVERLAP_MIN=0
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -- python bench.py $ARGS > $OUT/fetch.log 2>&1
