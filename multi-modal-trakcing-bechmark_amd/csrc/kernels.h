@@ -150,6 +150,9 @@ struct LnPromptArgs {
 // the fovea statistics of the row's sequence, s8 of its slot, the prompt residual (conv1x1 of s8, formed per
 // row from an LDS copy of conv1x1) and LN1, for the compact rows
 void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s);
+// a deep layer's prompt_reduce (pa) and prompt_expand_ln (la, mode 2) as one launch whose blocks meet at a
+// per-sequence barrier (bar: [B][32] ints, zero at allocation, left zero); false: not taken (the caller launches the two)
+bool prompt_ln_fused(const PromptArgs& pa, const LnPromptArgs& la, int* bar, hipStream_t s);
 
 // ---------------------------------------------------------------- candidate elimination
 struct CEArgs {

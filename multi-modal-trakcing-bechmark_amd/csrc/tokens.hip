@@ -184,7 +184,7 @@ __device__ __forceinline__ void fovea_stats(const FoveaStage& fs, int Lz, int Lx
   __syncthreads();
   const float cm = st[part * 16 + c];
   float sum = 0.f;
-  for (int k = stripe; k < n; k += 32) sum += __expf(va[(lo + k) * 8 + c] * sm - cm);
+  for (int k = stripe; k < n; k += 32) sum += __expf(__builtin_fmaf(va[(lo + k) * 8 + c], sm, -cm));
   sum += dpp<DPP_ROR8>(sum);
   sum = xsum16(sum, sum);
   sum = xsum32(sum, sum);
@@ -195,8 +195,9 @@ __device__ __forceinline__ void fovea_stats(const FoveaStage& fs, int Lz, int Lx
   __syncthreads();
 }
 // s8[c] of one slot (lane c < 8 of the caller): fovea mask * a8 + c8 (the former fovea kernel's expression)
+// (the arithmetic spelled out, as ln_row: the deep prompt, LN1 and fused prompt + LN1 kernels form the same bits)
 __device__ __forceinline__ float fovea_s8(float a, float cc, const float* st, int part, int c, float sm) {
-  return (__expf(a * sm - st[part * 16 + c]) / st[part * 16 + 8 + c]) * a + cc;
+  return __builtin_fmaf(__expf(__builtin_fmaf(a, sm, -st[part * 16 + c])) / st[part * 16 + 8 + c], a, cc);
 }
 
 // ------------------------------------------------------------------ LayerNorm (optionally fused CE gather)
@@ -327,6 +328,50 @@ __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) 
 constexpr int TOK_THREADS = 512;   // 8 waves per block share one LDS copy of the weights
 constexpr int TOK_ROWS = TOK_THREADS / 64;
 
+// One slot of a deep prompt block (the wave's x row, already current; live = the slot has a row): returns, valid in
+// lanes 0-7, a8 = conv0_0(LN_A(x)) + b00 (LN_A's affine folded into W0 / b00 by pack_weights) and c8 from the previous
+// prompt's s8 (ap, cp: the previous a8 / c8 of the slot, stp: their fovea statistics) through the folded LN_B + conv0_1.
+// The arithmetic is spelled out (contraction off): the deep prompt kernel and the fused prompt + LN1 kernel inline it.
+__device__ __forceinline__ float2 deep_slot(const Row12& x, bool live, int part_id, float ap, float cp, const float* stp,
+                                            const float* fold, const float* W0, float ba, float smooth_p, int lane) {
+#pragma clang fp contract(off)
+  const int kk = lane & 7;
+  // s8_prev of the slot in lanes 0-7, then the lane's pair of it for the LN_B variance form
+  const float s8v = lane < 8 ? fovea_s8(ap, cp, stp, part_id, lane, smooth_p) : 0.f;
+  const float sp = __shfl(s8v, kk, 64), sq = __shfl(s8v, lane >> 3, 64);
+  // the lane's coefficients of the LN_B variance form: G[q][p] s_p s_q (+ 2 g_q s_q for p = 0, + gb in lane 0)
+  const float vG = fold[FOLD_G + lane], vg = kk == 0 ? 2.f * fold[FOLD_g + (lane >> 3)] : 0.f;
+  const float vb = lane == 0 ? fold[FOLD_gb] : 0.f;
+  float ra = 0.f;   // a pruned slot is a zero row: its LN is 0 and a8 = b00 exactly
+  if (live) {       // wave-uniform
+    const Row12 y = ln_hat(x);
+    float part[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const float4 w = reinterpret_cast<const float4*>(W0 + k * C768)[lane + 64 * i];
+        t = __builtin_fmaf(y.v[i].x, w.x, t);
+        t = __builtin_fmaf(y.v[i].y, w.y, t);
+        t = __builtin_fmaf(y.v[i].z, w.z, t);
+        t = __builtin_fmaf(y.v[i].w, w.w, t);
+      }
+      part[k] = t;
+    }
+    ra = reduce8(part, lane);
+  }
+  // c8 from the previous prompt's s8: var = s^T G s + 2 g.s + gb, one (q, p) term per lane
+  const float var = wave_sum(__builtin_fmaf(__builtin_fmaf(vG, sp, vg), sq, vb));
+  const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + LN_EPS);
+  // lane kk < 8: mk = mc[kk] + MC[kk][:] . s   (s[q] is lane 8q's sq)
+  float mk = fold[FOLD_mc + kk];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    mk = __builtin_fmaf(fold[FOLD_MC + kk * 8 + q], u2f(__builtin_amdgcn_readlane(f2u(sq), 8 * q)), mk);
+  return make_float2(ra + ba, __builtin_fmaf(rstd, mk, fold[FOLD_cb + kk]));
+}
+
 // R: slots per wave (the block's weight fill and fovea statistics shared by R x 8 slots; 2 at large batches)
 template <bool RR, int R>
 __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const PromptArgs a) {
@@ -382,41 +427,11 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
     x = apply_reduce(x, a.rr, xrow, lane);
     store_f32(const_cast<float*>(a.srcA) + xrow * C768, x, lane);
   }
-  const int kk = lane & 7;
-  // s8_prev of the slot in lanes 0-7, then the lane's pair of it for the LN_B variance form
-  const float s8v = lane < 8 ? fovea_s8(ap, cp, st, s < a.Lz ? 0 : 1, lane, a.smooth_p) : 0.f;
-  const float sp = __shfl(s8v, kk, 64), sq = __shfl(s8v, lane >> 3, 64);
-  // the lane's coefficients of the LN_B variance form: G[q][p] s_p s_q (+ 2 g_q s_q for p = 0, + gb in lane 0)
-  const float vG = fold[FOLD_G + lane], vg = kk == 0 ? 2.f * fold[FOLD_g + (lane >> 3)] : 0.f;
-  const float vb = lane == 0 ? fold[FOLD_gb] : 0.f;
-  float ra = 0.f;   // a pruned slot is a zero row: its LN is 0 and a8 = b00 exactly
-  if (pos >= 0) {   // wave-uniform
-    const Row12 y = ln_hat(x);   // LN_A's affine is folded into w00 / b00 (engine pack_weights)
-    float part[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const float4 w = reinterpret_cast<const float4*>(W0 + k * C768)[lane + 64 * i];
-        t += y.v[i].x * w.x + y.v[i].y * w.y + y.v[i].z * w.z + y.v[i].w * w.w;
-      }
-      part[k] = t;
-    }
-    ra = reduce8(part, lane);
-  }
-  // c8 from the previous prompt's s8: var = s^T G s + 2 g.s + gb, one (q, p) term per lane
-  const float var = wave_sum(fmaf(fmaf(vG, sp, vg), sq, vb));
-  const float rstd = 1.0f / sqrtf(fmaxf(var, 0.f) + LN_EPS);
-  // lane kk < 8: mk = mc[kk] + MC[kk][:] . s   (s[q] is lane 8q's sq)
-  float mk = fold[FOLD_mc + kk];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) mk += fold[FOLD_MC + kk * 8 + q] * u2f(__builtin_amdgcn_readlane(f2u(sq), 8 * q));
-  const float rb = rstd * mk + fold[FOLD_cb + kk];
+  const float2 ac = deep_slot(x, pos >= 0, s < a.Lz ? 0 : 1, ap, cp, st, fold, W0, ba, a.smooth_p, lane);
   if (lane < 8) {
     const int64_t row = (int64_t)b * L + s;
-    a.a8[row * 8 + lane] = ra + ba;
-    a.c8[row * 8 + lane] = rb;
+    a.a8[row * 8 + lane] = ac.x;
+    a.c8[row * 8 + lane] = ac.y;
   }
   }
 }
@@ -461,6 +476,53 @@ void prompt_reduce(const PromptArgs& a, hipStream_t s) {
 //                    (candidate_elimination_prompt + x_ori add, attn_blocks.py:9-18, vit_ce_prompt.py:310)
 // then out = LN(X[r]) (norm1 of the block).  One block = 8 compact rows of one sequence, one per wave; the
 // slot, rows and weights are all requested before the statistics and barriers.
+//
+// One compact row r (the wave's; xv its X row -- mode 1: tok_rgb -- q its position row in mode 1, av / cv the slot's
+// a8 / c8 in lanes 0-7, st the sequence's fovea statistics, W1t / cst the block's LDS copies): the arithmetic
+// spelled out (contraction off), as the fused prompt + LN1 kernel inlines it too
+template <int MODE>
+__device__ __forceinline__ void ln_prompt_row(const Row12& xv, const Row12& q, float av, float cv, int part_id,
+                                              const float* st, const float* W1t, const float* cst,
+                                              const LnPromptArgs& a, int64_t r, int lane) {
+#pragma clang fp contract(off)
+  const float s8v = lane < 8 ? fovea_s8(av, cv, st, part_id, lane, a.smooth) : 0.f;
+  float f[8];
+#pragma unroll
+  for (int ch = 0; ch < 8; ++ch) f[ch] = u2f(__builtin_amdgcn_readlane(f2u(s8v), ch));
+  Row12 x;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 b1 = reinterpret_cast<const float4*>(cst)[lane + 64 * i];
+    float pv[4] = {b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) {
+      const float4 wv = reinterpret_cast<const float4*>(W1t + ch * C768)[lane + 64 * i];
+      pv[0] = __builtin_fmaf(wv.x, f[ch], pv[0]);
+      pv[1] = __builtin_fmaf(wv.y, f[ch], pv[1]);
+      pv[2] = __builtin_fmaf(wv.z, f[ch], pv[2]);
+      pv[3] = __builtin_fmaf(wv.w, f[ch], pv[3]);
+    }
+    const float4 xx = xv.v[i];
+    if (MODE == 1) {
+      const float4 ps = q.v[i];
+      x.v[i] = make_float4((xx.x + pv[0]) + ps.x, (xx.y + pv[1]) + ps.y, (xx.z + pv[2]) + ps.z, (xx.w + pv[3]) + ps.w);
+    } else {
+      x.v[i] = make_float4(xx.x + pv[0], xx.y + pv[1], xx.z + pv[2], xx.w + pv[3]);
+    }
+  }
+  store_f32(a.X + r * C768, x, lane);
+  Row12 y = ln_hat(x);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 gw = reinterpret_cast<const float4*>(cst + C768)[lane + 64 * i];
+    const float4 gb = reinterpret_cast<const float4*>(cst + 2 * C768)[lane + 64 * i];
+    y.v[i] = make_float4(__builtin_fmaf(y.v[i].x, gw.x, gb.x), __builtin_fmaf(y.v[i].y, gw.y, gb.y),
+                         __builtin_fmaf(y.v[i].z, gw.z, gb.z), __builtin_fmaf(y.v[i].w, gw.w, gb.w));
+  }
+  if (a.out_lo) store_split(a.out + r * C768, a.out_lo + r * C768, y, a.out_scale, lane);
+  else store_bf16(a.out + r * C768, y, lane);
+}
+
 template <int MODE, int R>
 // LNP_WPE (build-time tuning): waves per SIMD the register allocation targets; 6 (80 VGPRs, three blocks per CU)
 // spills 5 VGPRs in mode 2 and measured -0.35 % at 32 sequences against the default (tests/r3_run23.sh)
@@ -519,45 +581,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
 #pragma unroll
   for (int rr = 0; rr < R; ++rr) {
   if (tv[rr] >= a.rows_per_seq) break;   // wave-uniform; later rows of the wave lie further out
-  const int slot = slotv[rr];
-  const int64_t r = rv[rr];
-  const Row12 xv = xvv[rr], q = qv[rr];
-  const float av = avv[rr], cv = cvv[rr];
-  const float s8v = lane < 8 ? fovea_s8(av, cv, st, slot < a.Lz ? 0 : 1, lane, a.smooth) : 0.f;
-  float f[8];
-#pragma unroll
-  for (int ch = 0; ch < 8; ++ch) f[ch] = u2f(__builtin_amdgcn_readlane(f2u(s8v), ch));
-  Row12 x;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const float4 b1 = reinterpret_cast<const float4*>(cst)[lane + 64 * i];
-    float pv[4] = {b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-    for (int ch = 0; ch < 8; ++ch) {
-      const float4 wv = reinterpret_cast<const float4*>(W1t + ch * C768)[lane + 64 * i];
-      pv[0] += wv.x * f[ch];
-      pv[1] += wv.y * f[ch];
-      pv[2] += wv.z * f[ch];
-      pv[3] += wv.w * f[ch];
-    }
-    const float4 xx = xv.v[i];
-    if (MODE == 1) {
-      const float4 ps = q.v[i];
-      x.v[i] = make_float4((xx.x + pv[0]) + ps.x, (xx.y + pv[1]) + ps.y, (xx.z + pv[2]) + ps.z, (xx.w + pv[3]) + ps.w);
-    } else {
-      x.v[i] = make_float4(xx.x + pv[0], xx.y + pv[1], xx.z + pv[2], xx.w + pv[3]);
-    }
-  }
-  store_f32(a.X + r * C768, x, lane);
-  Row12 y = ln_hat(x);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const float4 gw = reinterpret_cast<const float4*>(cst + C768)[lane + 64 * i];
-    const float4 gb = reinterpret_cast<const float4*>(cst + 2 * C768)[lane + 64 * i];
-    y.v[i] = make_float4(y.v[i].x * gw.x + gb.x, y.v[i].y * gw.y + gb.y, y.v[i].z * gw.z + gb.z, y.v[i].w * gw.w + gb.w);
-  }
-  if (a.out_lo) store_split(a.out + r * C768, a.out_lo + r * C768, y, a.out_scale, lane);
-  else store_bf16(a.out + r * C768, y, lane);
+  ln_prompt_row<MODE>(xvv[rr], qv[rr], avv[rr], cvv[rr], slotv[rr] < a.Lz ? 0 : 1, st, W1t, cst, a, rv[rr], lane);
   }
 }
 
@@ -575,6 +599,167 @@ void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((ln_prompt_kernel<2, 2>), grid, dim3(TOK_THREADS), va_bytes, s, a);
   else
     hipLaunchKernelGGL((ln_prompt_kernel<2, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
+}
+
+// ------------------------------------------------------------------ deep prompt block + LN1, one launch
+// A deep layer's prompt reduce (prompt_reduce_deep_kernel) and LN1 with the prompt residual (ln_prompt_kernel,
+// mode 2) are one row kernel but for the fovea statistics between them: LN1 of any row needs the softmax statistics
+// of this layer's a8 over all slots of its sequence.  Here the blocks of a sequence meet at a barrier between the
+// two halves instead of a launch boundary, and each wave keeps its slot's residual row in registers across it: the
+// slot's compact row (slot2pos and gidx are inverse maps) is the row LN1 finishes, so X is read once and written
+// once (unfused: read twice, written twice when a split-K update is pending).  The arithmetic is deep_slot +
+// ln_prompt_row, as the two kernels inline it: the same bits.
+//
+// The barrier (seq_barrier): an arrival counter and a generation word per sequence, the last arrival resetting
+// the counter and advancing the generation (agent-scope release / acquire: the a8 / c8 stores of every block are
+// visible to every other after it, whichever XCD wrote them).  It needs every block of an unfinished sequence to
+// be resident or dispatchable: blocks are dispatched in order and a sequence has at most 128 blocks of 8 waves,
+// ~45 KB of LDS, so the lowest unfinished sequence's blocks always fit beside the (finishing) ones before it.  The
+// spin is bounded: a broken invariant ends the kernel with a flag (bar[8] of the sequence) instead of a hang.
+constexpr int kBarSpin = 1 << 22;
+constexpr int kBarStride = 32;   // ints per sequence: counter [0], timeout flag [8], generation [16]
+__device__ __forceinline__ void seq_barrier(int* w, int nblocks) {
+  const int g = __hip_atomic_load(w + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int old = __hip_atomic_fetch_add(w, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == nblocks - 1) {
+    __hip_atomic_store(w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w + 16, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the last arrival reads the others' rows too
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+  for (int k = 0; __hip_atomic_load(w + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g; ++k) {
+    if (k >= kBarSpin) {
+      __hip_atomic_store(w + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate done before the block's barrier releases
+}
+
+template <bool RR, int R>
+__global__ __launch_bounds__(TOK_THREADS) void prompt_ln_kernel(const PromptArgs a, const LnPromptArgs la, int* bar) {
+  __shared__ float fold[FOLD_N];
+  __shared__ __attribute__((aligned(16))) float W[8 * C768];     // conv0_0 (LN_A folded)
+  __shared__ __attribute__((aligned(16))) float W1t[8 * C768];   // conv1x1 (its own copy: held in registers across
+                                                                 // the barrier, the fill went to scratch)
+  __shared__ __attribute__((aligned(16))) float cst[3 * C768];   // conv1x1 bias, norm1 weight, norm1 bias
+  extern __shared__ __attribute__((aligned(16))) float va[];    // [L][8]
+  __shared__ float red[64], st[32];
+  const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, b = blockIdx.y;
+  // ---- every global load of the first half, then the second half's weights
+  const bool pre = a.fstat_p != nullptr;
+  FoveaStage fsg;
+  if (!pre) fsg = fovea_stage(a.a8p + (int64_t)b * L * 8, L);
+  const float stv = pre && threadIdx.x < 32 ? a.fstat_p[b * 32 + threadIdx.x] : 0.f;
+  int sv[R], posv[R];
+  int64_t xrowv[R];
+  Row12 xv[R];
+  float apv[R], cpv[R];
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+    const int s = (blockIdx.x * R + rr) * TOK_ROWS + (threadIdx.x >> 6);
+    const int pos = s >= L ? -1 : s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];   // wave-uniform
+    sv[rr] = s;
+    posv[rr] = pos;
+    xrowv[rr] = (int64_t)b * a.srcA_rows + max(pos, 0);
+    xv[rr] = load_row(a.srcA + xrowv[rr] * C768, lane);
+    const int64_t srow = ((int64_t)b * L + min(s, L - 1)) * 8;
+    apv[rr] = lane < 8 ? a.a8p[srow + lane] : 0.f;
+    cpv[rr] = lane < 8 ? a.c8p[srow + lane] : 0.f;
+  }
+  constexpr int WV = 8 * C768 / 4 / TOK_THREADS;
+  float4 wst[WV], w1v[WV];   // (w1v: stored to W1t with the first half's fills)
+#pragma unroll
+  for (int k = 0; k < WV; ++k) wst[k] = reinterpret_cast<const float4*>(a.w00)[threadIdx.x + TOK_THREADS * k];
+  const float fo = threadIdx.x < FOLD_N ? a.fold[threadIdx.x] : 0.f;
+  const float ba = lane < 8 ? a.b00[lane] : 0.f;
+#pragma unroll
+  for (int k = 0; k < WV; ++k) w1v[k] = reinterpret_cast<const float4*>(la.w1)[threadIdx.x + TOK_THREADS * k];
+  float cs[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int e = threadIdx.x + TOK_THREADS * k;
+    cs[k] = e < C768 ? la.b1[e] : e < 2 * C768 ? la.w[e - C768] : e < 3 * C768 ? la.b[e - 2 * C768] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W)[threadIdx.x + TOK_THREADS * k] = wst[k];
+#pragma unroll
+  for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W1t)[threadIdx.x + TOK_THREADS * k] = w1v[k];
+  if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int e = threadIdx.x + TOK_THREADS * k;
+    if (e < 3 * C768) cst[e] = cs[k];
+  }
+  if (pre) {
+    if (threadIdx.x < 32) st[threadIdx.x] = stv;
+    __syncthreads();
+  } else {
+    fovea_stats(fsg, a.Lz, a.Lx, a.smooth_p, va, red, st);   // ends with a barrier
+  }
+  // ---- first half: a8 / c8 of the wave's slots (prompt_reduce_deep_kernel)
+  float avv[R] = {}, cvv[R] = {};
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+    const int s = sv[rr], pos = posv[rr];
+    if (s >= L) break;   // wave-uniform
+    if (RR && pos >= 0 && a.rr.ws) xv[rr] = apply_reduce(xv[rr], a.rr, xrowv[rr], lane);   // kept, not stored
+    const float2 ac = deep_slot(xv[rr], pos >= 0, s < a.Lz ? 0 : 1, apv[rr], cpv[rr], st, fold, W, ba, a.smooth_p,
+                                lane);
+    avv[rr] = ac.x;
+    cvv[rr] = ac.y;
+    if (lane < 8) {
+      const int64_t row = (int64_t)b * L + s;
+      a.a8[row * 8 + lane] = ac.x;
+      a.c8[row * 8 + lane] = ac.y;
+    }
+  }
+  // ---- the sequence's blocks meet.  Every wave waits for its a8 / c8 stores to land in this XCD's L2 (the
+  // workgroup barrier alone does not wait for stores on gfx950), then thread 0's agent-scope release writes the L2
+  // back once for the block and its acquire after the wait invalidates this CU's and XCD's stale lines once (a
+  // __threadfence in every wave, 8 write-backs and invalidates per block, cost 10 us per launch, r5_run18.sh)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) seq_barrier(bar + (int64_t)b * kBarStride, gridDim.x);
+  __syncthreads();
+  // ---- second half: this layer's fovea statistics, LN1 of the wave's compact rows (ln_prompt_kernel, mode 2)
+  const FoveaStage fsg2 = fovea_stage(la.a8 + (int64_t)b * L * 8, L);
+  fovea_stats(fsg2, a.Lz, a.Lx, la.smooth, va, red, st);   // ends with a barrier
+  if (la.fstat && blockIdx.x == 0 && threadIdx.x < 32) la.fstat[b * 32 + threadIdx.x] = st[threadIdx.x];
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+    if (sv[rr] >= L) break;
+    if (posv[rr] < 0) continue;   // a pruned slot has no row
+    ln_prompt_row<2>(xv[rr], xv[rr], avv[rr], cvv[rr], sv[rr] < a.Lz ? 0 : 1, st, W1t, cst, la,
+                     (int64_t)b * la.rows_per_seq + posv[rr], lane);
+  }
+}
+
+bool prompt_ln_fused(const PromptArgs& pa, const LnPromptArgs& la, int* bar, hipStream_t s) {
+  // MMT_PROMPT_FUSED (opt-in): the largest batch that takes the fused launch (default 0, never; read per call, so a
+  // test can compare the two paths in one process).  Measured slower: at one sequence 15.4 us per launch against
+  // 6.7 + 6.3 us for the two kernels (1 084 against 1 118 frames/s), at 32 sequences 6 267 against 6 444 -- the
+  // barrier's chain (L2 write-back, device atomic, polling past the L2, invalidate, a8 re-read) is ~4 us, more
+  // than the launch boundary it replaces (profiles/r05_ab_prompt_ln_fused.txt)
+  const char* env = getenv("MMT_PROMPT_FUSED");
+  const int maxb = env ? atoi(env) : 0;
+  const int L = pa.Lz + pa.Lx;
+  if (!bar || pa.layer == 0 || la.mode != 2 || pa.B > maxb || L > FOVEA_MAX_TOKENS || la.a8 != pa.a8 ||
+      la.c8 != pa.c8 || la.X != pa.srcA || la.rows_per_seq != pa.srcA_rows)
+    return false;
+  const int R = pa.rr.ws ? 1 : tok_rows_per_wave(pa.B);
+  const dim3 grid((L + TOK_ROWS * R - 1) / (TOK_ROWS * R), pa.B);
+  const size_t va_bytes = (size_t)L * 8 * sizeof(float);
+  if (pa.rr.ws)
+    hipLaunchKernelGGL((prompt_ln_kernel<true, 1>), grid, dim3(TOK_THREADS), va_bytes, s, pa, la, bar);
+  else if (R == 2)
+    hipLaunchKernelGGL((prompt_ln_kernel<false, 2>), grid, dim3(TOK_THREADS), va_bytes, s, pa, la, bar);
+  else
+    hipLaunchKernelGGL((prompt_ln_kernel<false, 1>), grid, dim3(TOK_THREADS), va_bytes, s, pa, la, bar);
+  return true;
 }
 
 // ------------------------------------------------------------------ candidate elimination
