@@ -155,10 +155,12 @@ def test_dimp_decisions_match_reference(nets, name):
 @pytest.mark.parametrize("precision", ["f16x3", "fp32"])
 def test_dimp_branches_match_reference(nets, precision, name):
     """End to end (patch sampling, both backbones, classifier, state machine, filter updates on the device) on
-    the branch sequences: the reference's flag, box and confidence on every frame up to the first frame whose
-    reference decision was within MIN_MARGIN of a threshold or whose score map had a second peak within
-    MAX_RUNNER_UP of its maximum (near-ties that fp32 summation order decides; the decision test above covers
-    those frames on the reference's own maps); when no such frame occurs, also the filter after the first
+    the branch sequences: the reference's flag, box and confidence on every frame.  A frame whose reference decision
+    was within MIN_MARGIN of a threshold or whose score map had a second peak within MAX_RUNNER_UP of its maximum is
+    a near-tie that fp32 summation order decides: there the run continues only if the device made the reference's
+    decision too (flag, box, confidence), else it stops (the decision test above covers those frames on the
+    reference's own maps).  So the distractor sequences are asserted past their first near-tie whenever the device
+    decides it as the reference did.  When the sequence has no near-tie, also the filter after the first
     hard-negative update and at the end, and the sample memory bookkeeping."""
     from mmtrack_amd import _lib, synth
     from mmtrack_amd.dimp_tracker import DiMP
@@ -168,24 +170,37 @@ def test_dimp_branches_match_reference(nets, precision, name):
     margin, runner = gd[p + "margin"], gd[p + "runner_up"]
     n = len(flags)
     thin = [t for t in range(1, n) if margin[t] < MIN_MARGIN or runner[t] > MAX_RUNNER_UP]
-    last = thin[0] if thin else n   # frames [1, last) are asserted
-    frames, _ = synth.make_frames(seed, last, H, W, C, box=tuple(gd["init_box"]), **json.loads(str(gd[p + "events"])))
+    frames, _ = synth.make_frames(seed, n, H, W, C, box=tuple(gd["init_box"]), **json.loads(str(gd[p + "events"])))
     tr = DiMP(_params(gd, p), net=nets[precision])
     torch.manual_seed(tseed)
     tr.initialize(frames[0], {"init_bbox": list(gd["init_box"])})
     hn_frame = int(gd[p + "hn_frame"]) if p + "hn_frame" in gd.files else -1
-    bar = confidence_bar(name, last)
-    dconf = []
-    for t in range(1, last):
+    # the bar: 2 x the reference's fp32-order spread over the frames before the first near-tie (dimp_tolerance.py);
+    # past it, the spread over the whole sequence (its variants may take the other side of a tie: at most the 1 % cap)
+    bar0 = bar = confidence_bar(name, thin[0] if thin else n)
+    dconf, passed, stop = [], [], None
+    for t in range(1, n):
+        if thin and t == thin[0]:
+            bar = max(bar0, confidence_bar(name, n))
         out = tr.track(frames[t])
-        dconf.append(_check_frame(name, t, out, tr.debug_info["flag"], boxes[t], (conf[t], str(flags[t])), bar))
+        if t in thin:
+            try:
+                dconf.append(_check_frame(name, t, out, tr.debug_info["flag"], boxes[t], (conf[t], str(flags[t])),
+                                          bar))
+                passed.append(t)
+            except AssertionError as err:   # decided the other way: the states part here
+                stop = (t, str(err))
+                break
+        else:
+            dconf.append(_check_frame(name, t, out, tr.debug_info["flag"], boxes[t], (conf[t], str(flags[t])), bar))
         if t == hn_frame:
             close(tr.target_filter.cpu(), gd[p + "hn_filter"], 1e-2)
+    last = stop[0] if stop else n   # frames [1, last) asserted
     asserted = dict(zip(*np.unique(flags[1:last], return_counts=True)))
-    print(f"{name} [{precision}]: frames 1..{last - 1} asserted {asserted}, max confidence rel. diff "
-          f"{max(dconf):.2e} (bar {bar:.2e}: 2 x the reference's fp32-order spread {reference_spread(name, last)}), "
-          f"smallest reference margin there {np.nanmin(margin[1:last]):.4f}"
-          + (f"; stopped before frame {last} (margin {margin[last]:.4f}, runner-up {runner[last]:.4f})" if thin else ""))
+    print(f"{name} [{precision}]: frames 1..{last - 1} asserted {asserted} ({len(passed)} near-ties decided as the "
+          f"reference did), max confidence rel. diff {max(dconf):.2e} (bar {bar0:.2e}, {bar:.2e} past a near-tie)"
+          + (f"; stopped at near-tie frame {stop[0]} (margin {margin[stop[0]]:.4f}, runner-up {runner[stop[0]]:.4f}):"
+             f" {stop[1][:120]}" if stop else ""))
     if thin:
         return
     close(tr.target_filter.cpu(), gd[p + "final_filter"], 1e-2)
