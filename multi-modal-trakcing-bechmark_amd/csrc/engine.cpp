@@ -85,6 +85,7 @@ struct mmt_engine {
   hipStream_t xstream[kMaxParts - 1] = {};   // parts 1.. of a split launch (part 0 runs on `stream`)
   hipEvent_t fork_ev = nullptr, join_ev[kMaxParts - 1] = {};
   int nparts = 2;                      // parts of a split launch (MMT_NPARTS, 2..4)
+  int conc_parts = 1;                  // parts of the launch being enqueued (GemmArgs::conc: they share the chip)
   int overlap_min = 64;                // split launches of >= this many sequences over two streams (0: never)
   std::string err;
   std::map<std::string, std::vector<int64_t>> expected;
@@ -696,6 +697,7 @@ GemmArgs dense(mmt_engine* e, float* ws, const bf16_t* A, const bf16_t* Al, int6
   // sizes to fp32 rounding, not bit for bit (test_batch_equals_single).
   a.ws = ws;
   a.ws_elems = ws ? kSplitKWsElems : 0;
+  a.conc = e->conc_parts;
   return a;
 }
 
@@ -1121,12 +1123,14 @@ void enqueue_split(mmt_engine* e, int b0, int n) {
   crop_geometry(e->params_dev, e->state_dev + b0, n, e->cfg.search_factor, e->cfg.search_size,
                 e->ring_handoff ? &e->hring : nullptr, e->gidx0, e->slot2pos, e->Lz, e->Lx, e->stream);
   const int P = std::min(e->nparts, n);
+  e->conc_parts = P;
   hipEventRecord(e->fork_ev, e->stream);
   for (int p = 1; p < P; ++p) hipStreamWaitEvent(e->xstream[p - 1], e->fork_ev, 0);
   for (int p = 0; p < P; ++p) {
     const int r0 = n * p / P, r1 = n * (p + 1) / P;
     enqueue_forward(e, b0 + r0, r0, r1 - r0, p ? e->xstream[p - 1] : e->stream, p, false);
   }
+  e->conc_parts = 1;
   for (int p = 1; p < P; ++p) {
     hipEventRecord(e->join_ev[p - 1], e->xstream[p - 1]);
     hipStreamWaitEvent(e->stream, e->join_ev[p - 1], 0);

@@ -178,7 +178,10 @@ struct LdsTile {
   static constexpr int ESZ = epi_is_bf16(EPI) ? 2 : 4;
   static constexpr int CH = 16 / ESZ;                 // elements per 16-B chunk
   static constexpr int NCH = COLS / CH;               // chunks per row
-  static constexpr int MASK = (NCH < 16 ? NCH : 16) - 1;
+  // the row's chunk XOR stays inside an aligned group of chunks: the largest power of two dividing NCH, at most 16
+  // (a 192-wide bf16 tile has 24 chunks per row: XOR with up to 15 would send chunks 16..23 past the row)
+  static constexpr int LOWBIT = NCH & -NCH;
+  static constexpr int MASK = (LOWBIT < 16 ? LOWBIT : 16) - 1;
   __device__ static int off(int row, int col) {       // byte offset of (row, col), col % 4 == 0
     return row * COLS * ESZ + ((((col / CH) ^ (row & MASK))) << 4) + (col % CH) * ESZ;
   }
@@ -334,8 +337,10 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
                         BM * BN * 4 <= T::NSTAGE * T::STAGE * 2 && (BM * (BN / 4)) % T::NT == 0;
   constexpr int SF_N = SF32 ? BM * (BN / 4) / T::NT : 1;   // drain chunks per thread
   constexpr bool SF_R = SF32 && epi_has_r(EPI);
-  u32x4 rsf[SF_R ? SF_N : 1];
-  if constexpr (SF_R) {
+  // (prefetched up to 8 chunks per thread: the 12 of a 128 x 192 tile held over the main loop spill)
+  constexpr bool SF_RPRE = SF_R && SF_N <= 8;
+  u32x4 rsf[SF_RPRE ? SF_N : 1];
+  if constexpr (SF_RPRE) {
     const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
 #pragma unroll
     for (int k = 0; k < SF_N; ++k) {
@@ -657,7 +662,14 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
     for (int k = 0; k < SF_N; ++k) {
       const int idx = tid + k * T::NT, r = idx / (BN / 4), c = idx - r * (BN / 4);
       f32x4 v = *reinterpret_cast<const f32x4*>(lds + r * BN * 4 + ((c ^ (r & LF::MASK)) << 4));
-      if constexpr (SF_R) v = __builtin_bit_cast(f32x4, rsf[k]) + v;   // R + (acc * inv + bias), as store4v
+      if constexpr (SF_RPRE) {
+        v = __builtin_bit_cast(f32x4, rsf[k]) + v;   // R + (acc * inv + bias), as store4v
+      } else if constexpr (SF_R) {
+        const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
+        const int m = m0 + r, row = EPI == EPI_POS_F32 ? m % args.pos_rows : m;
+        const uint32_t o = m < M ? (uint32_t)(((int64_t)row * g.ldr + n0 + 4 * c) * 4) : kBufOob;
+        v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rR, o, 0, 0)) + v;
+      }
       const uint32_t go = r < rows ? (uint32_t)(((int64_t)r * g.ldc + n0 + 4 * c) * 4) : kBufOob;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rC, go, 0, 0);
     }
@@ -1880,6 +1892,19 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         if (n768 == 1) return launch_cfg<256, 128, 4, 2, true, 3, 32>(a, epi, s);
         if (n768 == 2) return launch_cfg<256, 128, 4, 2, true, 2, 32>(a, epi, s);
         if (n768 == 3) return launch_cfg<128, 256, 2, 4, true, 2, 32>(a, epi, s);
+      }
+      // 128 x 192 tiles where all of them fit one round of the chip's one-workgroup-per-CU slots and 128 x 128 tiles
+      // would take two or more, counting the launches of the other stream parts that run beside this one (a.conc):
+      // the head's conv1 at 2 x 16 sequences (256 tiles in one round instead of 384: 287 -> 196 us alone), fc2 / proj
+      // after candidate elimination (fc2 123.6 -> 107.4 us per launch; the line +0.8 %, profiles/r05_ab_t192.txt).
+      // Where the 192-wide tiles take several rounds too (OSTrack-384's long layers: 3 against 5) they lost 1 %, so
+      // a one-round fit is the rule.  MMT_T192: 0 never, 2 always (tuning)
+      static const int t192 = getenv("MMT_T192") ? atoi(getenv("MMT_T192")) : 1;
+      if (t192 && a.N % 192 == 0 && a.groups == 1 && (a.amode == A_CONV3 || a.K % 64 == 0)) {
+        const int conc = a.conc > 1 ? a.conc : 1, slots = num_cus();
+        const int r128 = (conc * t128 * (a.N / 128) + slots - 1) / slots;
+        const int r192 = (conc * t128 * (a.N / 192) + slots - 1) / slots;
+        if (t192 == 2 || (r192 == 1 && r128 >= 2)) return launch_cfg<128, 192, 4, 2, true, 2, 64>(a, epi, s);
       }
       // (the N = 768 GEMMs -- proj, patch -- take the register-pipelined 64-deep tile since it exists: proj at one
       // half's rows 31 -> 25 us (5 120 rows) .. 27 -> 22 us (2 432), tests/r3_run33.sh; the wide qkv / fc1 fallbacks

@@ -52,6 +52,7 @@ struct GemmArgs {
   int sk_epi;
   int sk_sc1;       // 1: the slabs move write-through (sc1 stores and loads), no release / acquire fences
   int defer_reduce; // EPI_RESID_F32, one group: a split-K run leaves its partial slabs for the consumer (gemm())
+  int conc;         // launches of this shape running at once on the chip (the engine's stream parts; 0 / 1: alone)
 };
 
 // A residual-stream update whose split-K partial sums were left in the workspace (gemm() with defer_reduce):
