@@ -1822,6 +1822,19 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // TF/s vs 240-250 for the 2-barrier 128 x 128 kernel); N = 768 stays on 128-row tiles (3 column tiles of
     // 256 leave most CUs idle)
     static const int t256_min = getenv("MMT_256S_MIN") ? atoi(getenv("MMT_256S_MIN")) : 128;
+    // MMT_T192W (tuning, percent; 0 = off): a wide GEMM whose 256 x 256 tiles take two or more rounds of the chip
+    // (counting the concurrent stream part) takes 128 x 192 tiles instead when their rounds x 0.375 (their work
+    // against a 256 x 256 tile) x MMT_T192W / 100 (their lower MFMA efficiency) is smaller.  Off: at 150 the two
+    // halves' qkv / fc1 of the candidate-eliminated layers switch and the line loses 1.5 % (each class alone gains
+    // 6 %, profiles/r05_ab_t192_wide_rejected.txt)
+    static const int t192w = getenv("MMT_T192W") ? atoi(getenv("MMT_T192W")) : 0;
+    if (t192w > 0 && a.N >= 2048 && a.N % 192 == 0 && a.K % 64 == 0 && a.groups == 1 && a.amode == A_DENSE &&
+        (a.M + 127) / 128 >= 8) {
+      const int conc = a.conc > 1 ? a.conc : 1, slots = num_cus();
+      const int r256 = (conc * ((a.M + 255) / 256) * (a.N / 256) + slots - 1) / slots;
+      const int r192 = (conc * ((a.M + 127) / 128) * (a.N / 192) + slots - 1) / slots;
+      if (r256 >= 2 && r192 * 375 * t192w < r256 * 100000) return launch_cfg<128, 192, 4, 2, true, 2, 64>(a, epi, s);
+    }
     if (a.N >= 2048 && (a.M + 255) / 256 * (a.N / 256) * a.groups >= t256_min && launch256s_epi(a, epi, s)) return;
   }
   if constexpr (!SPLIT) {
