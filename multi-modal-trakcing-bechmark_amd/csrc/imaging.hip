@@ -81,12 +81,14 @@ __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
   const int O = a.out_sz;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= O * O) return;
-  const int oy = idx / O, ox = idx - oy * O;
+  // thread -> (patch, pixel within the patch): a wave's 64 pixels are 64 consecutive elements of each channel plane
+  // of a patch row (within = (oy & 15) * 16 + (ox & 15)), so every store instruction writes whole 128-B lines
+  // (an output-row order wrote 4 separate 32-B pieces per instruction, each line finished by 4 other workgroups)
+  const int np = O / 16;
+  const int patch = idx >> 8, within = idx & 255;
+  const int oy = (patch / np) * 16 + (within >> 4), ox = (patch % np) * 16 + (within & 15);
   int u8[6];
   cv_linear_u8([&](int r, int x, int c) { return crop_px(p, r, x, c); }, p.crop_sz, O, oy, ox, a.C, u8);
-  const int np = O / 16;
-  const int patch = (oy >> 4) * np + (ox >> 4);
-  const int within = (oy & 15) * 16 + (ox & 15);
   const int64_t rowoff = ((int64_t)b * a.rows_per_seq + a.row0 + patch) * 768;
   for (int c = 0; c < a.C; ++c) {
     const float t = ((float)u8[c] / 255.0f - kMean[c]) / kStd[c];
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
     } else {
       (c < 3 ? a.A_rgb : a.A_aux)[o] = f2bf(t);
     }
-    if (a.dbg_patch) a.dbg_patch[((int64_t)b * O * O + idx) * a.C + c] = (uint8_t)u8[c];
+    if (a.dbg_patch) a.dbg_patch[((int64_t)b * O * O + oy * O + ox) * a.C + c] = (uint8_t)u8[c];
   }
 }
 
