@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 5, run 32: the decode kernel with the conv5 outputs kept in the LDS (no dependent re-read by thread 0) and a
+# wave-butterfly argmax: parity / benchpath / OSTrack tests, then base vs variant at one sequence (+ trace) and 32
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r5_run32
+mkdir -p $O
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_benchpath.py tests/test_gpu_kernels.py > $O/tests.txt 2>&1 || { grep -E "FAIL|Error" $O/tests.txt | head; tail -3 $O/tests.txt; exit 1; }
+tail -1 $O/tests.txt
+ROUNDS=3 STEPS=300 ARGS="--batch 1" LIBDIR=abx timeout -k 10 500 bash tools/ab_bench.sh > $O/ab_b1.txt 2>&1 || { tail -5 $O/ab_b1.txt; exit 1; }
+cat $O/ab_b1.txt
+ROUNDS=2 STEPS=60 LIBDIR=abx timeout -k 10 400 bash tools/ab_bench.sh > $O/ab_b32.txt 2>&1 || { tail -5 $O/ab_b32.txt; exit 1; }
+cat $O/ab_b32.txt
+for lib in a_base b_decode; do
+  MMTRACK_LIB=$PWD/abx/lib$lib.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$lib -o run -- python bench.py --batch 1 --steps 100 --warmup 10 --no-cpu-baseline --no-extras --probe none --host-frames 0 > $O/prof_$lib.log 2>&1 || { tail -5 $O/prof_$lib.log; exit 1; }
+  echo "$lib: $(grep -h decode_kernel $(find $O/prof_$lib -name '*kernel_stats.csv') | cut -d, -f1-6)"
+  rm -rf $O/prof_$lib
+done
