@@ -8,7 +8,9 @@ timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread -
 tail -2 $O/gpu_suite.txt
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail -5 $O/smoke.txt; exit 1; }
 tail -1 $O/smoke.txt
+T0=$SECONDS
 timeout -k 10 400 python bench.py > $O/bench32.json 2> $O/bench32.err || { tail -5 $O/bench32.err; exit 1; }
+echo "default bench.py invocation: $((SECONDS - T0)) s wall" | tee $O/bench32_wall.txt
 python -c "import json; d=json.load(open('$O/bench32.json')); print('vit32', d['value'], d['roofline']['frac'], d['cpu_baseline']['value'])"
 timeout -k 10 300 python bench.py --batch 1 --steps 300 --warmup 30 --no-cpu-baseline > $O/bench1.json 2> $O/bench1.err || exit 1
 python -c "import json; d=json.load(open('$O/bench1.json')); print('vit1', d['value'], d['roofline']['kernel'], d['roofline']['frac'])"
