@@ -58,9 +58,16 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
   // would cost them workgroups per CU), stage through registers into one slot per wave / per workgroup.
   constexpr bool DMA = !KSPLIT && (WAVES >= 8 || !SPLIT);
   constexpr int KW = KSPLIT ? WAVES : (DMA ? 2 : 1);   // K / V staging slots (per wave, ring stages, or one)
-  __shared__ __attribute__((aligned(16))) bf16_t KsAll[KW][NH][KB * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t VsAll[KW][NH][KB * 64];
-  __shared__ float ce_row[CE_MAX];
+  // CE_V: the 5-wave key split (N <= 320, one key tile per wave) fills all 160 KB with its K / V slots, so each wave
+  // keeps its tile's CE logits in registers and stores them after the loop into the V slots' space (free by then)
+  constexpr bool CE_V = KSPLIT && WAVES == 5;
+  constexpr int KV_BYTES = KW * NH * KB * 64 * 2;   // the K (or V) slots
+  __shared__ __attribute__((aligned(16))) char lds_raw[2 * KV_BYTES + (CE_V ? 0 : CE_MAX * 4)];
+  bf16_t(&KsAll)[KW][NH][KB * 64] = *reinterpret_cast<bf16_t(*)[KW][NH][KB * 64]>(lds_raw);
+  bf16_t(&VsAll)[KW][NH][KB * 64] = *reinterpret_cast<bf16_t(*)[KW][NH][KB * 64]>(lds_raw + KV_BYTES);
+  float* const ce_row = reinterpret_cast<float*>(lds_raw + (CE_V ? KV_BYTES : 2 * KV_BYTES));
+  float cel[CE_V ? 16 : 1];
+  int cekb = -1;
 
   // XCD-aware order: logical id = (b * heads + h) * nqt + qt; blocks bid, bid + 8, ... (one XCD) take a
   // contiguous logical range, so the query tiles of one (b, h) share an L2
@@ -241,10 +248,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
       bmax = xmax32(bmax);
       if (ce_lane && rb == ce_rb) {
         // the tile's 64 logits (keys past N land in ce_row's slack, CE_MAX >= N + 64, and are never read)
+        if constexpr (CE_V) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+          for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) ce_row[kb + 16 * t + 4 * g + r] = sc[rb][t][r];
+            for (int r = 0; r < 4; ++r) cel[4 * t + r] = sc[rb][t][r];
+          cekb = kb;
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ce_row[kb + 16 * t + 4 * g + r] = sc[rb][t][r];
+        }
       }
       // f16x3: m, the logits and ce_row stay in the unscaled units of the accumulator; the scale qk_inv = 2^k
       // enters through lg = qk_inv log2(e) (exact: a power of two times log2(e)), so fma(s, lg, -m lg) is bit for bit
@@ -321,6 +336,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
     // merge the waves' partial softmax states in wave order: m = max m_w, l = sum l_w e^(m_w - m),
     // O = sum O_w e^(m_w - m); the K / V slots are free once every wave is past its last tile
     __syncthreads();
+    if constexpr (CE_V) {   // each wave's tile of the CE query's logits, now that every V slot is free
+      if (ce_lane && cekb >= 0)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ce_row[cekb + 16 * t + 4 * g + r] = cel[4 * t + r];
+    }
     float* st = reinterpret_cast<float*>(&KsAll[0][0][0]);   // [WAVES][18][64]
     if (wave > 0) {
       float* my = st + wave * 18 * 64 + lane;
@@ -427,7 +449,13 @@ static void attention_t(const AttnArgs& a, hipStream_t s) {
     // 240 workgroups whose K / V tiles load 4 waves at a time instead of one).  f16x3 only: the merge
     // changes the fp32 rounding with the batch size, which the bf16 mode keeps bit-exact (its kernel
     // choice does not change a query's arithmetic; test_batch_equals_single)
-    hipLaunchKernelGGL((attn_kernel<4, SPLIT, 1, true>), dim3((a.N + 15) / 16 * bh), dim3(256), 0, s, a);
+    // (257..320 keys: five tiles, so five waves take one each instead of the first wave taking two; MMT_ATTN_KS5=0,
+    // tuning: four)
+    static const bool ks5 = !getenv("MMT_ATTN_KS5") || atoi(getenv("MMT_ATTN_KS5")) != 0;
+    if (ks5 && a.N > 4 * KB && a.N <= 5 * KB)
+      hipLaunchKernelGGL((attn_kernel<5, SPLIT, 1, true>), dim3((a.N + 15) / 16 * bh), dim3(320), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_kernel<4, SPLIT, 1, true>), dim3((a.N + 15) / 16 * bh), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL((attn_kernel<1, SPLIT>), dim3((a.N + 15) / 16 * bh), dim3(64), 0, s, a);
   }
