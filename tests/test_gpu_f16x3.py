@@ -69,7 +69,8 @@ def _gemm(lib, Ah, Al, Wh, Wl, bias, C, Cl, inv, out_scale, epi, R=None, M=None)
     (4896, 2304, 768, 0),     # qkv after the last CE (153 tokens)
     (10240, 768, 768, 2),     # proj: 128 x 128, 32-deep K-tiles
     (4896, 768, 3072, 2),     # fc2 after the last CE: 128 x 128, 64-deep K-tiles
-    (7808, 768, 3072, 2),     # fc2 (244 tokens)
+    (7808, 768, 3072, 2),     # fc2 (244 tokens): 128 x 192 tiles (one round of them against two of 128 x 128)
+    (6080, 768, 768, 2),      # proj (190 tokens): 128 x 192, the residual chunks loaded in the drain
     (4096, 768, 768, 4),      # patch embed (fp32 output)
     (320, 2304, 768, 0),      # one sequence: 64 x 64 few-tile kernels
     (320, 3072, 768, 1),
