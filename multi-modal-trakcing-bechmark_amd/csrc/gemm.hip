@@ -1642,7 +1642,8 @@ template <int EPI>
 static void launch256s(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   const int tiles_m = (a.M + 255) / 256;
-  a.gm = tiles_m < 4 ? tiles_m : 4;
+  static const int gm256 = getenv("MMT_GM256") ? atoi(getenv("MMT_GM256")) : 4;   // tuning: super-tile height
+  a.gm = tiles_m < gm256 ? tiles_m : gm256;
   hipLaunchKernelGGL(gemm256s_kernel<EPI>, dim3(tiles_m * (a.N / 256), 1, a.groups), dim3(512), 0, s, a);
 }
 
