@@ -422,7 +422,8 @@ int mmt_dimp_optimize_strided(const float* feat, int64_t feat_img_stride, int64_
 int mmt_op_gemm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, void* C, int64_t ldc,
                 const float* R, int64_t ldr, int M, int N, int K, int epi, int conv_hw, int conv_cin, int pos_rows,
                 void* hip_stream);
-int mmt_gemm_force_config(int cfg);   /* tuning: pin the dense-GEMM tile config (-1 = heuristic) */
+int mmt_gemm_force_config(int cfg);   /* tuning: pin the dense-GEMM tile config (-1 = heuristic); 320 / 256 pin the
+                                         f16x3 qkv / fc1 GEMMs to 320 x 256 / 256 x 256 tiles */
 int mmt_gemm_stamps(void* dev_buf);   /* tuning: per-block s_memtime stamps [blocks][4] (start, main loop,
                                          epilogue, end) into a device buffer; NULL turns them off */
 int mmt_op_attention(const void* qkv, void* out, int B, int N, int heads, int ce_query, int ce_lens_t,

@@ -134,7 +134,6 @@ struct mmt_engine {
         *c8 = nullptr, *fstat = nullptr, *h4 = nullptr, *ce_prob = nullptr, *res = nullptr, *dbg_maps = nullptr,
         *dbg_feat = nullptr;
   int *gidx0 = nullptr, *gidx1 = nullptr, *slot2pos = nullptr, *gather = nullptr, *removed = nullptr;
-  int* pbar = nullptr;          // [B][32] per-sequence barrier words of the fused prompt + LN1 kernel (zero)
   float* splitk_ws = nullptr;   // [kMaxParts launch parts][kSplitKWsElems] fp32 split-K partials (few-tile GEMMs)
   uint8_t* dbg_patch = nullptr;
   CropParam* params_dev = nullptr;
@@ -568,7 +567,7 @@ int alloc_acts(mmt_engine* e) {
       {(void**)&e->ce_prob, (size_t)B * HEADS * Lx * 4}, {(void**)&e->res, (size_t)B * 8 * 4},
       {(void**)&e->gidx0, (size_t)B * Lx * 4},         {(void**)&e->gidx1, (size_t)B * Lx * 4},
       {(void**)&e->slot2pos, (size_t)B * Lx * 4},      {(void**)&e->gather, (size_t)B * L * 4},
-      {(void**)&e->removed, (size_t)B * Lx * 4},       {(void**)&e->pbar, (size_t)B * 32 * 4},
+      {(void**)&e->removed, (size_t)B * Lx * 4},
       {(void**)&e->params_dev, (size_t)B * sizeof(CropParam)},
       {(void**)&e->state_dev, (size_t)B * sizeof(SeqState)}, {(void**)&e->out_dev, (size_t)B * sizeof(TrackOut)},
   };
@@ -907,10 +906,8 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
       la.out = q_Hn;
       la.out_lo = q_Hn_l;
       la.out_scale = w.ln1_s;
-      if (ln_mode == 1 || !prompt_ln_fused(pa, la, e->pbar + (size_t)r0 * 32, s)) {
-        if (ln_mode == 2) prompt_reduce(pa, s);
-        prompt_expand_ln(la, s);
-      }
+      if (ln_mode == 2) prompt_reduce(pa, s);
+      prompt_expand_ln(la, s);
     } else {
       layernorm(X, w.n1w, w.n1b, q_Hn, q_Hn_l, w.ln1_s, nullptr, n * Na, Na, nullptr, Na, nullptr, s, pend);
       pend = RowReduce{};

@@ -120,7 +120,7 @@ __device__ __forceinline__ void store4v(const GemmGroup& g, const GemmArgs& args
 
 constexpr bool epi_has_r(int e) { return e == EPI_RESID_F32 || e == EPI_POS_F32; }
 
-// the same loading its own operands (one fragment: the split-K reduce, sk_combine)
+// the same loading its own operands (one fragment: the split-K reduce)
 template <int EPI, bool SPLIT>
 __device__ __forceinline__ void store4(const GemmGroup& g, const GemmArgs& args, int m, int n, const f32x4& a) {
   const float4 bv = g.bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -231,35 +231,6 @@ struct LdsTile {
     }
   }
 };
-
-// the last slice of a split-K tile sums the ksplit fp32 slabs of the tile in slice order and applies
-// the epilogue (the arithmetic of splitk_reduce_kernel)
-template <int EPI, bool SPLIT, int BM, int BN, int NT>
-__device__ __forceinline__ void sk_combine(const GemmArgs& args, const GemmGroup& g, int m0, int n0) {
-  const int64_t MN = (int64_t)args.M * args.N;
-  const float* base = args.ws + (int64_t)blockIdx.z * args.ksplit * MN;
-  const rsrc_t rs = make_rsrc(base, args.ksplit * MN * 4);
-  constexpr int NCH = BN / 4;
-#pragma unroll
-  for (int k = 0; k < BM * NCH / NT; ++k) {
-    const int idx = threadIdx.x + k * NT;
-    const int r = idx / NCH, c = idx - r * NCH;
-    const int m = m0 + r, n = n0 + c * 4;
-    if (m >= args.M) continue;
-    f32x4 acc;
-    if (args.sk_sc1) {   // every load of a write-through slab is an sc1 load (no acquire was taken)
-      const int o = (m * args.N + n) * 4;
-      acc = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
-      for (int s = 1; s < args.ksplit; ++s)
-        acc += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + (int)(s * MN * 4), 0, 16));
-    } else {
-      const float* p = base + (int64_t)m * args.N + n;
-      acc = *reinterpret_cast<const f32x4*>(p);
-      for (int s = 1; s < args.ksplit; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * MN);
-    }
-    store4<EPI, SPLIT>(g, args, m, n, acc);
-  }
-}
 
 // scheduling groups: NR times {one LDS read, K MFMAs}
 template <int NR, int K>
@@ -574,59 +545,7 @@ __global__ __launch_bounds__(WMW* WNW * 64) void gemm_kernel(const GemmArgs args
         LT::put(lds, wm * T::WM + i * 16 + (lane & 15), col, v);
       }
     __syncthreads();
-    if (args.sk_cnt && args.sk_sc1) {   // write-through slab stores straight from the LDS tile
-      const int rows = min(BM, M - m0);
-      const rsrc_t rs = make_rsrc(static_cast<float*>(gp.C) + (int64_t)m0 * args.N, (int64_t)rows * args.N * 4);
-#pragma unroll
-      for (int k = 0; k < BM * LT::NCH / T::NT; ++k) {
-        const int idx = tid + k * T::NT;
-        const int r = idx / LT::NCH, c = idx - r * LT::NCH;
-        if (r >= rows) continue;
-        const u32x4 d = *reinterpret_cast<const u32x4*>(lds + r * BN * 4 + ((c ^ (r & LT::MASK)) << 4));
-        __builtin_amdgcn_raw_buffer_store_b128(d, rs, (r * args.N + n0 + c * 4) * 4, 0, 16);
-      }
-    } else {
-      LT::template drain<BM, T::NT>(lds, gp, args, m0, n0, M);
-    }
-    if (args.sk_cnt) {
-      // in-launch combine (cdna_hip_programming.md, split-K seam): every wave retires its slab stores,
-      // one lane publishes them with an agent-scope release and draws a ticket; the slice that draws
-      // ksplit - 1 resets the ticket, acquires, and reduces the slabs in slice order 0, 1, .. -- the
-      // order and arithmetic of splitk_reduce_kernel, so either path gives the same bits
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      int* flag = reinterpret_cast<int*>(smem);
-      if (tid == 0) {
-        unsigned* cnt = args.sk_cnt + blockIdx.z * ntiles + id;
-        if (!args.sk_sc1) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = t == (unsigned)(args.ksplit - 1);
-        if (last) {
-          __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (!args.sk_sc1) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-        }
-        flag[0] = last;
-      }
-      __syncthreads();
-      if (flag[0]) {
-        switch (args.sk_epi) {
-          case EPI_BF16: sk_combine<EPI_BF16, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
-          case EPI_GELU_BF16: sk_combine<EPI_GELU_BF16, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
-          case EPI_RESID_F32: sk_combine<EPI_RESID_F32, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
-          case EPI_RELU_BF16: sk_combine<EPI_RELU_BF16, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
-          case EPI_F32: sk_combine<EPI_F32, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
-          case EPI_RELU_F32: sk_combine<EPI_RELU_F32, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
-          case EPI_POS_F32: sk_combine<EPI_POS_F32, SPLIT, BM, BN, T::NT>(args, g, m0, n0); break;
-          default: break;
-        }
-      }
-    }
+    LT::template drain<BM, T::NT>(lds, gp, args, m0, n0, M);
   } else if constexpr (LDS_EPI) {
     char* lds = reinterpret_cast<char*>(smem);
 #pragma unroll
@@ -1342,43 +1261,73 @@ static void launch256_epi(const GemmArgs& a, int epi, hipStream_t s) {
 // 240-260 TF/s, 29-31 % of the pipe); here loads run 5-6 phases ahead and the two wave groups (waves 0-3,
 // 4-7, one barrier apart) alternate MFMA and fragment/load work on every SIMD.  Each phase multiplies
 // one 128 x 128 quadrant: per wave 64 x 32 = 4 x 2 fragment pairs x 3 products = 24 MFMAs.
-template <int EPI>
+//
+// MI = 5 (round 6): the same kernel on 320 x 256 tiles, for the bf16-output GEMMs (qkv, fc1) whose 256 x 256 tiles
+// take two rounds of the chip's one-workgroup-per-CU slots for a little over one round of work while 320-row tiles
+// fit one (the candidate-eliminated layers: qkv at 2 x 16 x 244 rows, 288 -> 234 tiles; fc1 at 2 x 16 x 190 rows,
+// 288 -> 240).  A quadrant is 160 x 128, a wave's share 80 x 32 = 5 x 2 fragment pairs (30 MFMAs per phase, 160
+// accumulators).  An A half-tile is 160 rows: the two planes' rows 0..127 load as in the 256-row kernel, rows
+// 128..159 by one more instruction on waves 0-3 (waves 0, 1: hi; 2, 3: lo), so those waves count 3 loads per A
+// half-tile in their vmcnt waits and waves 4-7 count 2.  The bias goes to the LDS (one DMA by wave 0) instead of
+// 16 VGPRs and is read back after the K loop, when the fragment registers are free; the epilogue stages a
+// 160-row half (hi + lo planes: the whole 160 KB).
+template <int EPI, int MI>
 __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
+  static_assert(MI == 4 || (MI == 5 && epi_is_bf16(EPI)), "320-row tiles: 16-bit epilogues only");
+  constexpr int BM = 64 * MI, HR = BM / 2;                   // tile rows; rows per A half-tile
+  constexpr int AH = HR * 32;                                // elements of one A half-tile plane
+  constexpr int P1 = 2 * AH, P2 = P1 + 8192, P3 = P2 + 8192;  // stage offsets of W0, W1, A1 (A0 at 0)
+  constexpr int STG = P3 + 2 * AH;                           // elements per stage
+  constexpr bool BIAS_LDS = MI > 4;
+  constexpr int SMEM_OPS = 2 * STG + (BIAS_LDS ? 512 : 0);
+  constexpr int SMEM_EPI = epi_is_bf16(EPI) ? HR * 256 * 2 : 0;
+  constexpr int SMEM = SMEM_OPS > SMEM_EPI ? SMEM_OPS : SMEM_EPI;
+  static_assert(SMEM * 2 <= 160 * 1024, "LDS");
 #ifdef GEMM_PHASE_STAMPS
-  // tuning build: per phase, wave 0 and wave 4 stamp (before the counted wait, after the first barrier = MFMA start,
-  // after the second barrier) into an LDS tail of the one staging array; copied to mmt_gemm_stamps' buffer at the end
+  // tuning build (256-row tiles): per phase, wave 0 and wave 4 stamp (before the counted wait, after the first
+  // barrier = MFMA start, after the second barrier) into an LDS tail of the one staging array; copied to
+  // mmt_gemm_stamps' buffer at the end
   constexpr int PS_PH = 3 * 96;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 8192 + 2 * PS_PH * 4];
-  unsigned long long* const pst = reinterpret_cast<unsigned long long*>(smem + 8 * 8192);
-#define PSTAMP(slot)                                                                                          \
-  do {                                                                                                        \
-    if ((threadIdx.x & 255) == 0 && (slot) < PS_PH) pst[(threadIdx.x >> 8) * PS_PH + (slot)] = __builtin_amdgcn_s_memtime(); \
+  constexpr int PSE = MI == 4 ? 2 * PS_PH * 4 : 0;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM + PSE];
+  unsigned long long* const pst = reinterpret_cast<unsigned long long*>(smem + SMEM);
+#define PSTAMP(slot)                                                                                           \
+  do {                                                                                                         \
+    if (MI == 4 && (threadIdx.x & 255) == 0 && (slot) < PS_PH)                                                 \
+      pst[(threadIdx.x >> 8) * PS_PH + (slot)] = __builtin_amdgcn_s_memtime();                                 \
   } while (0)
 #else
-  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 8192];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
 #define PSTAMP(slot) do { } while (0)
 #endif
   GEMM_STAMP_DECL;
   const GemmGroup& g = args.g[blockIdx.z];
   const int M = args.M, K = args.K;
-  const int tiles_m = (M + 255) / 256, tiles_n = args.N / 256, ntiles = tiles_m * tiles_n;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = args.N / 256, ntiles = tiles_m * tiles_n;
   const int b = blockIdx.x, x = b & 7, j = b >> 3;
   const int q = ntiles >> 3, r8 = ntiles & 7;
   const int id = (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + j;
   int tm, tn;
   tile_of(id, tiles_m, tiles_n, args.gm, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
+  const int m0 = tm * BM, n0 = tn * 256;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   GEMM_STAMP(0);
-  // the lane's 4 bias chunks (2 column halves x 2), requested before the first half-tile loads (the prologue's
-  // counted wait retires them; the epilogue then starts without a dependent round trip)
+  // the bias: MI = 4, the lane's 4 bias chunks (2 column halves x 2), requested before the first half-tile loads (the
+  // prologue's counted wait retires them; the epilogue then starts without a dependent round trip); MI = 5, the
+  // tile's 256 values DMA'd to the LDS tail by wave 0 ahead of its operand loads (retired by the same wait)
   const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)args.N * 4 : 0);
   float4 bq[2][2];
+  float* const bias_lds = reinterpret_cast<float*>(smem + 2 * STG);
+  if constexpr (BIAS_LDS) {
+    if (wave == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lptr_t)bias_lds, 16, (uint32_t)(n0 + lane * 4) * 4, 0, 0, 0);
+  } else {
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) bq[h][jj] = epi_bias(rB, n0 + h * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4);
+      for (int jj = 0; jj < 2; ++jj) bq[h][jj] = epi_bias(rB, n0 + h * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4);
+  }
 
   // half-tile loads: a wave-instruction fills 16 rows x 64 B (swzk<32> image, source chunk pre-swizzled)
   const int chunk = ((lane & 3) ^ ((lane >> 4) & 2)) * 16;
@@ -1388,19 +1337,30 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
   const rsrc_t rW = make_rsrc(g.W + (int64_t)n0 * g.ldw, (int64_t)256 * g.ldw * 2);
   const rsrc_t rWl = make_rsrc(g.W_lo + (int64_t)n0 * g.ldw, (int64_t)256 * g.ldw * 2);
   const uint32_t va = (uint32_t)(lrow * g.lda * 2 + chunk), vw = (uint32_t)(lrow * g.ldw * 2 + chunk);
-  const uint32_t a128 = 128u * g.lda * 2, w128 = 128u * g.ldw * 2;
+  const uint32_t aH = (uint32_t)HR * g.lda * 2, w128 = 128u * g.ldw * 2;
+  // MI = 5: rows 128..159 of an A half-tile (waves 0-3: wave & 1 picks the 16-row group, wave & 2 the plane)
+  const uint32_t vx = (uint32_t)((128 + (wave & 1) * 16 + (lane >> 2)) * g.lda * 2 + chunk);
   const int nk = K / 32, NL = 4 * nk;
 
-  // half-tile L (pos = L & 3: 0 A rows 0-127, 1 W rows 0-127, 2 W rows 128-255, 3 A rows 128-255)
+  // half-tile L (pos = L & 3: 0 A rows 0..HR-1, 1 W rows 0-127, 2 W rows 128-255, 3 A rows HR..BM-1)
   auto issue = [&](int L, auto pos_c) {
     constexpr int pos = decltype(pos_c)::value;
+    constexpr bool isA = pos == 0 || pos == 3;
+    constexpr int poff = pos == 0 ? 0 : pos == 1 ? P1 : pos == 2 ? P2 : P3;
+    constexpr int plo = isA ? AH : 4096;
     const int kt = L >> 2;
-    bf16_t* dst = smem + ((kt & 1) * 4 + pos) * 8192 + wave * 512;
+    bf16_t* const slot = smem + (kt & 1) * STG + poff;
+    bf16_t* dst = slot + wave * 512;
     const int soff = kt * 64;
-    const bool isA = pos == 0 || pos == 3;
-    const uint32_t v = pos == 0 ? va : pos == 3 ? va + a128 : pos == 1 ? vw : vw + w128;
+    const uint32_t v = pos == 0 ? va : pos == 3 ? va + aH : pos == 1 ? vw : vw + w128;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rW, (lptr_t)dst, 16, v, soff, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rAl : rWl, (lptr_t)(dst + 4096), 16, v, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rAl : rWl, (lptr_t)(dst + plo), 16, v, soff, 0, 0);
+    if constexpr (isA && MI == 5) {
+      if (wave < 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds((wave & 2) ? rAl : rA,
+                                                 (lptr_t)(slot + ((wave & 2) ? AH : 0) + 128 * 32 + (wave & 1) * 512),
+                                                 16, pos == 0 ? vx : vx + aH, soff, 0, 0);
+    }
   };
   auto wait_vm = [&](int n) {   // n half-tiles (2 loads each) may stay in flight
     if (n >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -1409,22 +1369,33 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
     else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
+  // steady-state wait of one phase: G0 loads may stay in flight on waves 0-3, G1 on waves 4-7 (MI = 4: the same)
+  auto wait_steady = [&](auto g0_c, auto g1_c) {
+    constexpr int G0 = decltype(g0_c)::value, G1 = decltype(g1_c)::value;
+    if constexpr (G0 == G1) vm_wait_n<G0>();
+    else if (wr == 0) vm_wait_n<G0>();
+    else vm_wait_n<G1>();
+  };
+  using I6 = std::integral_constant<int, 6>;
+  using I8 = std::integral_constant<int, 8>;
+  using I7 = std::integral_constant<int, 7>;
+  using I10 = std::integral_constant<int, 10>;
 
-  f32x4 acc[4][4][2];
+  f32x4 acc[4][MI][2];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) acc[a][i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 Ah[4], Al[4], B0h[2], B0l[2], B1h[2], B1l[2];
+  bf16x8 Ah[MI], Al[MI], B0h[2], B0l[2], B1h[2], B1l[2];
   const int c = lane >> 4;
   auto read_a = [&](const bf16_t* S) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wr * 64 + i * 16 + (lane & 15);
+    for (int i = 0; i < MI; ++i) {
+      const int row = wr * (16 * MI) + i * 16 + (lane & 15);
       Ah[i] = *reinterpret_cast<const bf16x8*>(S + swzk<32>(row, c));
-      Al[i] = *reinterpret_cast<const bf16x8*>(S + 4096 + swzk<32>(row, c));
+      Al[i] = *reinterpret_cast<const bf16x8*>(S + AH + swzk<32>(row, c));
     }
   };
   auto read_b = [&](const bf16_t* S, bf16x8 (&Bh)[2], bf16x8 (&Bl)[2]) {
@@ -1435,28 +1406,18 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
       Bl[jj] = *reinterpret_cast<const bf16x8*>(S + 4096 + swzk<32>(row, c));
     }
   };
-#ifndef GEMM256S_DMA_IN_MFMA
-#define GEMM256S_DMA_IN_MFMA 0
-#endif
-  // mid(): GEMM256S_DMA_IN_MFMA (tuning build) issues the phase's half-tile loads after the first eight MFMAs instead
-  // of before the phase barrier, so their issue cost leaves the fragment-read side of the ping-pong
-  auto mma = [&](f32x4 (&C)[4][2], const bf16x8 (&Bh)[2], const bf16x8 (&Bl)[2], auto mid) {
+  auto mma = [&](f32x4 (&C)[MI][2], const bf16x8 (&Bh)[2], const bf16x8 (&Bl)[2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bh[jj], Ah[i], C[i][jj]);
-    if constexpr (GEMM256S_DMA_IN_MFMA) {
-      __builtin_amdgcn_sched_barrier(0);
-      mid();
-      __builtin_amdgcn_sched_barrier(0);
-    }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bl[jj], Ah[i], C[i][jj]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bh[jj], Al[i], C[i][jj]);
     __builtin_amdgcn_s_setprio(0);
@@ -1467,56 +1428,73 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
     const int need = P + (p == 2 ? 1 : 2);
     return max(min(P + 6, NL) - need - 1, 0);
   };
+  // the tail phases' wait: MI = 4, n_after half-tiles of 2 loads; MI = 5, those half-tiles' loads counted one by one
+  // (an A half-tile is 3 loads on waves 0-3)
+  auto wait_tail = [&](int P, int p) {
+    const int n = n_after(P, p);
+    if constexpr (MI == 4) {
+      wait_vm(n);
+    } else {
+      const int need = P + (p == 2 ? 1 : 2), na = wr == 0 ? 3 : 2;
+      int loads = 0;
+      for (int L = need + 1; L <= need + n; ++L) loads += ((L & 3) == 0 || (L & 3) == 3) ? na : 2;
+      vm_wait_rt<16>(loads);
+    }
+  };
   auto ktile = [&](int kt, auto steady_c) {
     constexpr bool STEADY = decltype(steady_c)::value;
-    const bf16_t* S = smem + (kt & 1) * 4 * 8192;
+    const bf16_t* S = smem + (kt & 1) * STG;
     const int P0 = 4 * kt;
-    read_b(S + 8192, B0h, B0l);
+    read_b(S + P1, B0h, B0l);
     read_a(S);
     PSTAMP(3 * P0);
-    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0, 0));
-    auto ld0 = [&]() {
-      if (STEADY || P0 + 6 < NL) issue(P0 + 6, std::integral_constant<int, 2>{});
-    };
-    if constexpr (!GEMM256S_DMA_IN_MFMA) ld0();
+    if (STEADY) {
+      if constexpr (MI == 4) wait_steady(I6{}, I6{}); else wait_steady(I8{}, I6{});
+    } else {
+      wait_tail(P0, 0);
+    }
+    if (STEADY || P0 + 6 < NL) issue(P0 + 6, std::integral_constant<int, 2>{});
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 1);
-    mma(acc[0], B0h, B0l, ld0);
+    mma(acc[0], B0h, B0l);
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 2);
-    read_b(S + 2 * 8192, B1h, B1l);
+    read_b(S + P2, B1h, B1l);
     PSTAMP(3 * P0 + 3);
-    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 1, 1));
-    auto ld1 = [&]() {
-      if (STEADY || P0 + 7 < NL) issue(P0 + 7, std::integral_constant<int, 3>{});
-    };
-    if constexpr (!GEMM256S_DMA_IN_MFMA) ld1();
+    if (STEADY) {
+      if constexpr (MI == 4) wait_steady(I6{}, I6{}); else wait_steady(I7{}, I6{});
+    } else {
+      wait_tail(P0 + 1, 1);
+    }
+    if (STEADY || P0 + 7 < NL) issue(P0 + 7, std::integral_constant<int, 3>{});
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 4);
-    mma(acc[1], B1h, B1l, ld1);
+    mma(acc[1], B1h, B1l);
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 5);
-    read_a(S + 3 * 8192);
+    read_a(S + P3);
     PSTAMP(3 * P0 + 6);
-    if (STEADY) asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); else wait_vm(n_after(P0 + 2, 2));
-    auto ld2 = [&]() {
-      if (STEADY || P0 + 8 < NL) issue(P0 + 8, std::integral_constant<int, 0>{});
-    };
-    if constexpr (!GEMM256S_DMA_IN_MFMA) ld2();
+    if (STEADY) {
+      if constexpr (MI == 4) wait_steady(I8{}, I8{}); else wait_steady(I10{}, I8{});
+    } else {
+      wait_tail(P0 + 2, 2);
+    }
+    if (STEADY || P0 + 8 < NL) issue(P0 + 8, std::integral_constant<int, 0>{});
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 7);
-    mma(acc[2], B1h, B1l, ld2);
+    mma(acc[2], B1h, B1l);
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 8);
     PSTAMP(3 * P0 + 9);
-    if (STEADY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else wait_vm(n_after(P0 + 3, 3));
-    auto ld3 = [&]() {
-      if (STEADY || P0 + 9 < NL) issue(P0 + 9, std::integral_constant<int, 1>{});
-    };
-    if constexpr (!GEMM256S_DMA_IN_MFMA) ld3();
+    if (STEADY) {
+      if constexpr (MI == 4) wait_steady(I6{}, I6{}); else wait_steady(I8{}, I6{});
+    } else {
+      wait_tail(P0 + 3, 3);
+    }
+    if (STEADY || P0 + 9 < NL) issue(P0 + 9, std::integral_constant<int, 1>{});
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 10);
-    mma(acc[3], B0h, B0l, ld3);
+    mma(acc[3], B0h, B0l);
     __builtin_amdgcn_s_barrier();
     PSTAMP(3 * P0 + 11);
   };
@@ -1525,12 +1503,15 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
   issue(1, std::integral_constant<int, 1>{});
   issue(2, std::integral_constant<int, 2>{});
   issue(3, std::integral_constant<int, 3>{});
+  // half-tiles 0 and 1 (A0, W0) landed: 2..5 (or 2, 3) may stay in flight
   if (nk > 1) {
     issue(4, std::integral_constant<int, 0>{});
     issue(5, std::integral_constant<int, 1>{});
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (MI == 4) wait_steady(I8{}, I8{}); else wait_steady(I10{}, I8{});
   } else {
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if constexpr (MI == 4) vm_wait_n<4>();
+    else if (wr == 0) vm_wait_n<5>();
+    else vm_wait_n<4>();
   }
   __builtin_amdgcn_s_barrier();
   GEMM_STAMP(1);
@@ -1544,25 +1525,32 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
 
   constexpr int QA[4] = {0, 0, 1, 1}, QB[4] = {0, 1, 1, 0};
   if constexpr (epi_is_bf16(EPI)) {
-    // 16-bit outputs (qkv, fc1): per 128-row half, the hi and lo planes of the half go to the LDS (64 KB each, the
-    // whole staging array), then every lane stores whole 16-B row chunks, eight lanes per 128-B line.  Stored straight
-    // from the fragments, a wave-instruction wrote 16 rows x 32 B and the epilogue took ~35k of a tile's ~145k
-    // cycles (round-5 phase stamps, tools/gemm256s_phases.py); same values, same bits.
-    using LT = LdsTile<EPI_BF16, 256>;   // [128][256] 16-bit, 16-B chunks XOR-swizzled by row
+    // 16-bit outputs (qkv, fc1): per HR-row half, the hi and lo planes of the half go to the LDS (the whole staging
+    // array), then every lane stores whole 16-B row chunks, eight lanes per 128-B line.  Stored straight from the
+    // fragments, a wave-instruction wrote 16 rows x 32 B and the epilogue took ~35k of a tile's ~145k cycles
+    // (round-5 phase stamps, tools/gemm256s_phases.py); same values, same bits.
+    if constexpr (BIAS_LDS) {   // the bias back from the LDS tail before the staging overwrites it
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          bq[h][jj] = *reinterpret_cast<const float4*>(bias_lds + h * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4);
+    }
+    using LT = LdsTile<EPI_BF16, 256>;   // [HR][256] 16-bit, 16-B chunks XOR-swizzled by row
     char* const planeH = reinterpret_cast<char*>(smem);
-    char* const planeL = planeH + 128 * 256 * 2;
+    char* const planeL = planeH + HR * 256 * 2;
     const int tid = threadIdx.x;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      __syncthreads();   // h = 0: every wave's last fragment reads are done; h = 1: the first half is drained
+      __syncthreads();   // h = 0: every wave's last fragment (and bias) reads are done; h = 1: the first half is drained
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd) {
         if (QA[qd] != h) continue;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) {
-            const int row = wr * 64 + i * 16 + (lane & 15);
+            const int row = wr * (16 * MI) + i * 16 + (lane & 15);
             const int col = QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4;
             const f32x4& a = acc[qd][i][jj];
             const float4 bv = bq[QB[qd]][jj];
@@ -1589,13 +1577,13 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
           }
       }
       __syncthreads();
-      // 128 rows x 32 chunks per plane; rows past M fall outside the C resources (zero-sized tail) and are dropped
-      const int rows = max(0, min(128, M - (m0 + h * 128)));
-      const rsrc_t rC = make_rsrc(static_cast<bf16_t*>(g.C) + (int64_t)(m0 + h * 128) * g.ldc, (int64_t)rows * g.ldc * 2);
-      const rsrc_t rCl = make_rsrc(static_cast<bf16_t*>(g.C_lo) + (int64_t)(m0 + h * 128) * g.ldc,
+      // HR rows x 32 chunks per plane; rows past M fall outside the C resources (zero-sized tail) and are dropped
+      const int rows = max(0, min(HR, M - (m0 + h * HR)));
+      const rsrc_t rC = make_rsrc(static_cast<bf16_t*>(g.C) + (int64_t)(m0 + h * HR) * g.ldc, (int64_t)rows * g.ldc * 2);
+      const rsrc_t rCl = make_rsrc(static_cast<bf16_t*>(g.C_lo) + (int64_t)(m0 + h * HR) * g.ldc,
                                    (int64_t)rows * g.ldc * 2);
 #pragma unroll
-      for (int it = 0; it < 128 * 32 / 512; ++it) {
+      for (int it = 0; it < HR * 32 / 512; ++it) {
         const int idx = tid + it * 512, r = idx >> 5, c = idx & 31;
         const int lo = r * 512 + ((c ^ (r & 15)) << 4);
         const uint32_t go = r < rows ? (uint32_t)(((int64_t)r * g.ldc + n0 + c * 8) * 2) : kBufOob;
@@ -1605,56 +1593,67 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
     }
     GEMM_STAMP(3);
 #ifdef GEMM_PHASE_STAMPS
+    if constexpr (MI == 4) {
+      __syncthreads();
+      if (gemm_stamps_ && blockIdx.x < 256)
+        for (int e = threadIdx.x; e < 2 * PS_PH; e += 512)
+          gemm_stamps_[65536 + (size_t)blockIdx.x * 2 * PS_PH + e] = pst[e];
+    }
+#endif
+    return;
+  } else {
+    // (the residual epilogues, not used by the path's launches, keep the per-fragment store4)
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd)
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + QA[qd] * HR + wr * (16 * MI) + i * 16 + (lane & 15);
+        if (m >= M) continue;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          if constexpr (epi_has_r(EPI))
+            store4<EPI, true>(g, args, m, n0 + QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, acc[qd][i][jj]);
+          else
+            store4v<EPI, true>(g, args, m, n0 + QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, acc[qd][i][jj],
+                               bq[QB[qd]][jj], zero4);
+      }
+    GEMM_STAMP(3);
+#ifdef GEMM_PHASE_STAMPS
     __syncthreads();
-    if (gemm_stamps_ && blockIdx.x < 256)
+    if (gemm_stamps_ && blockIdx.x < 256)   // blocks' phase stamps after the [blocks][4] kernel stamps
       for (int e = threadIdx.x; e < 2 * PS_PH; e += 512)
         gemm_stamps_[65536 + (size_t)blockIdx.x * 2 * PS_PH + e] = pst[e];
 #endif
-    return;
   }
-  // (the residual epilogues, not used by the path's launches, keep the per-fragment store4)
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + QA[qd] * 128 + wr * 64 + i * 16 + (lane & 15);
-      if (m >= M) continue;
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
-        if constexpr (epi_has_r(EPI))
-          store4<EPI, true>(g, args, m, n0 + QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, acc[qd][i][jj]);
-        else
-          store4v<EPI, true>(g, args, m, n0 + QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, acc[qd][i][jj],
-                             bq[QB[qd]][jj], zero4);
-    }
-  GEMM_STAMP(3);
-#ifdef GEMM_PHASE_STAMPS
-  __syncthreads();
-  if (gemm_stamps_ && blockIdx.x < 256)   // blocks' phase stamps after the [blocks][4] kernel stamps
-    for (int e = threadIdx.x; e < 2 * PS_PH; e += 512)
-      gemm_stamps_[65536 + (size_t)blockIdx.x * 2 * PS_PH + e] = pst[e];
-#endif
 }
 #undef PSTAMP
 
-template <int EPI>
+template <int EPI, int MI>
 static void launch256s(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
-  const int tiles_m = (a.M + 255) / 256;
+  const int tiles_m = (a.M + 64 * MI - 1) / (64 * MI);
   static const int gm256 = getenv("MMT_GM256") ? atoi(getenv("MMT_GM256")) : 4;   // tuning: super-tile height
   a.gm = tiles_m < gm256 ? tiles_m : gm256;
-  hipLaunchKernelGGL(gemm256s_kernel<EPI>, dim3(tiles_m * (a.N / 256), 1, a.groups), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((gemm256s_kernel<EPI, MI>), dim3(tiles_m * (a.N / 256), 1, a.groups), dim3(512), 0, s, a);
 }
 
-static bool launch256s_epi(const GemmArgs& a, int epi, hipStream_t s) {
+// t320: the 320 x 256 tiles (16-bit epilogues; false if the epilogue has none)
+static bool launch256s_epi(const GemmArgs& a, int epi, hipStream_t s, bool t320 = false) {
   if (a.N % 256 || a.K % 32 || a.K < 64 || a.amode != A_DENSE) return false;
+  if (t320) {
+    switch (epi) {
+      case EPI_BF16: return launch256s<EPI_BF16, 5>(a, s), true;
+      case EPI_GELU_BF16: return launch256s<EPI_GELU_BF16, 5>(a, s), true;
+      default: return false;
+    }
+  }
   switch (epi) {
-    case EPI_BF16: return launch256s<EPI_BF16>(a, s), true;
-    case EPI_GELU_BF16: return launch256s<EPI_GELU_BF16>(a, s), true;
-    case EPI_RESID_F32: return launch256s<EPI_RESID_F32>(a, s), true;
-    case EPI_F32: return launch256s<EPI_F32>(a, s), true;
-    case EPI_POS_F32: return launch256s<EPI_POS_F32>(a, s), true;
+    case EPI_BF16: return launch256s<EPI_BF16, 4>(a, s), true;
+    case EPI_GELU_BF16: return launch256s<EPI_GELU_BF16, 4>(a, s), true;
+    case EPI_RESID_F32: return launch256s<EPI_RESID_F32, 4>(a, s), true;
+    case EPI_F32: return launch256s<EPI_F32, 4>(a, s), true;
+    case EPI_POS_F32: return launch256s<EPI_POS_F32, 4>(a, s), true;
     default: return false;
   }
 }
@@ -1760,19 +1759,8 @@ static void launch_splitk(const GemmArgs& a0, int epi, int ks, hipStream_t s) {
     g_last_ks = ks;
     return;
   }
-  // MMT_SK_INLAUNCH (tuning): the tile's last slice combines in-launch -- 1: write-through slabs, 2: plain
-  // slabs behind agent-scope release / acquire.  Both give the separate reduce's bits and both measured slower
-  // at one sequence (825 -> 749 / 673 frames/s, tests/sk_ab.sh): ~60 reducing workgroups read their slabs
-  // serially at the tail, where the reduce launch spreads the same bytes over every CU
-  static const int inlaunch = getenv("MMT_SK_INLAUNCH") ? atoi(getenv("MMT_SK_INLAUNCH")) : 0;
-  if (inlaunch > 0 && tiles_m * (a.N / BN) * a.groups <= kSkCounters) {
-    a.sk_cnt = reinterpret_cast<unsigned*>(a.ws + a.ws_elems - kSkCounters);
-    a.sk_epi = epi;
-    a.sk_sc1 = inlaunch == 1 ? 1 : 0;
-  }
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WMW, WNW, EPI_PARTIAL, AM, SPLIT, ST>), dim3(tiles_m * (a.N / BN), ks, a.groups),
                      dim3(WMW * WNW * 64), 0, s, a);
-  if (a.sk_cnt) return;
   const dim3 rg((unsigned)(((int64_t)a.M * a.N / 4 + 255) / 256), 1, a.groups);
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((splitk_reduce_kernel<EPI_BF16, SPLIT>), rg, dim3(256), 0, s, a); break;
@@ -1836,7 +1824,22 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
       const int r192 = (conc * ((a.M + 127) / 128) * (a.N / 192) + slots - 1) / slots;
       if (r256 >= 2 && r192 * 375 * t192w < r256 * 100000) return launch_cfg<128, 192, 4, 2, true, 2, 64>(a, epi, s);
     }
-    if (a.N >= 2048 && (a.M + 255) / 256 * (a.N / 256) * a.groups >= t256_min && launch256s_epi(a, epi, s)) return;
+    // 320 x 256 tiles where they take fewer rounds of the one-workgroup-per-CU slots than 256 x 256 ones by more than
+    // their 1.25x work per tile, counting the concurrent stream part (qkv of the 244-token layers, fc1 of the
+    // 190-token ones at 2 x 16 sequences: two rounds -> one).  MMT_T320: 0 never, 1 the round rule, 2 always (tuning)
+    static const int t320 = getenv("MMT_T320") ? atoi(getenv("MMT_T320")) : 1;
+    bool use320 = false;
+    if (t320 && a.groups == 1 && (epi == EPI_BF16 || epi == EPI_GELU_BF16)) {
+      const int conc = a.conc > 1 ? a.conc : 1, slots = num_cus();
+      const int r256 = (conc * ((a.M + 255) / 256) * (a.N / 256) + slots - 1) / slots;
+      const int r320 = (conc * ((a.M + 319) / 320) * (a.N / 256) + slots - 1) / slots;
+      use320 = t320 == 2 || 5 * r320 < 4 * r256;
+    }
+    const bool forced = g_force_cfg == 320 || g_force_cfg == 256;   // tests: pin the tile (any tile count)
+    if (forced) use320 = g_force_cfg == 320 && (epi == EPI_BF16 || epi == EPI_GELU_BF16);
+    if (a.N >= 2048 && ((a.M + 255) / 256 * (a.N / 256) * a.groups >= t256_min || forced) &&
+        launch256s_epi(a, epi, s, use320))
+      return;
   }
   if constexpr (!SPLIT) {
     if (g_force_cfg >= 0 && a.amode == A_DENSE) {
@@ -1936,7 +1939,7 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
         int best = 1;
         double bcost = (double)((tiles + slots - 1) / slots);
         for (int ks = 2; ks <= (sk128 > 1 ? sk128 : kMaxDeferKs); ++ks) {
-          if (nk / ks < 8 || (int64_t)ks * a.M * a.N > a.ws_elems - kSkCounters) break;
+          if (nk / ks < 8 || (int64_t)ks * a.M * a.N > a.ws_elems) break;
           const double cost = (double)((tiles * ks + slots - 1) / slots) / ks;
           if (cost < 0.9 * bcost) {
             best = ks;
@@ -1969,11 +1972,11 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // loads -- at one sequence these GEMMs are bound by what a CU can take in (one tile per CU, ~400 KB of
     // hi + lo operands at ~45 GB/s), 906 -> 929 frames/s (tests/few_w8_ab.sh); MMT_FEW_W4: 4 waves (tuning)
     static const bool few_w8 = getenv("MMT_FEW_W4") == nullptr;
-    if (a.ws && a.ws_elems > kSkCounters && tiles < sk_tiles && nk >= 2 * sk_minkt) {
+    if (a.ws && a.ws_elems > 0 && tiles < sk_tiles && nk >= 2 * sk_minkt) {
       int ks = sk_ceil ? (sk_target + tiles - 1) / tiles : sk_target / tiles;
       ks = ks < nk / sk_minkt ? ks : nk / sk_minkt;
       ks = ks < sk_max ? ks : sk_max;
-      while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems - kSkCounters) --ks;   // tickets at the end
+      while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems) --ks;
       if (ks > 1) {
         // f16x3: a 3-deep ring (96 KB of LDS) beat 4-deep at one sequence (tests/sweep_ring_b1.sh)
         constexpr int SKST = SPLIT ? 3 : 4;

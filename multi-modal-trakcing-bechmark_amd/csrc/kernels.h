@@ -46,11 +46,6 @@ struct GemmArgs {
   float* ws;        // split-K workspace ([groups][ksplit][M][N] fp32) or null: never split
   int64_t ws_elems; // its capacity in floats
   const bf16_t* zero;   // unused by the buffer-load kernels (kept for ABI stability of the struct)
-  // (set by the launcher) in-launch split-K combine: per-tile arrival tickets (the workspace's last
-  // kSkCounters words, zero between launches) and the final epilogue the last arriving slice applies
-  unsigned* sk_cnt;
-  int sk_epi;
-  int sk_sc1;       // 1: the slabs move write-through (sc1 stores and loads), no release / acquire fences
   int defer_reduce; // EPI_RESID_F32, one group: a split-K run leaves its partial slabs for the consumer (gemm())
   int conc;         // launches of this shape running at once on the chip (the engine's stream parts; 0 / 1: alone)
 };
@@ -65,7 +60,6 @@ struct RowReduce {
   float inv;              // f16x3 1 / (s_A s_W) (1 in bf16 mode)
   const float* bias;      // [768]
 };
-constexpr int kSkCounters = 1024;
 
 // returns the K splits it ran: 1, or (a.defer_reduce and few tiles) ks > 1 with the raw fp32 partial slabs left
 // in a.ws ([ks][M][N], one group) for the consumer to combine (RowReduce below) instead of a reduce launch
@@ -153,7 +147,6 @@ struct LnPromptArgs {
 void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s);
 // a deep layer's prompt_reduce (pa) and prompt_expand_ln (la, mode 2) as one launch whose blocks meet at a
 // per-sequence barrier (bar: [B][32] ints, zero at allocation, left zero); false: not taken (the caller launches the two)
-bool prompt_ln_fused(const PromptArgs& pa, const LnPromptArgs& la, int* bar, hipStream_t s);
 
 // ---------------------------------------------------------------- candidate elimination
 struct CEArgs {

@@ -601,167 +601,6 @@ void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((ln_prompt_kernel<2, 1>), grid, dim3(TOK_THREADS), va_bytes, s, a);
 }
 
-// ------------------------------------------------------------------ deep prompt block + LN1, one launch
-// A deep layer's prompt reduce (prompt_reduce_deep_kernel) and LN1 with the prompt residual (ln_prompt_kernel,
-// mode 2) are one row kernel but for the fovea statistics between them: LN1 of any row needs the softmax statistics
-// of this layer's a8 over all slots of its sequence.  Here the blocks of a sequence meet at a barrier between the
-// two halves instead of a launch boundary, and each wave keeps its slot's residual row in registers across it: the
-// slot's compact row (slot2pos and gidx are inverse maps) is the row LN1 finishes, so X is read once and written
-// once (unfused: read twice, written twice when a split-K update is pending).  The arithmetic is deep_slot +
-// ln_prompt_row, as the two kernels inline it: the same bits.
-//
-// The barrier (seq_barrier): an arrival counter and a generation word per sequence, the last arrival resetting
-// the counter and advancing the generation (agent-scope release / acquire: the a8 / c8 stores of every block are
-// visible to every other after it, whichever XCD wrote them).  It needs every block of an unfinished sequence to
-// be resident or dispatchable: blocks are dispatched in order and a sequence has at most 128 blocks of 8 waves,
-// ~45 KB of LDS, so the lowest unfinished sequence's blocks always fit beside the (finishing) ones before it.  The
-// spin is bounded: a broken invariant ends the kernel with a flag (bar[8] of the sequence) instead of a hang.
-constexpr int kBarSpin = 1 << 22;
-constexpr int kBarStride = 32;   // ints per sequence: counter [0], timeout flag [8], generation [16]
-__device__ __forceinline__ void seq_barrier(int* w, int nblocks) {
-  const int g = __hip_atomic_load(w + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int old = __hip_atomic_fetch_add(w, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  if (old == nblocks - 1) {
-    __hip_atomic_store(w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(w + 16, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the last arrival reads the others' rows too
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-  }
-  for (int k = 0; __hip_atomic_load(w + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g; ++k) {
-    if (k >= kBarSpin) {
-      __hip_atomic_store(w + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the invalidate done before the block's barrier releases
-}
-
-template <bool RR, int R>
-__global__ __launch_bounds__(TOK_THREADS) void prompt_ln_kernel(const PromptArgs a, const LnPromptArgs la, int* bar) {
-  __shared__ float fold[FOLD_N];
-  __shared__ __attribute__((aligned(16))) float W[8 * C768];     // conv0_0 (LN_A folded)
-  __shared__ __attribute__((aligned(16))) float W1t[8 * C768];   // conv1x1 (its own copy: held in registers across
-                                                                 // the barrier, the fill went to scratch)
-  __shared__ __attribute__((aligned(16))) float cst[3 * C768];   // conv1x1 bias, norm1 weight, norm1 bias
-  extern __shared__ __attribute__((aligned(16))) float va[];    // [L][8]
-  __shared__ float red[64], st[32];
-  const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, b = blockIdx.y;
-  // ---- every global load of the first half, then the second half's weights
-  const bool pre = a.fstat_p != nullptr;
-  FoveaStage fsg;
-  if (!pre) fsg = fovea_stage(a.a8p + (int64_t)b * L * 8, L);
-  const float stv = pre && threadIdx.x < 32 ? a.fstat_p[b * 32 + threadIdx.x] : 0.f;
-  int sv[R], posv[R];
-  int64_t xrowv[R];
-  Row12 xv[R];
-  float apv[R], cpv[R];
-#pragma unroll
-  for (int rr = 0; rr < R; ++rr) {
-    const int s = (blockIdx.x * R + rr) * TOK_ROWS + (threadIdx.x >> 6);
-    const int pos = s >= L ? -1 : s < a.Lz ? s : a.slot2pos[b * a.Lx + (s - a.Lz)];   // wave-uniform
-    sv[rr] = s;
-    posv[rr] = pos;
-    xrowv[rr] = (int64_t)b * a.srcA_rows + max(pos, 0);
-    xv[rr] = load_row(a.srcA + xrowv[rr] * C768, lane);
-    const int64_t srow = ((int64_t)b * L + min(s, L - 1)) * 8;
-    apv[rr] = lane < 8 ? a.a8p[srow + lane] : 0.f;
-    cpv[rr] = lane < 8 ? a.c8p[srow + lane] : 0.f;
-  }
-  constexpr int WV = 8 * C768 / 4 / TOK_THREADS;
-  float4 wst[WV], w1v[WV];   // (w1v: stored to W1t with the first half's fills)
-#pragma unroll
-  for (int k = 0; k < WV; ++k) wst[k] = reinterpret_cast<const float4*>(a.w00)[threadIdx.x + TOK_THREADS * k];
-  const float fo = threadIdx.x < FOLD_N ? a.fold[threadIdx.x] : 0.f;
-  const float ba = lane < 8 ? a.b00[lane] : 0.f;
-#pragma unroll
-  for (int k = 0; k < WV; ++k) w1v[k] = reinterpret_cast<const float4*>(la.w1)[threadIdx.x + TOK_THREADS * k];
-  float cs[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const int e = threadIdx.x + TOK_THREADS * k;
-    cs[k] = e < C768 ? la.b1[e] : e < 2 * C768 ? la.w[e - C768] : e < 3 * C768 ? la.b[e - 2 * C768] : 0.f;
-  }
-#pragma unroll
-  for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W)[threadIdx.x + TOK_THREADS * k] = wst[k];
-#pragma unroll
-  for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W1t)[threadIdx.x + TOK_THREADS * k] = w1v[k];
-  if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const int e = threadIdx.x + TOK_THREADS * k;
-    if (e < 3 * C768) cst[e] = cs[k];
-  }
-  if (pre) {
-    if (threadIdx.x < 32) st[threadIdx.x] = stv;
-    __syncthreads();
-  } else {
-    fovea_stats(fsg, a.Lz, a.Lx, a.smooth_p, va, red, st);   // ends with a barrier
-  }
-  // ---- first half: a8 / c8 of the wave's slots (prompt_reduce_deep_kernel)
-  float avv[R] = {}, cvv[R] = {};
-#pragma unroll
-  for (int rr = 0; rr < R; ++rr) {
-    const int s = sv[rr], pos = posv[rr];
-    if (s >= L) break;   // wave-uniform
-    if (RR && pos >= 0 && a.rr.ws) xv[rr] = apply_reduce(xv[rr], a.rr, xrowv[rr], lane);   // kept, not stored
-    const float2 ac = deep_slot(xv[rr], pos >= 0, s < a.Lz ? 0 : 1, apv[rr], cpv[rr], st, fold, W, ba, a.smooth_p,
-                                lane);
-    avv[rr] = ac.x;
-    cvv[rr] = ac.y;
-    if (lane < 8) {
-      const int64_t row = (int64_t)b * L + s;
-      a.a8[row * 8 + lane] = ac.x;
-      a.c8[row * 8 + lane] = ac.y;
-    }
-  }
-  // ---- the sequence's blocks meet.  Every wave waits for its a8 / c8 stores to land in this XCD's L2 (the
-  // workgroup barrier alone does not wait for stores on gfx950), then thread 0's agent-scope release writes the L2
-  // back once for the block and its acquire after the wait invalidates this CU's and XCD's stale lines once (a
-  // __threadfence in every wave, 8 write-backs and invalidates per block, cost 10 us per launch, r5_run18.sh)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) seq_barrier(bar + (int64_t)b * kBarStride, gridDim.x);
-  __syncthreads();
-  // ---- second half: this layer's fovea statistics, LN1 of the wave's compact rows (ln_prompt_kernel, mode 2)
-  const FoveaStage fsg2 = fovea_stage(la.a8 + (int64_t)b * L * 8, L);
-  fovea_stats(fsg2, a.Lz, a.Lx, la.smooth, va, red, st);   // ends with a barrier
-  if (la.fstat && blockIdx.x == 0 && threadIdx.x < 32) la.fstat[b * 32 + threadIdx.x] = st[threadIdx.x];
-#pragma unroll
-  for (int rr = 0; rr < R; ++rr) {
-    if (sv[rr] >= L) break;
-    if (posv[rr] < 0) continue;   // a pruned slot has no row
-    ln_prompt_row<2>(xv[rr], xv[rr], avv[rr], cvv[rr], sv[rr] < a.Lz ? 0 : 1, st, W1t, cst, la,
-                     (int64_t)b * la.rows_per_seq + posv[rr], lane);
-  }
-}
-
-bool prompt_ln_fused(const PromptArgs& pa, const LnPromptArgs& la, int* bar, hipStream_t s) {
-  // MMT_PROMPT_FUSED (opt-in): the largest batch that takes the fused launch (default 0, never; read per call, so a
-  // test can compare the two paths in one process).  Measured slower: at one sequence 15.4 us per launch against
-  // 6.7 + 6.3 us for the two kernels (1 084 against 1 118 frames/s), at 32 sequences 6 267 against 6 444 -- the
-  // barrier's chain (L2 write-back, device atomic, polling past the L2, invalidate, a8 re-read) is ~4 us, more
-  // than the launch boundary it replaces (profiles/r05_ab_prompt_ln_fused.txt)
-  const char* env = getenv("MMT_PROMPT_FUSED");
-  const int maxb = env ? atoi(env) : 0;
-  const int L = pa.Lz + pa.Lx;
-  if (!bar || pa.layer == 0 || la.mode != 2 || pa.B > maxb || L > FOVEA_MAX_TOKENS || la.a8 != pa.a8 ||
-      la.c8 != pa.c8 || la.X != pa.srcA || la.rows_per_seq != pa.srcA_rows)
-    return false;
-  const int R = pa.rr.ws ? 1 : tok_rows_per_wave(pa.B);
-  const dim3 grid((L + TOK_ROWS * R - 1) / (TOK_ROWS * R), pa.B);
-  const size_t va_bytes = (size_t)L * 8 * sizeof(float);
-  if (pa.rr.ws)
-    hipLaunchKernelGGL((prompt_ln_kernel<true, 1>), grid, dim3(TOK_THREADS), va_bytes, s, pa, la, bar);
-  else if (R == 2)
-    hipLaunchKernelGGL((prompt_ln_kernel<false, 2>), grid, dim3(TOK_THREADS), va_bytes, s, pa, la, bar);
-  else
-    hipLaunchKernelGGL((prompt_ln_kernel<false, 1>), grid, dim3(TOK_THREADS), va_bytes, s, pa, la, bar);
-  return true;
-}
-
 // ------------------------------------------------------------------ candidate elimination
 // attn_blocks.py:37-73: score = mean over heads of the CTR_POINT template row of P over the
 // search keys, sort descending, keep ceil(ratio * Ls); ties broken by the lower index.

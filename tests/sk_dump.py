@@ -1,7 +1,7 @@
-"""Helper of test_gpu_kernels.py::test_splitk_combine_bitwise (run as a child process, GPU only): split-K
+"""Helper of test_gpu_kernels.py::test_ring_copy_bitwise (run as a child process, GPU only): split-K
 GEMM outputs through mmt_op_gemm (bf16 operands) and one parity-mode sequence tracked by the engine (its
-few-tile f16x3 GEMMs split K), saved to an .npz.  The test runs it with the separate reduce launch and with
-the in-launch combines (MMT_SK_INLAUNCH=1 / 2) and compares the files bit for bit.
+few-tile f16x3 GEMMs split K), saved to an .npz.  The test runs it with the ring hand-off and with copy launches
+(MMT_RING_COPY=1) and compares the files bit for bit.
 
 usage: python tests/sk_dump.py <out.npz>"""
 import os

@@ -114,6 +114,48 @@ def test_gemm_f16x3_vs_fp64(lib, M, N, K, epi):
     assert torch.isfinite(out).all()
 
 
+@pytest.mark.parametrize("M,N,K,epi", [
+    (7808, 2304, 768, 0),     # qkv after the first CE (244 tokens): the rule picks 320 x 256 (225 tiles, one round)
+    (6080, 3072, 768, 1),     # fc1 after the second CE (190 tokens): 320 x 256 by the rule (228 tiles)
+    (10240, 3072, 768, 1),    # forced: whole tiles, 32 rows per M tile
+    (4896, 2304, 768, 0),     # forced: M % 320 = 96 (the last tile's second half-tile empty)
+    (700, 3072, 128, 1),      # forced: K = 128 (four K-steps: the tail-wait path only), M % 320 = 60
+    (330, 2304, 64, 0),       # forced: K = 64 (two K-steps), M = 320 + 10
+])
+def test_gemm_f16x3_t320(lib, M, N, K, epi):
+    """The 320 x 256 eight-phase tile (gemm256s_kernel<EPI, 5>) against fp64, and bit-identical to the 256 x 256 tile:
+    both accumulate every output over the same K order, so only the tiling differs (attn.py:17-19 qkv, timm Mlp fc1)."""
+    g = torch.Generator(device="cuda").manual_seed(M + 7 * N + K + epi)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g) * (0.5 / math.sqrt(K))
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    sa, sw = range_scale(A), range_scale(W)
+    Ah, Al, A64 = split(A, sa)
+    Wh, Wl, W64 = split(W, sw)
+    ref = A64 @ W64.t() + bias.double()
+    y = F.gelu(ref) if epi == 1 else ref
+    so = range_scale(y.float())
+    outs = []
+    try:
+        for cfg in (320, 256):
+            lib.mmt_gemm_force_config(cfg)
+            C = torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16)
+            Cl = torch.full_like(C, float("nan"))
+            _gemm(lib, Ah, Al, Wh, Wl, bias, C, Cl, 1.0 / (sa * sw), so, epi)
+            outs.append((C, Cl))
+    finally:
+        lib.mmt_gemm_force_config(-1)
+    (C, Cl), (C2, Cl2) = outs
+    out = (C.double() + Cl.double()) / so
+    err = float((out - y).abs().max())
+    tol = 1e-5 * float(y.abs().max())
+    print(f"f16x3 gemm 320x256 M={M} N={N} K={K} epi={epi}: max|err| {err:.3e} (tol {tol:.3e})")
+    assert torch.isfinite(out).all()
+    assert err <= tol
+    assert torch.equal(C.view(torch.int16), C2.view(torch.int16)) and torch.equal(Cl.view(torch.int16),
+                                                                                  Cl2.view(torch.int16))
+
+
 @pytest.mark.parametrize("B,N", [(32, 320), (16, 320), (16, 244), (16, 153), (16, 720), (12, 190), (1, 320),
                                  (1, 153), (2, 244), (1, 720)])
 def test_attention_f16x3_vs_fp64(lib, B, N):

@@ -58,32 +58,27 @@ def test_gemm_dense(lib, M, N, K, epi):
         torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-3)
 
 
-def test_splitk_combine_bitwise(tmp_path):
-    """The in-launch split-K combines (the tile's last-arriving slice reduces the slabs, gemm.hip sk_combine;
-    MMT_SK_INLAUNCH=1 write-through, =2 release / acquire) and the default separate reduce launch give the same
-    bits: op-level GEMMs and a parity-mode sequence whose few-tile GEMMs split K (tests/sk_dump.py, one child
-    process each).  So does the engine with copy launches for the frame parameters and results
-    (MMT_RING_COPY=1) instead of the ring hand-off, including device frames whose size and address change
-    between launches that reuse a ring entry."""
+def test_ring_copy_bitwise(tmp_path):
+    """The engine with copy launches for the frame parameters and results (MMT_RING_COPY=1) instead of the ring
+    hand-off gives the same bits, including device frames whose size and address change between launches that reuse a
+    ring entry: op-level GEMMs and a parity-mode sequence whose few-tile GEMMs split K (tests/sk_dump.py, one child
+    process each)."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    modes = (("separate", {}), ("sc1", {"MMT_SK_INLAUNCH": "1"}), ("fenced", {"MMT_SK_INLAUNCH": "2"}),
-             ("ringcopy", {"MMT_RING_COPY": "1"}))
-    for mode, extra in modes:
-        env = {k: v for k, v in os.environ.items() if k not in ("MMT_SK_INLAUNCH", "MMT_RING_COPY")}
+    for mode, extra in (("ring", {}), ("ringcopy", {"MMT_RING_COPY": "1"})):
+        env = {k: v for k, v in os.environ.items() if k != "MMT_RING_COPY"}
         env.update(extra)
         path = str(tmp_path / f"{mode}.npz")
         r = subprocess.run([sys.executable, os.path.join(here, "sk_dump.py"), path], env=env, capture_output=True,
                            text=True, timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr
         res[mode] = np.load(path)
-    for mode in ("sc1", "fenced", "ringcopy"):
-        assert sorted(res[mode].files) == sorted(res["separate"].files)
-        for k in res[mode].files:
-            np.testing.assert_array_equal(res[mode][k], res["separate"][k], err_msg=f"{mode} {k}")
+    assert sorted(res["ringcopy"].files) == sorted(res["ring"].files)
+    for k in res["ring"].files:
+        np.testing.assert_array_equal(res["ringcopy"][k], res["ring"][k], err_msg=f"ringcopy {k}")
 
 
 @pytest.mark.parametrize("M,N,K", [(4896, 3072, 768), (10240, 2304, 768), (300, 256, 128), (7808, 768, 3072),

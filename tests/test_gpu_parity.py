@@ -418,30 +418,3 @@ def test_ostrack384_tracker_sequence_matches_reference():
         assert max(dsc) < 1e-3
     finally:
         eng.close()
-
-
-@pytest.mark.parametrize("precision,n,maxb", [("fp32", 1, "7"), ("bf16", 1, "7"), ("fp32", 3, "7"),
-                                              ("fp32", 8, "64")])
-def test_fused_prompt_ln_bitwise(precision, n, maxb, monkeypatch):
-    """The fused deep prompt + LN1 kernel (tokens.hip prompt_ln_kernel: the sequence's blocks meet at a barrier
-    instead of a launch boundary) gives the bits of prompt_reduce_deep_kernel + ln_prompt_kernel: final features,
-    score maps and boxes, one sequence (the split-K update of X applied in it) and batches of one / two slots per
-    wave (MMT_PROMPT_FUSED=0 turns it off)."""
-    sd = synth.make_state_dict(0, **SHAPES["deep_rgbt"])
-    seqs = [synth.make_frames(500 + i, 4, 360, 480, 6, box=(150.0 + 20 * i, 120.0, 40.0 + 3 * i, 30.0))
-            for i in range(n)]
-    res = {}
-    for mode in ("0", maxb):
-        monkeypatch.setenv("MMT_PROMPT_FUSED", mode)
-        eng = Engine(EngineConfig(max_batch=n, debug_outputs=True, use_graphs=True, precision=precision), sd)
-        for i, (fr, gt) in enumerate(seqs):
-            eng.initialize(i, fr[0], list(gt[0]))
-        out = []
-        for t in range(1, 4):
-            boxes, scores = eng.track_batch(0, [seqs[i][0][t] for i in range(n)])
-            out += [np.asarray(boxes), np.asarray(scores)]
-            out += [eng.debug("feat", bi) for bi in (0, n - 1)] + [eng.debug("maps", bi) for bi in (0, n - 1)]
-        res[mode] = out
-        eng.close()
-    for a, b in zip(res["0"], res[maxb]):
-        np.testing.assert_array_equal(a, b)
