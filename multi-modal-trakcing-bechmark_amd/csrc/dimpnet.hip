@@ -48,7 +48,10 @@ struct ConvArgs {
 // otherwise (the 3-channel stem) each k is decoded separately.
 // W4 (the 3-channel stem, MMT_CONV_W4): weights padded to 4 channels per tap, a K-tile is 4 taps and a
 // thread loads one tap (3 pixel values + 0, one float4 of weights) -- no per-element index decode
-template <bool FAST, int BK, bool W4 = false>
+#ifndef CONV_F32_NACC
+#define CONV_F32_NACC 4
+#endif
+template <bool FAST, int BK, bool W4 = false, int NACC = CONV_F32_NACC>
 __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
   static_assert(!W4 || (!FAST && BK == 16), "W4: BK 16");
   constexpr int VPT = BK / 4;   // K values per thread per K-tile (A and W each)
@@ -134,17 +137,21 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
     }
   };
 
-  f32x4v acc[2][2];
+  // NACC accumulator sets, K-tile kt into set kt % NACC, summed pairwise after the loop: each MFMA adds its 4
+  // products to the accumulator one rounding at a time (an fmaf chain), so one set is a K-long sequential fp32 sum
+  f32x4v acc[NACC][2][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int s = 0; s < NACC; ++s)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[s][i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
   load(0);
   stash();
   __syncthreads();
   const int li = lane & 15, lk = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
+  auto ktile = [&](int kt, f32x4v (&A)[2][2]) {
     if (kt + 1 < nk) load(kt + 1);
     if constexpr (KV) {
       f32x4v av[2][VPT / 4], bv[2][VPT / 4];
@@ -164,28 +171,41 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
         for (int p = 0; p < 2; ++p)
 #pragma unroll
           for (int c = 0; c < 2; ++c)
-            acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[c][k4 / 4][k4 % 4], av[p][k4 / 4][k4 % 4], acc[p][c], 0,
-                                                             0, 0);
-    } else
+            A[p][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[c][k4 / 4][k4 % 4], av[p][k4 / 4][k4 % 4], A[p][c], 0, 0, 0);
+    } else {
 #pragma unroll
-    for (int k4 = 0; k4 < BK / 4; ++k4) {
-      const int kk = k4 * 4 + lk;
-      float fa[2], fb[2];
+      for (int k4 = 0; k4 < BK / 4; ++k4) {
+        const int kk = k4 * 4 + lk;
+        float fa[2], fb[2];
 #pragma unroll
-      for (int p = 0; p < 2; ++p) fa[p] = sA[kk][wr * 32 + p * 16 + li];
+        for (int p = 0; p < 2; ++p) fa[p] = sA[kk][wr * 32 + p * 16 + li];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) fb[c] = sB[kk][wc * 32 + c * 16 + li];
+        for (int c = 0; c < 2; ++c) fb[c] = sB[kk][wc * 32 + c * 16 + li];
 #pragma unroll
-      for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[c], fa[p], acc[p][c], 0, 0, 0);
+          for (int c = 0; c < 2; ++c) A[p][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[c], fa[p], A[p][c], 0, 0, 0);
+      }
     }
     __syncthreads();
     if (kt + 1 < nk) {
       stash();
       __syncthreads();
     }
+  };
+  for (int kt = 0; kt < nk; kt += NACC) {
+#pragma unroll
+    for (int s = 0; s < NACC; ++s)
+      if (kt + s < nk) ktile(kt + s, acc[s]);
   }
+#pragma unroll
+  for (int w = 1; w < NACC; w *= 2)   // pairwise: (s0 + s1) + (s2 + s3)
+#pragma unroll
+    for (int s = 0; s + w < NACC; s += 2 * w)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[s][p][c] += acc[s + w][p][c];
   // lane holds channels n0 + wc*32 + c*16 + 4*lk + (0..3) of pixel m0 + wr*32 + p*16 + li
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -194,7 +214,7 @@ __global__ __launch_bounds__(256) void conv_f32_kernel(const ConvArgs a) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int no = n0 + wc * 32 + c * 16 + 4 * lk;
-      f32x4v v = acc[p][c];
+      f32x4v v = acc[0][p][c];
       if (a.bias) v += *reinterpret_cast<const f32x4v*>(a.bias + no);
       if (a.resid) v += *reinterpret_cast<const f32x4v*>(a.resid + (int64_t)mo * a.ldy + no);
       if (a.flags & MMT_CONV_RELU)
@@ -322,7 +342,11 @@ __global__ __launch_bounds__(256) void l2norm_sumsq_kernel(const float* __restri
 __global__ __launch_bounds__(256) void l2norm_scale_kernel(const float* __restrict__ x, int HW, int C, float scale,
                                                            float eps, const float* __restrict__ ws,
                                                            float* __restrict__ y_nhwc, float* __restrict__ y_nchw) {
-  __shared__ float tile[kL2Pix * kL2MaxC];
+  // pixel rows padded by 4 floats: the transposed read (16 pixels of one channel per 16 lanes) strides C + 4 words, so
+  // a 32-lane group covers 32 distinct banks (unpadded, C % 64 == 0 put all 16 pixels on one bank: 88 % of the
+  // kernel's LDS cycles were conflicts, r05_pmc_mfma_dimp_b1.txt); the float4 stores stay 16-B aligned
+  constexpr int kPad = 4;
+  __shared__ __attribute__((aligned(16))) float tile[kL2Pix * (kL2MaxC + kPad)];
   __shared__ float fsh;
   const int n = blockIdx.y, p0 = blockIdx.x * kL2Pix, np = min(kL2Pix, HW - p0);
   if (threadIdx.x == 0) {
@@ -339,14 +363,17 @@ __global__ __launch_bounds__(256) void l2norm_scale_kernel(const float* __restri
     float4 v = xs[i];
     v.x *= f; v.y *= f; v.z *= f; v.w *= f;
     if (y_nhwc) reinterpret_cast<float4*>(y_nhwc + base)[i] = v;
-    if (y_nchw) *reinterpret_cast<float4*>(&tile[i * 4]) = v;
+    if (y_nchw) {
+      const int p = (i * 4) / C, c = i * 4 - p * C;
+      *reinterpret_cast<float4*>(&tile[p * (C + kPad) + c]) = v;
+    }
   }
   if (!y_nchw) return;
   __syncthreads();
   float* yo = y_nchw + (int64_t)n * C * HW + p0;
   for (int i = threadIdx.x; i < kL2Pix * C; i += 256) {
     const int c = i / kL2Pix, p = i - c * kL2Pix;
-    if (p < np) yo[(int64_t)c * HW + p] = tile[p * C + c];
+    if (p < np) yo[(int64_t)c * HW + p] = tile[p * (C + kPad) + c];
   }
 }
 

@@ -932,7 +932,9 @@ void enqueue_forward(mmt_engine* e, int b0, int r0, int n, hipStream_t s, int pa
     aa.ce_query = ce ? c.ce_template_index : -1;
     aa.ce_lens_t = Lz;
     aa.ce_prob = q_ce_prob;
-    probe_begin(e, s, "attn", 4.0 * n * HEADS * (double)Na * Na * 64, (double)n * Na * 4 * C * 2);
+    // algorithmic bytes: Q, K, V in and O out, 2 B per element, twice in the parity mode (hi + lo planes: 12 288 B per
+    // token row), as the GEMM classes count their operands
+    probe_begin(e, s, "attn", 4.0 * n * HEADS * (double)Na * Na * 64, (double)n * Na * 4 * C * 2 * (e->split ? 2 : 1));
     attention(aa, s);
     probe_end(e, s, "attn");
     pend = run_resid_gemm(

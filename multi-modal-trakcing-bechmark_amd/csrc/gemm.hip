@@ -1406,6 +1406,8 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
       Bl[jj] = *reinterpret_cast<const bf16x8*>(S + 4096 + swzk<32>(row, c));
     }
   };
+  // the phase's MFMAs at priority 1 (per-phase flips: 6 279 frames/s against 6 140 for waves 4-7 at a static priority 1
+  // and 6 140 for no priorities, profiles/r06_ab_256s_prio.txt)
   auto mma = [&](f32x4 (&C)[MI][2], const bf16x8 (&Bh)[2], const bf16x8 (&Bl)[2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -2001,6 +2003,14 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
 
 int gemm(const GemmArgs& a, int epi, hipStream_t s) {
   g_last_ks = 1;
+  // the f16x3 16-bit epilogues (gemm_kernel's staged split epilogue, gemm256s) always store a lo plane: a caller
+  // without one is a programming error, not a bf16 fallback
+  if (a.split && epi_is_bf16(epi))
+    for (int i = 0; i < a.groups; ++i)
+      if (!a.g[i].C_lo) {
+        fprintf(stderr, "mmt: f16x3 GEMM with a 16-bit epilogue needs C_lo (group %d)\n", i);
+        abort();
+      }
   if (a.split)
     gemm_dispatch<true>(a, epi, s);
   else

@@ -46,27 +46,38 @@ __device__ void geometry_of(const double box[4], double factor, int out_sz, Crop
 // done here -- every workgroup derives its sequence's crop from the device state (and the frame from the host ring
 // entry) itself; workgroup 0 of each sequence stores the parameters, rf / err and the token index reset, and
 // records the ring entry for decode, which advances the counter (g.ring_advance) -- one launch fewer
+// (fused mode: the geometry fields x1, y1, crop_sz of params[b] are written by workgroup 0 and read by nobody in this
+// launch -- every workgroup forms its own -- and the frame fields are only read: from the ring entry, or, without the
+// ring, from params[b], where the host put them and nothing in this launch writes them)
 template <bool FUSED_GEOM>
 __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
   const int b = blockIdx.y;
-  CropParam p = a.params[b];
+  CropParam p;
   if constexpr (FUSED_GEOM) {
     const GeomArgs& g = a.geom;
     const int e = g.use_ring ? *g.ring.ctr : 0;
-    if (g.use_ring) {
-      const CropParam h = g.ring.params[(int64_t)e * g.ring.pitch + b];
-      p.frame = h.frame;
-      p.stride = h.stride;
-      p.H = h.H;
-      p.W = h.W;
-      p.C = h.C;
-    }
+    const CropParam& h = g.use_ring ? g.ring.params[(int64_t)e * g.ring.pitch + b] : a.params[b];
+    p.frame = h.frame;
+    p.stride = h.stride;
+    p.H = h.H;
+    p.W = h.W;
+    p.C = h.C;
     double rf;
     int err;
     geometry_of(g.state[b].box, g.factor, a.out_sz, p, rf, err);
     if (blockIdx.x == 0) {
       if (threadIdx.x == 0) {
-        const_cast<CropParam*>(a.params)[b] = p;
+        CropParam* const dst = const_cast<CropParam*>(a.params) + b;
+        if (g.use_ring) {   // the frame fields too (decode and the host read params after the launch)
+          dst->frame = p.frame;
+          dst->stride = p.stride;
+          dst->H = p.H;
+          dst->W = p.W;
+          dst->C = p.C;
+        }
+        dst->x1 = p.x1;
+        dst->y1 = p.y1;
+        dst->crop_sz = p.crop_sz;
         g.state[b].rf = rf;
         g.state[b].err = err;
         if (g.use_ring && b == 0) *g.ring.cur = e;
@@ -77,6 +88,8 @@ __global__ __launch_bounds__(256) void crop_kernel(const CropArgs a) {
           g.slot2pos[b * g.Lx + j] = g.Lz + j;
         }
     }
+  } else {
+    p = a.params[b];
   }
   const int O = a.out_sz;
   const int idx = blockIdx.x * 256 + threadIdx.x;

@@ -184,13 +184,14 @@ def test_dimp_branches_match_reference(nets, precision, name):
             bar = max(bar0, confidence_bar(name, n))
         out = tr.track(frames[t])
         if t in thin:
-            try:
-                dconf.append(_check_frame(name, t, out, tr.debug_info["flag"], boxes[t], (conf[t], str(flags[t])),
-                                          bar))
-                passed.append(t)
-            except AssertionError as err:   # decided the other way: the states part here
-                stop = (t, str(err))
+            # decided the other way (flag or box): the states part here and the run stops; decided as the reference
+            # did, the confidence bar holds as on any other frame (a drift past it fails, it does not stop the run)
+            fl, ov = tr.debug_info["flag"], iou(out["target_bbox"], boxes[t])
+            if fl != str(flags[t]) or ov < 0.999:
+                stop = (t, f"flag {fl} (reference {flags[t]}), box IoU {ov:.4f}")
                 break
+            dconf.append(_check_frame(name, t, out, fl, boxes[t], (conf[t], str(flags[t])), bar))
+            passed.append(t)
         else:
             dconf.append(_check_frame(name, t, out, tr.debug_info["flag"], boxes[t], (conf[t], str(flags[t])), bar))
         if t == hn_frame:
@@ -199,8 +200,12 @@ def test_dimp_branches_match_reference(nets, precision, name):
     asserted = dict(zip(*np.unique(flags[1:last], return_counts=True)))
     print(f"{name} [{precision}]: frames 1..{last - 1} asserted {asserted} ({len(passed)} near-ties decided as the "
           f"reference did), max confidence rel. diff {max(dconf):.2e} (bar {bar0:.2e}, {bar:.2e} past a near-tie)"
-          + (f"; stopped at near-tie frame {stop[0]} (margin {margin[stop[0]]:.4f}, runner-up {runner[stop[0]]:.4f}):"
-             f" {stop[1][:120]}" if stop else ""))
+          + (f"; stopped at near-tie frame {stop[0]} (margin {margin[stop[0]]:.4f}, runner-up {runner[stop[0]]:.4f}"
+             f"{', its first near-tie' if stop[0] == thin[0] else ''}): {stop[1][:120]}" if stop else ""))
+    if precision == "fp32":
+        # the fp32 convolutions' four accumulator sets (dimpnet.hip CONV_F32_NACC) put the fp32 mode within 60 % of
+        # every derived bar (one set: up to 74 %, profiles/r05_dimp_branches_past_near_ties.txt)
+        assert max(dconf) <= 0.6 * bar0, (name, max(dconf), bar0)
     if thin:
         return
     close(tr.target_filter.cpu(), gd[p + "final_filter"], 1e-2)

@@ -76,6 +76,87 @@ def test_conv2d_f16x3_vs_fp64(N, C, H, W, Co, k, s, p):
     assert torch.equal(got3, got)
 
 
+def _dimp_layer_inputs():
+    """Every convolution of the RGB ResNet-50 to layer3 and the clf conv on the network's own activations: the fp64
+    forward of oracle/dimpnet.py (seeded synthetic weights, BN folded as the HIP path folds it) of a 288 x 288 patch
+    of a synthetic frame, each conv's fp64 input rounded to fp32.  Yields (name, x32, w32, stride, pad)."""
+    from mmtrack_amd import synth
+    sd = {k: v.double() for k, v in synth.make_dimp_state_dict(0).items()}
+    frames, _ = synth.make_frames(3, 1, 480, 640, 6, box=(300.0, 200.0, 60.0, 45.0))
+    im = torch.from_numpy(np.ascontiguousarray(frames[0][96:384, 176:464, :3])).permute(2, 0, 1)[None].double()
+    mean = torch.tensor(odn.MEAN, dtype=torch.float64).view(1, -1, 1, 1)
+    std = torch.tensor(odn.STD, dtype=torch.float64).view(1, -1, 1, 1)
+    x = (im / 255 - mean) / std
+
+    def fold(w, pre):   # conv + BN -> conv weight, bias
+        sc = sd[pre + ".weight"] / torch.sqrt(sd[pre + ".running_var"] + 1e-5)
+        return w * sc.view(-1, 1, 1, 1), sd[pre + ".bias"] - sd[pre + ".running_mean"] * sc
+
+    def conv(name, x, w, b, stride, pad):
+        out = F.conv2d(x, w, b, stride=stride, padding=pad)
+        return out, (name, x.float(), w.float(), stride, pad)
+
+    fe = "feature_extractor"
+    res = []
+    w, b = fold(sd[fe + ".conv1.weight"], fe + ".bn1")
+    y, rec = conv("stem", x, w, b, 2, 3)
+    res.append(rec)
+    x = F.max_pool2d(F.relu(y), 3, 2, 1)
+    for li, (planes, blocks, stride) in enumerate(odn.LAYERS):
+        for bi in range(blocks):
+            pre = f"{fe}.layer{li + 1}.{bi}"
+            st = stride if bi == 0 else 1
+            w, b = fold(sd[pre + ".conv1.weight"], pre + ".bn1")
+            y, rec = conv(pre + ".conv1", x, w, b, 1, 0)
+            res.append(rec)
+            y = F.relu(y)
+            w, b = fold(sd[pre + ".conv2.weight"], pre + ".bn2")
+            y, rec = conv(pre + ".conv2", y, w, b, st, 1)
+            res.append(rec)
+            y = F.relu(y)
+            w, b = fold(sd[pre + ".conv3.weight"], pre + ".bn3")
+            y, rec = conv(pre + ".conv3", y, w, b, 1, 0)
+            res.append(rec)
+            if bi == 0:
+                w, b = fold(sd[pre + ".downsample.0.weight"], pre + ".downsample.1")
+                r, rec = conv(pre + ".downsample", x, w, b, st, 0)
+                res.append(rec)
+            else:
+                r = x
+            x = F.relu(y + r)
+    _, rec = conv("clf", x, sd["classifier.feature_extractor.0.weight"], None, 1, 1)
+    res.append(rec)
+    return res
+
+
+def test_conv2d_fp32_per_layer_vs_fp64():
+    """precision="fp32" convolutions (conv_f32_kernel, fp32-input MFMA) layer by layer on the network's own
+    activations, against float64 on the same fp32 operands, beside the parity-mode kernel and the CPU's fp32 conv
+    (torch, the reference's arithmetic) on the same operands.  An fp32-input MFMA adds its four products to the
+    accumulator one rounding at a time, so one accumulator per output is a K-long sequential sum (K = 9 216 for the
+    clf conv): the kernel keeps four accumulator sets over interleaved K-tiles and adds them pairwise (dimpnet.hip
+    CONV_F32_NACC), which brings it to the CPU's distance from float64 on every layer (DeT dimpnet.py:421-476,
+    resnet.py:76-95)."""
+    from mmtrack_amd import dimpnet
+    rows = []
+    for name, x, w, stride, pad in _dimp_layer_inputs():
+        ref = F.conv2d(x.double(), w.double(), stride=stride, padding=pad)
+        scale = float(ref.abs().max())
+        err = lambda got: float((got.double() - ref).abs().max()) / scale
+        e32 = err(dimpnet.conv2d(x.cuda(), w, stride=stride, pad=pad).cpu())
+        e16 = err(dimpnet.conv2d(x.cuda(), w, stride=stride, pad=pad, precision="f16x3").cpu())
+        ecpu = err(F.conv2d(x, w, stride=stride, padding=pad))
+        rows.append((name, w.shape[1] * w.shape[2] * w.shape[3], e32, e16, ecpu))
+    for name, K, e32, e16, ecpu in rows:
+        print(f"{name:40s} K {K:5d}  fp32 {e32:.2e}  f16x3 {e16:.2e}  cpu-fp32 {ecpu:.2e}")
+    for name, K, e32, e16, ecpu in rows:
+        assert e32 < 1e-5, (name, e32)
+        assert e16 < 1e-5, (name, e16)
+        # (one accumulator set: up to 2.85e-6 on the clf conv and above the parity-mode kernel on 30 of 44 layers;
+        # four: 1.33e-6, at or below it on every layer -- profiles/r06_dimp_fp32_per_layer.txt)
+        assert e32 <= 1.1 * max(ecpu, e16), (name, e32, ecpu, e16)
+
+
 def test_conv_kernels_bitwise(tmp_path):
     """The f16x3 conv kernels against each other (tests/conv_dump.py, one child process per setting: the knobs are
     read once per process): the deep-pipelined generic kernel (conv_f16x3_deep_kernel: three or two register sets,

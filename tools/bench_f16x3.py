@@ -18,7 +18,9 @@ SHAPES = {"fc2": (10240, 768, 3072, 2), "fc2_ce": (4896, 768, 3072, 2), "proj": 
           "fc2_243": (3888, 768, 3072, 2), "fc2_189": (3024, 768, 3072, 2), "fc2_152": (2432, 768, 3072, 2),
           "proj_152": (2432, 768, 768, 2), "proj_half": (5120, 768, 768, 2), "proj_243": (3888, 768, 768, 2),
           "proj_189": (3024, 768, 768, 2), "qkv_half": (5120, 2304, 768, 0), "fc1_half": (5120, 3072, 768, 1),
-          "qkv_243": (3888, 2304, 768, 0), "fc1_243": (3888, 3072, 768, 1), "fc1_152": (2432, 3072, 768, 1), "qkv_152": (2432, 2304, 768, 0)}
+          "qkv_243": (3888, 2304, 768, 0), "fc1_243": (3888, 3072, 768, 1), "fc1_152": (2432, 3072, 768, 1), "qkv_152": (2432, 2304, 768, 0),
+          # the FLOPs of fc2 at 32 sequences as 240 tiles of 256 x 256 over K = 1536 (a two-way K split's round)
+          "fc2_sk2_emul": (20480, 768, 1536, 2), "fc2_k1536": (10240, 768, 1536, 2)}
 sel = os.environ.get("SHAPES")
 s = torch.cuda.current_stream().cuda_stream
 for name, (M, N, K, epi) in SHAPES.items():
