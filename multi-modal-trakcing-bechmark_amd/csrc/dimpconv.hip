@@ -671,6 +671,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 // fragments read the same finite weights against the zero pixel).
 constexpr int kPoolT = 8, kPoolS = 2 * kPoolT + 1, kPoolPx = kPoolS * kPoolS;   // 8 x 8 pooled, 17 x 17 stem
 constexpr int kPoolPW = (kPoolS - 1) * 2 + 7, kPoolMaxP = kPoolPW * kPoolPW;      // 39 x 39 input pixels
+constexpr int kPoolHalf = (kPoolPW + 1) / 2;                                         // a row's even columns
 constexpr int kPoolLdsP = 2 * (kPoolMaxP + 1) * 4 * 2;                               // patch hi / lo (+ zero pixel)
 constexpr int kPoolLdsW = 6 * 2 * 64 * 32 * 2 + 2 * 64 * 8 * 2;                     // K-tiles 0-5, chunk 0 of 6
 constexpr int kPoolLds = kPoolLdsP + kPoolLdsW > kPoolPx * 64 * 4 ? kPoolLdsP + kPoolLdsW : kPoolPx * 64 * 4;
@@ -725,9 +726,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   }
   const rsrc_t rX = make_rsrc(g.x, (int64_t)a.N * a.H * a.W * 16);
   float4 pv[NPL];
+  int lq[NPL];   // the pixel's LDS slot: each patch row stores its even columns, then its odd ones (see below)
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
     const int q = t + 512 * k, py = q / kPoolPW, px = q - py * kPoolPW;
+    lq[k] = py * kPoolPW + (px & 1) * kPoolHalf + (px >> 1);
     const int iy = iy0 + py, ix = ix0 + px;
     const bool ok = q < kPoolMaxP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
     const uint32_t vo = ok ? (uint32_t)(((img * a.H + iy) * a.W + ix) * 16) : kBufOob;
@@ -742,21 +745,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
       split_h(pv[k].y * sa, h[1], l[1]);
       split_h(pv[k].z * sa, h[2], l[2]);
       split_h(pv[k].w * sa, h[3], l[3]);
-      *reinterpret_cast<uint2*>(&sPh[q * 4]) = make_uint2(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16);
-      *reinterpret_cast<uint2*>(&sPl[q * 4]) = make_uint2(l[0] | (uint32_t)l[1] << 16, l[2] | (uint32_t)l[3] << 16);
+      *reinterpret_cast<uint2*>(&sPh[lq[k] * 4]) = make_uint2(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16);
+      *reinterpret_cast<uint2*>(&sPl[lq[k] * 4]) = make_uint2(l[0] | (uint32_t)l[1] << 16, l[2] | (uint32_t)l[3] << 16);
     }
   }
   if (t < 2) *reinterpret_cast<uint2*>(&(t ? sPl : sPh)[kPoolMaxP * 4]) = make_uint2(0u, 0u);   // the zero pixel
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // fragment i of wave row wm: stem pixels p = (wm + 4 i) * 16 + (lane & 15) of the 17 x 17 tile (p >= 289: idle)
+  // fragment i of wave row wm: stem pixels p = (wm + 4 i) * 16 + (lane & 15) of the 17 x 17 tile (p >= 289: idle).
+  // The stride-2 stem reads input columns 2 sc + kx: with each patch row stored as its even columns then its odd ones,
+  // the 16 lanes of a fragment column read 16 consecutive 8-B slots (32 banks) for any tap, and the next lane group's
+  // tap (kx + 2, same parity) the slots one further -- the same addresses but for its last lane, whose banks are free.
+  // Interleaved, the slots were 16 B apart and that last lane met lane 0's banks: 38 % of the kernel's LDS cycles
+  // were bank conflicts (r05_pmc_mfma_dimp_b1.txt)
   const int c = lane >> 4, col = lane & 15;
   int pbase[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int p = (wm + 4 * i) * 16 + col, sr = p / kPoolS, sc = p - sr * kPoolS;
-    pbase[i] = p < kPoolPx ? (sr * 2) * kPoolPW + sc * 2 : -1;
+    pbase[i] = p < kPoolPx ? (sr * 2) * kPoolPW + sc : -1;
   }
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -773,7 +781,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int tap = kt * 8 + 2 * c + h, ky = tap / 7, kx = tap - ky * 7;
-        const int pix = tap < 49 && pbase[i] >= 0 ? pbase[i] + ky * kPoolPW + kx : kPoolMaxP;
+        const int pix = tap < 49 && pbase[i] >= 0 ? pbase[i] + ky * kPoolPW + (kx & 1) * kPoolHalf + (kx >> 1)
+                                                  : kPoolMaxP;
         hv[h] = *reinterpret_cast<const uint2*>(&sPh[pix * 4]);
         lv[h] = *reinterpret_cast<const uint2*>(&sPl[pix * 4]);
       }
