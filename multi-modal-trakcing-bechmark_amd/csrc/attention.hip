@@ -205,6 +205,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
     bf16_t(&Ks)[NH][KB * 64] = KsAll[DMA ? stage : (KSPLIT ? wave : 0)];
     bf16_t(&Vs)[NH][KB * 64] = VsAll[DMA ? stage : (KSPLIT ? wave : 0)];
     stage ^= 1;
+    // a wave whose queries all lie past N (the last query tile of a sequence: at 153 tokens 6 of its 8 waves) still
+    // stages its share of the K / V tiles and meets the barriers, but multiplies nothing: its MFMA and softmax issue
+    // slots go to the other waves of its SIMDs (wave-uniform)
+    if (!KSPLIT && q0 >= N) continue;
 
     f32x4 sc[RB][4];
 #pragma unroll
