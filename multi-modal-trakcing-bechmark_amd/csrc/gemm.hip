@@ -1813,22 +1813,11 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // TF/s vs 240-250 for the 2-barrier 128 x 128 kernel); N = 768 stays on 128-row tiles (3 column tiles of
     // 256 leave most CUs idle)
     static const int t256_min = getenv("MMT_256S_MIN") ? atoi(getenv("MMT_256S_MIN")) : 128;
-    // MMT_T192W (tuning, percent; 0 = off): a wide GEMM whose 256 x 256 tiles take two or more rounds of the chip
-    // (counting the concurrent stream part) takes 128 x 192 tiles instead when their rounds x 0.375 (their work
-    // against a 256 x 256 tile) x MMT_T192W / 100 (their lower MFMA efficiency) is smaller.  Off: at 150 the two
-    // halves' qkv / fc1 of the candidate-eliminated layers switch and the line loses 1.5 % (each class alone gains
-    // 6 %, profiles/r05_ab_t192_wide_rejected.txt)
-    static const int t192w = getenv("MMT_T192W") ? atoi(getenv("MMT_T192W")) : 0;
-    if (t192w > 0 && a.N >= 2048 && a.N % 192 == 0 && a.K % 64 == 0 && a.groups == 1 && a.amode == A_DENSE &&
-        (a.M + 127) / 128 >= 8) {
-      const int conc = a.conc > 1 ? a.conc : 1, slots = num_cus();
-      const int r256 = (conc * ((a.M + 255) / 256) * (a.N / 256) + slots - 1) / slots;
-      const int r192 = (conc * ((a.M + 127) / 128) * (a.N / 192) + slots - 1) / slots;
-      if (r256 >= 2 && r192 * 375 * t192w < r256 * 100000) return launch_cfg<128, 192, 4, 2, true, 2, 64>(a, epi, s);
-    }
     // 320 x 256 tiles where they take fewer rounds of the one-workgroup-per-CU slots than 256 x 256 ones by more than
     // their 1.25x work per tile, counting the concurrent stream part (qkv of the 244-token layers, fc1 of the
-    // 190-token ones at 2 x 16 sequences: two rounds -> one).  MMT_T320: 0 never, 1 the round rule, 2 always (tuning)
+    // 190-token ones at 2 x 16 sequences: two rounds -> one; OSTrack-384 2 914 -> 3 000 frames/s, r06_ab_t320_ostrack.txt;
+    // ties, 5 rounds of 320-row tiles for 5 of 256-row ones, measured -0.6 %).  MMT_T320: 0 never, 1 the rule, 2 always
+    // (tuning)
     static const int t320 = getenv("MMT_T320") ? atoi(getenv("MMT_T320")) : 1;
     bool use320 = false;
     if (t320 && a.groups == 1 && (epi == EPI_BF16 || epi == EPI_GELU_BF16)) {
@@ -1900,18 +1889,10 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // more vs 128 once the head convs (grouped, N = 3 x 128) take it too, sweep_t128.sh / ab_env.sh); a short
     // K streams 32-deep K-tiles (proj 51 -> 48 us, patch 98 -> 85 us at 32 sequences, tests/sweep_split_cfg_b32.sh),
     // fc2's K = 3072 keeps 64-deep ones (144 -> 135 us)
-    static const bool old_rule = getenv("MMT_SPLIT_OLD") != nullptr;
     static const int t128_min = getenv("MMT_SPLIT_T128") ? atoi(getenv("MMT_SPLIT_T128")) : 64;
-    static const bool conv_old = getenv("MMT_SPLIT_CONV_OLD") != nullptr;
-    // (not for one sequence's few rows: fc1 at M = 320 keeps 240 64 x 64 workgroups instead of 72)
-    if (!old_rule && (a.amode == A_DENSE || !conv_old) && a.N % 128 == 0 && t128n >= t128_min && t128 >= 8) {
-      // the head's implicit 3x3 conv (A_CONV3, K = 6912) gathers 64-channel K-tiles
-      static const int n768 = getenv("MMT_SPLIT_N768") ? atoi(getenv("MMT_SPLIT_N768")) : 0;   // tuning
-      if (n768 && a.amode == A_DENSE && a.N % 256 == 0) {
-        if (n768 == 1) return launch_cfg<256, 128, 4, 2, true, 3, 32>(a, epi, s);
-        if (n768 == 2) return launch_cfg<256, 128, 4, 2, true, 2, 32>(a, epi, s);
-        if (n768 == 3) return launch_cfg<128, 256, 2, 4, true, 2, 32>(a, epi, s);
-      }
+    // (not for one sequence's few rows: fc1 at M = 320 keeps 240 64 x 64 workgroups instead of 72; the head's implicit
+    // 3x3 conv, A_CONV3 with K = 6912, gathers 64-channel K-tiles)
+    if (a.N % 128 == 0 && t128n >= t128_min && t128 >= 8) {
       // 128 x 192 tiles where all of them fit one round of the chip's one-workgroup-per-CU slots and 128 x 128 tiles
       // would take two or more, counting the launches of the other stream parts that run beside this one (a.conc):
       // the head's conv1 at 2 x 16 sequences (256 tiles in one round instead of 384: 287 -> 196 us alone), fc2 / proj
@@ -1928,28 +1909,7 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
       // (the N = 768 GEMMs -- proj, patch -- take the register-pipelined 64-deep tile since it exists: proj at one
       // half's rows 31 -> 25 us (5 120 rows) .. 27 -> 22 us (2 432), tests/r3_run33.sh; the wide qkv / fc1 fallbacks
       // keep the 32-deep ring, level or better there)
-      static const bool k32_all = getenv("MMT_SPLIT_K32") != nullptr;   // tuning: the 32-deep tile for N = 768 too
-      if (a.K <= 1024 && a.amode == A_DENSE && (k32_all || a.N > 768))
-        return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
-      // MMT_SK128 (tuning): a long-K residual GEMM with too few tiles for whole rounds of workgroups (fc2 in the
-      // CE-pruned layers: 114-186 tiles of one 128-KB workgroup per CU) splits K so that rounds x (1 / ks) drops,
-      // the slabs left for the consumer's deferred reduce.  Measured against the two-stream halves (whose other
-      // half fills the tail): up to 8 slices -2.8 %, at most 2 (the 152-token layers only) level (tests/r3_run22.sh)
-      static const int sk128 = getenv("MMT_SK128") ? atoi(getenv("MMT_SK128")) : 0;
-      if (sk128 > 0 && a.ws && a.defer_reduce && epi == EPI_RESID_F32 && a.groups == 1 && a.amode == A_DENSE) {
-        const int tiles = t128 * (a.N / 128), nk = a.K / 64, slots = num_cus();
-        int best = 1;
-        double bcost = (double)((tiles + slots - 1) / slots);
-        for (int ks = 2; ks <= (sk128 > 1 ? sk128 : kMaxDeferKs); ++ks) {
-          if (nk / ks < 8 || (int64_t)ks * a.M * a.N > a.ws_elems) break;
-          const double cost = (double)((tiles * ks + slots - 1) / slots) / ks;
-          if (cost < 0.9 * bcost) {
-            best = ks;
-            bcost = cost;
-          }
-        }
-        if (best > 1) return launch_splitk<128, 128, 4, 2, A_DENSE, true, 2>(a, epi, best, s);
-      }
+      if (a.K <= 1024 && a.amode == A_DENSE && a.N > 768) return launch_cfg<128, 128, 4, 2, true, 2, 32>(a, epi, s);
       return launch_cfg<128, 128, 4, 2, true, 2, 64>(a, epi, s);
     }
   }
@@ -1968,33 +1928,26 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     static const int sk_max = getenv("MMT_SPLITK_MAX") ? atoi(getenv("MMT_SPLITK_MAX")) : 8;
     // slices per tile rounded DOWN, so the slices of every tile run in one round of workgroups (fc2 at one
     // sequence: 60 tiles x 4 = 240 workgroups of 768-deep slices beat 300 of 614 that take two rounds on 44
-    // CUs; 823 -> 906 frames/s, tests/sk_round_ab.sh); MMT_SPLITK_CEIL: round up (tuning)
-    static const bool sk_ceil = getenv("MMT_SPLITK_CEIL") != nullptr;
-    // 64 x 64 few-tile GEMMs with 8 waves (16 x 32 each): twice the waves issuing each K-tile's LDS-DMA
-    // loads -- at one sequence these GEMMs are bound by what a CU can take in (one tile per CU, ~400 KB of
-    // hi + lo operands at ~45 GB/s), 906 -> 929 frames/s (tests/few_w8_ab.sh); MMT_FEW_W4: 4 waves (tuning)
-    static const bool few_w8 = getenv("MMT_FEW_W4") == nullptr;
+    // CUs; 823 -> 906 frames/s, round 2).  64 x 64 few-tile GEMMs with 8 waves (16 x 32 each): twice
+    // the waves issuing each K-tile's LDS-DMA loads -- at one sequence these GEMMs are bound by what a CU can take in
+    // (one tile per CU, ~400 KB of hi + lo operands at ~45 GB/s), 906 -> 929 frames/s against 4 waves
+    // (tests/few_w8_ab.sh)
     if (a.ws && a.ws_elems > 0 && tiles < sk_tiles && nk >= 2 * sk_minkt) {
-      int ks = sk_ceil ? (sk_target + tiles - 1) / tiles : sk_target / tiles;
+      int ks = sk_target / tiles;
       ks = ks < nk / sk_minkt ? ks : nk / sk_minkt;
       ks = ks < sk_max ? ks : sk_max;
       while (ks > 1 && (int64_t)ks * a.groups * a.M * a.N > a.ws_elems) --ks;
       if (ks > 1) {
         // f16x3: a 3-deep ring (96 KB of LDS) beat 4-deep at one sequence (tests/sweep_ring_b1.sh)
         constexpr int SKST = SPLIT ? 3 : 4;
-        if (few_w8) {
-          if (a.amode == A_CONV3) return launch_splitk<64, 64, 4, 2, A_CONV3, SPLIT, SKST>(a, epi, ks, s);
-          return launch_splitk<64, 64, 4, 2, A_DENSE, SPLIT, SKST>(a, epi, ks, s);
-        }
-        if (a.amode == A_CONV3) return launch_splitk<64, 64, 2, 2, A_CONV3, SPLIT, SKST>(a, epi, ks, s);
-        return launch_splitk<64, 64, 2, 2, A_DENSE, SPLIT, SKST>(a, epi, ks, s);
+        if (a.amode == A_CONV3) return launch_splitk<64, 64, 4, 2, A_CONV3, SPLIT, SKST>(a, epi, ks, s);
+        return launch_splitk<64, 64, 4, 2, A_DENSE, SPLIT, SKST>(a, epi, ks, s);
       }
     }
     // few tiles (small batches): each workgroup walks the whole K serially, so keep K-tiles in flight
     // (bf16: 4-deep LDS ring, an 8-deep one measured no better at M = 320; f16x3: 3-deep, qkv 17.3 ->
     // 15.4 us and fc1 16.8 -> 16.5 us at one sequence, tests/sweep_ring_b1.sh)
-    if (few_w8 && a.K >= 6 * 64) return launch_cfg<64, 64, 4, 2, SPLIT, SPLIT ? 3 : 4>(a, epi, s);
-    if (a.K >= 6 * 64) return launch_cfg<64, 64, 2, 2, SPLIT, SPLIT ? 3 : 4>(a, epi, s);
+    if (a.K >= 6 * 64) return launch_cfg<64, 64, 4, 2, SPLIT, SPLIT ? 3 : 4>(a, epi, s);
     return launch_cfg<64, 64, 2, 2, SPLIT>(a, epi, s);
   }
   if (t64 * (a.N / 32) * a.groups >= target) return launch_cfg<64, 32, 4, 1, SPLIT>(a, epi, s);

@@ -115,22 +115,31 @@ __device__ __forceinline__ void store_f32(float* p, const Row12& y, int lane) {
 // EPI_RESID_F32 arithmetic -- the bits of the splitk_reduce launch this replaces.  All slab loads are issued
 // before the first add.
 constexpr int kMaxDeferSlabs = 8;
-__device__ __forceinline__ Row12 apply_reduce(const Row12& x, const RowReduce& rr, int64_t row, int lane) {
+// the pending split-K update of a residual row in two halves: the loads of the row's slabs and bias (issued early by a
+// kernel that has the row index early), then the sum in slice order, scale, bias and residual add
+struct SlabRow {
   f32x4 p[kMaxDeferSlabs][3];
+  float4 bias[3];
+};
+__device__ __forceinline__ void load_slabs(const RowReduce& rr, int64_t row, int lane, SlabRow& q) {
   const float* base = rr.ws + row * C768;
 #pragma unroll
   for (int sl = 0; sl < kMaxDeferSlabs; ++sl)
     if (sl < rr.ks)
 #pragma unroll
-      for (int i = 0; i < 3; ++i) p[sl][i] = reinterpret_cast<const f32x4*>(base + sl * rr.slab)[lane + 64 * i];
+      for (int i = 0; i < 3; ++i) q.p[sl][i] = reinterpret_cast<const f32x4*>(base + sl * rr.slab)[lane + 64 * i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) q.bias[i] = reinterpret_cast<const float4*>(rr.bias)[lane + 64 * i];
+}
+__device__ __forceinline__ Row12 combine_slabs(const Row12& x, const RowReduce& rr, const SlabRow& q) {
   Row12 o;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    f32x4 acc = p[0][i];
+    f32x4 acc = q.p[0][i];
 #pragma unroll
     for (int sl = 1; sl < kMaxDeferSlabs; ++sl)
-      if (sl < rr.ks) acc += p[sl][i];
-    const float4 bv = reinterpret_cast<const float4*>(rr.bias)[lane + 64 * i];
+      if (sl < rr.ks) acc += q.p[sl][i];
+    const float4 bv = q.bias[i];
     const float sc = rr.inv;
     // (explicit fmaf: the same rounding in every consumer kernel, see ln_row)
     const float v[4] = {__builtin_fmaf(acc[0], sc, bv.x), __builtin_fmaf(acc[1], sc, bv.y),
@@ -139,6 +148,11 @@ __device__ __forceinline__ Row12 apply_reduce(const Row12& x, const RowReduce& r
     o.v[i] = make_float4(r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]);
   }
   return o;
+}
+__device__ __forceinline__ Row12 apply_reduce(const Row12& x, const RowReduce& rr, int64_t row, int lane) {
+  SlabRow q;
+  load_slabs(rr, row, lane, q);
+  return combine_slabs(x, rr, q);
 }
 
 // ------------------------------------------------------------------ fovea statistics (vit_ce_prompt.py:33-47)
@@ -389,6 +403,8 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
   int64_t xrowv[R];
   Row12 xv[R];
   float apv[R], cpv[R];
+  static_assert(!RR || R == 1, "the slab-holding variant keeps one slot per wave");
+  SlabRow slabs;   // RR: the pending fc2 slabs of the wave's row, requested with the row (not after the barrier)
 #pragma unroll
   for (int rr = 0; rr < R; ++rr) {
     const int s = (blockIdx.x * R + rr) * TOK_ROWS + (threadIdx.x >> 6);   // slot of this wave
@@ -397,6 +413,7 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
     posv[rr] = pos;
     xrowv[rr] = (int64_t)b * a.srcA_rows + max(pos, 0);
     xv[rr] = load_row(a.srcA + xrowv[rr] * C768, lane);
+    if (RR && a.rr.ws) load_slabs(a.rr, xrowv[rr], lane, slabs);
     const int64_t srow = ((int64_t)b * L + min(s, L - 1)) * 8;
     apv[rr] = lane < 8 ? a.a8p[srow + lane] : 0.f;
     cpv[rr] = lane < 8 ? a.c8p[srow + lane] : 0.f;
@@ -424,7 +441,7 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
   const float ap = apv[rr], cp = cpv[rr];
   if (s >= L) break;   // wave-uniform; later slots of the wave lie further out
   if (RR && pos >= 0 && a.rr.ws) {   // the previous block's fc2 update of this slot's residual row, written back
-    x = apply_reduce(x, a.rr, xrow, lane);
+    x = combine_slabs(x, a.rr, slabs);
     store_f32(const_cast<float*>(a.srcA) + xrow * C768, x, lane);
   }
   const float2 ac = deep_slot(x, pos >= 0, s < a.Lz ? 0 : 1, ap, cp, st, fold, W0, ba, a.smooth_p, lane);
