@@ -1603,8 +1603,53 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const GemmArgs args) {
     }
 #endif
     return;
+  } else if constexpr (EPI == EPI_RESID_F32 && MI == 4) {
+    // fp32 residual output (the long-K residual GEMM, MMT_FC2_256S): per 128-row half the residual chunks are requested
+    // first, the half's acc * inv + bias goes to the LDS ([128][256] fp32, 16-B chunks XOR-swizzled by row), then every
+    // lane stores whole 16-B row chunks of R + value (store4v's arithmetic: the same bits)
+    using LF = LdsTile<EPI_F32, 256>;
+    char* const lds = reinterpret_cast<char*>(smem);
+    const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int mb = m0 + h * 128;
+      u32x4 rv[128 * 64 / 512];
+#pragma unroll
+      for (int k = 0; k < 128 * 64 / 512; ++k) {
+        const int idx = tid + k * 512, r = idx >> 6, cc = idx & 63, m = mb + r;
+        const uint32_t o = m < M ? (uint32_t)(((int64_t)m * g.ldr + n0 + 4 * cc) * 4) : kBufOob;
+        rv[k] = __builtin_amdgcn_raw_buffer_load_b128(rR, o, 0, 0);
+      }
+      __syncthreads();   // h = 0: every wave's last fragment reads are done; h = 1: the first half is drained
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        if (QA[qd] != h) continue;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const f32x4& a = acc[qd][i][jj];
+            const float4 bv = bq[QB[qd]][jj];
+            const float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
+            LF::put(lds, wr * 64 + i * 16 + (lane & 15), QB[qd] * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, v);
+          }
+      }
+      __syncthreads();
+      const int rows = max(0, min(128, M - mb));
+      const rsrc_t rC = make_rsrc(static_cast<float*>(g.C) + (int64_t)mb * g.ldc, (int64_t)rows * g.ldc * 4);
+#pragma unroll
+      for (int k = 0; k < 128 * 64 / 512; ++k) {
+        const int idx = tid + k * 512, r = idx >> 6, cc = idx & 63;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(lds + r * 256 * 4 + ((cc ^ (r & LF::MASK)) << 4));
+        const f32x4 o = __builtin_bit_cast(f32x4, rv[k]) + v;
+        const uint32_t go = r < rows ? (uint32_t)(((int64_t)r * g.ldc + n0 + 4 * cc) * 4) : kBufOob;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rC, go, 0, 0);
+      }
+    }
+    GEMM_STAMP(3);
   } else {
-    // (the residual epilogues, not used by the path's launches, keep the per-fragment store4)
+    // (the remaining fp32 epilogues, not used by the path's launches, keep the per-fragment store4)
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd)
@@ -1813,6 +1858,16 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     // TF/s vs 240-250 for the 2-barrier 128 x 128 kernel); N = 768 stays on 128-row tiles (3 column tiles of
     // 256 leave most CUs idle)
     static const int t256_min = getenv("MMT_256S_MIN") ? atoi(getenv("MMT_256S_MIN")) : 128;
+    // the residual GEMMs (fc2, proj: N = 768) on the eight-phase kernel where its 256 x 256 tiles fill at least three
+    // quarters of a round of the chip, counting the concurrent stream part: OSTrack-384's 720- and 548-token layers
+    // (270 / 210 tiles; OSTrack 2 987 -> 3 045 frames/s with fc2 and proj at a full round, r06_ab_resid_256s.txt).  The
+    // ViT layers' 120 tiles stay on the 128-row kernels: fc2 there lost 10 % (four times the work per tile lengthens
+    // each stream half's chain).  MMT_RESID_256S: 0 never, 2 always (tuning)
+    static const int resid_256s = getenv("MMT_RESID_256S") ? atoi(getenv("MMT_RESID_256S")) : 1;
+    if (resid_256s && epi == EPI_RESID_F32 && a.groups == 1 && a.N % 256 == 0 &&
+        (resid_256s == 2 || 4 * (a.conc > 1 ? a.conc : 1) * ((a.M + 255) / 256) * (a.N / 256) >= 3 * num_cus()) &&
+        launch256s_epi(a, epi, s))
+      return;
     // 320 x 256 tiles where they take fewer rounds of the one-workgroup-per-CU slots than 256 x 256 ones by more than
     // their 1.25x work per tile, counting the concurrent stream part (qkv of the 244-token layers, fc1 of the
     // 190-token ones at 2 x 16 sequences: two rounds -> one; OSTrack-384 2 914 -> 3 000 frames/s, r06_ab_t320_ostrack.txt;
@@ -1828,7 +1883,7 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
     }
     const bool forced = g_force_cfg == 320 || g_force_cfg == 256;   // tests: pin the tile (any tile count)
     if (forced) use320 = g_force_cfg == 320 && (epi == EPI_BF16 || epi == EPI_GELU_BF16);
-    if (a.N >= 2048 && ((a.M + 255) / 256 * (a.N / 256) * a.groups >= t256_min || forced) &&
+    if ((a.N >= 2048 || forced) && ((a.M + 255) / 256 * (a.N / 256) * a.groups >= t256_min || forced) &&
         launch256s_epi(a, epi, s, use320))
       return;
   }

@@ -156,6 +156,35 @@ def test_gemm_f16x3_t320(lib, M, N, K, epi):
                                                                                   Cl2.view(torch.int16))
 
 
+@pytest.mark.parametrize("M,N,K", [(10240, 768, 3072), (4896, 768, 3072), (11520, 768, 768), (700, 768, 128)])
+def test_gemm_f16x3_256s_residual(lib, M, N, K):
+    """The eight-phase 256 x 256 tile with the fp32 residual epilogue (gemm256s_kernel<EPI_RESID_F32, 4>: the residual
+    chunks requested first, the tile staged through the LDS per 128-row half, whole 16-B row chunks stored), in place
+    on the residual stream as fc2 / proj run it at OSTrack-384's long layers (timm Mlp fc2, attn.py proj + the block's
+    residual adds, attn_blocks.py:93-104), vs fp64."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 11)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g) * (0.5 / math.sqrt(K))
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    sa, sw = range_scale(A), range_scale(W)
+    Ah, Al, A64 = split(A, sa)
+    Wh, Wl, W64 = split(W, sw)
+    ref = A64 @ W64.t() + bias.double()
+    R = torch.randn(M, N, device="cuda", generator=g)
+    C = R.clone()
+    lib.mmt_gemm_force_config(256)
+    try:
+        _gemm(lib, Ah, Al, Wh, Wl, bias, C, None, 1.0 / (sa * sw), 1.0, 2, R=C)
+    finally:
+        lib.mmt_gemm_force_config(-1)
+    y = R.double() + ref
+    err = float((C.double() - y).abs().max())
+    tol = 1e-5 * float(ref.abs().max()) + 4e-7 * float(y.abs().max())
+    print(f"f16x3 gemm 256x256 residual M={M} N={N} K={K}: max|err| {err:.3e} (tol {tol:.3e})")
+    assert torch.isfinite(C).all()
+    assert err <= tol
+
+
 @pytest.mark.parametrize("B,N", [(32, 320), (16, 320), (16, 244), (16, 153), (16, 720), (12, 190), (1, 320),
                                  (1, 153), (2, 244), (1, 720)])
 def test_attention_f16x3_vs_fp64(lib, B, N):
