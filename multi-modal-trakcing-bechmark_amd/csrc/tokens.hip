@@ -36,7 +36,20 @@ __device__ __forceinline__ float sumsq4(float4 d, float acc) {
   t = __builtin_fmaf(d.w, d.w, t);
   return acc + t;
 }
-__device__ __forceinline__ Row12 ln_row(const Row12& x, const float* w, const float* b, int lane) {
+// the LayerNorm affine of one lane's 12 columns, requested at kernel entry: loaded inside ln_row, after a store of
+// the residual row, it was a second dependent memory round trip per launch (the compiler may not move a load above
+// a store it cannot prove disjoint)
+struct LnAffine { float4 w[3], b[3]; };
+__device__ __forceinline__ LnAffine load_affine(const float* w, const float* b, int lane) {
+  LnAffine a;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    a.w[i] = reinterpret_cast<const float4*>(w)[lane + 64 * i];
+    a.b[i] = reinterpret_cast<const float4*>(b)[lane + 64 * i];
+  }
+  return a;
+}
+__device__ __forceinline__ Row12 ln_row(const Row12& x, const LnAffine& af) {
 #pragma clang fp contract(off)
   float s = 0.f;
 #pragma unroll
@@ -48,11 +61,9 @@ __device__ __forceinline__ Row12 ln_row(const Row12& x, const float* w, const fl
     q = sumsq4(make_float4(x.v[i].x - mean, x.v[i].y - mean, x.v[i].z - mean, x.v[i].w - mean), q);
   const float rstd = 1.0f / sqrtf(__builtin_fmaf(wave_sum(q), 1.0f / C768, LN_EPS));
   Row12 y;
-  const float4* w4 = reinterpret_cast<const float4*>(w);
-  const float4* b4 = reinterpret_cast<const float4*>(b);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const float4 ww = w4[lane + 64 * i], bb = b4[lane + 64 * i];
+    const float4 ww = af.w[i], bb = af.b[i];
     y.v[i] = make_float4(__builtin_fmaf((x.v[i].x - mean) * rstd, ww.x, bb.x),
                          __builtin_fmaf((x.v[i].y - mean) * rstd, ww.y, bb.y),
                          __builtin_fmaf((x.v[i].z - mean) * rstd, ww.z, bb.z),
@@ -124,12 +135,12 @@ struct SlabRow {
 __device__ __forceinline__ void load_slabs(const RowReduce& rr, int64_t row, int lane, SlabRow& q) {
   const float* base = rr.ws + row * C768;
 #pragma unroll
+  for (int i = 0; i < 3; ++i) q.bias[i] = reinterpret_cast<const float4*>(rr.bias)[lane + 64 * i];
+#pragma unroll
   for (int sl = 0; sl < kMaxDeferSlabs; ++sl)
     if (sl < rr.ks)
 #pragma unroll
       for (int i = 0; i < 3; ++i) q.p[sl][i] = reinterpret_cast<const f32x4*>(base + sl * rr.slab)[lane + 64 * i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) q.bias[i] = reinterpret_cast<const float4*>(rr.bias)[lane + 64 * i];
 }
 __device__ __forceinline__ Row12 combine_slabs(const Row12& x, const RowReduce& rr, const SlabRow& q) {
   Row12 o;
@@ -224,6 +235,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
                                                  const RowReduce rr) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
+  const LnAffine af = load_affine(w, b, lane);
   int64_t src = r;
   if (gather) {
     const int bs = r / rows_per_seq;
@@ -235,7 +247,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
     if (!xcopy) store_f32(const_cast<float*>(x) + src * C768, xv, lane);
   }
   if (xcopy) store_f32(xcopy + (int64_t)r * C768, xv, lane);
-  const Row12 y = ln_row(xv, w, b, lane);
+  const Row12 y = ln_row(xv, af);
   if (olo) store_split(ob + (int64_t)r * C768, olo + (int64_t)r * C768, y, oscale, lane);
   else if (ob) store_bf16(ob + (int64_t)r * C768, y, lane);
   if (of) store_f32(of + (int64_t)r * C768, y, lane);
@@ -308,6 +320,7 @@ __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) 
   const int L = a.Lz + a.Lx, lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * PR_ROWS;
   const float ba = lane < 8 ? a.b00[lane] : 0.f, bb = lane < 8 ? a.b01[lane] : 0.f;
+  const LnAffine afA = load_affine(a.lnA_w, a.lnA_b, lane), afB = load_affine(a.lnB_w, a.lnB_b, lane);
   for (int rr = 0; rr < PR_ROWS; ++rr) {
     const int row = row0 + rr;
     if (row >= a.B * L) return;
@@ -321,9 +334,9 @@ __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) 
     }
     const Row12 xb = load_row(a.srcB + (int64_t)row * C768, lane);
     float part[8];
-    dot8_lds(ln_row(xa, a.lnA_w, a.lnA_b, lane), W0, part, lane);
+    dot8_lds(ln_row(xa, afA), W0, part, lane);
     const float ra = reduce8(part, lane);
-    dot8_lds(ln_row(xb, a.lnB_w, a.lnB_b, lane), W1, part, lane);
+    dot8_lds(ln_row(xb, afB), W1, part, lane);
     const float rb = reduce8(part, lane);
     if (lane < 8) {
       a.a8[(int64_t)row * 8 + lane] = ra + ba;
@@ -696,6 +709,7 @@ __global__ __launch_bounds__(256) void ce_ln_kernel(const CEArgs a, const float*
   __shared__ float key[1024];
   __shared__ int inv[1024];
   const int bs = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const LnAffine af = load_affine(w, b, lane);
   const float* prob = a.prob + (int64_t)bs * a.heads * a.Ls;
   for (int i = tid; i < a.Ls; i += 256) {
     float v[CE_MAX_HEADS];
@@ -746,7 +760,7 @@ __global__ __launch_bounds__(256) void ce_ln_kernel(const CEArgs a, const float*
     if (!xcopy) store_f32(const_cast<float*>(x) + src * C768, xv, lane);
   }
   if (xcopy) store_f32(xcopy + r * C768, xv, lane);
-  const Row12 y = ln_row(xv, w, b, lane);
+  const Row12 y = ln_row(xv, af);
   if (olo) store_split(ob + r * C768, olo + r * C768, y, oscale, lane);
   else if (ob) store_bf16(ob + r * C768, y, lane);
 }
@@ -777,13 +791,14 @@ __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int row
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= B * L) return;
   const int bs = r / L, s = r - bs * L;
+  const LnAffine af = load_affine(w, b, lane);
   int pos = s < Lz ? s : slot2pos[bs * Lx + (s - Lz)];
   Row12 y = zero_row();
   if (pos >= 0) {
     const int64_t row = (int64_t)bs * rows_per_seq + pos;
     Row12 x = load_row(X + row * C768, lane);
     if (rr.ws) x = apply_reduce(x, rr, row, lane);   // the last block's fc2 update (nothing reads X after this)
-    y = ln_row(x, w, b, lane);
+    y = ln_row(x, af);
   }
   if (s >= Lz && feat_lo)
     store_split(feat + ((int64_t)bs * Lx + (s - Lz)) * C768, feat_lo + ((int64_t)bs * Lx + (s - Lz)) * C768, y, fscale,
