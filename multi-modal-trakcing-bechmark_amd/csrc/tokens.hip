@@ -8,6 +8,29 @@ namespace mmt {
 constexpr int C768 = 768;
 constexpr float LN_EPS = 1e-6f;   // vit_ce_prompt.py:121
 
+#if defined(ROW_STAMPS)   // tuning builds only (tools/b1_row_stamps.py): per-block phase cycles of the row kernels
+// [kind][block][8]: s_memtime at four phase points of wave 0, s_memrealtime at entry and end; kind 0 = ln_kernel<true>,
+// 1 = ln_prompt_kernel, 2 = prompt_reduce_deep_kernel (the last launch of each kind in a frame)
+__device__ unsigned long long* g_row_stamps = nullptr;
+extern "C" int mmt_row_stamps(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_row_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#define RSTAMP_DECL unsigned long long* const rst_ = g_row_stamps
+#define RSTAMP_AT(kind, k, v)                                                                               \
+  do {                                                                                                      \
+    if (rst_ && threadIdx.x == 0)                                                                           \
+      rst_[((size_t)(kind) * 4096 + blockIdx.x + (size_t)blockIdx.y * gridDim.x) * 8 + (k)] = (v);          \
+  } while (0)
+#define RSTAMP(kind, k) RSTAMP_AT(kind, k, __builtin_amdgcn_s_memtime())
+#define RSTAMP_RT(kind, k) RSTAMP_AT(kind, k, __builtin_amdgcn_s_memrealtime())
+#define RSTAMP_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define RSTAMP_DECL
+#define RSTAMP(kind, k) do { } while (0)
+#define RSTAMP_RT(kind, k) do { } while (0)
+#define RSTAMP_DRAIN() do { } while (0)
+#endif
+
 struct Row12 { float4 v[3]; };
 
 __device__ __forceinline__ Row12 load_row(const float* p, int lane) {
@@ -168,10 +191,10 @@ __device__ __forceinline__ Row12 apply_reduce(const Row12& x, const RowReduce& r
 
 // ------------------------------------------------------------------ fovea statistics (vit_ce_prompt.py:33-47)
 // Per (sequence, part) and channel: the max over the part's slots of a8 * smooth and the sum of
-// exp(a8 * smooth - max), part 0 = template slots [0, Lz), part 1 = search slots [Lz, L).  Run by a whole
-// 512-thread block, 256 threads per part in the thread layout and reduction order of the former standalone
-// fovea kernel (channel = tid & 7, slot stripes of 32), so every block that needs a sequence's statistics
-// forms the same bits.  st[part * 16 + c] = max, st[part * 16 + 8 + c] = sum.
+// exp(a8 * smooth - max), part 0 = template slots [0, Lz), part 1 = search slots [Lz, L).  The reduction order is
+// that of the former standalone fovea kernel (256 threads per part, channel = tid & 7, slot stripes of 32, four
+// 64-thread groups combined pairwise), so every block that needs a sequence's statistics forms the same bits.
+// st[part * 16 + c] = max, st[part * 16 + 8 + c] = sum.
 // The sequence's a8 first goes to LDS with coalesced 16-B loads (fovea_stage, issued by the caller with its other
 // early loads; fovea_stats stores them and reduces from LDS, as the former fovea kernel did).
 constexpr int FOVEA_MAX_TOKENS = 1024;
@@ -186,6 +209,10 @@ __device__ __forceinline__ FoveaStage fovea_stage(const float* a8seq, int L) {
   }
   return f;
 }
+// (a thread's slots -- n / 32 of them, 8 at the 256-slot search part -- are read once into registers for both
+// passes, and the max and sum partials of the four groups go to separate LDS rows: three barriers fewer than the
+// former kernel's six, the same operations in the same order)
+constexpr int FOVEA_KV = 8;
 __device__ __forceinline__ void fovea_stats(const FoveaStage& fs, int Lz, int Lx, float sm, float* va, float* red,
                                             float* st) {
 #pragma unroll
@@ -197,26 +224,44 @@ __device__ __forceinline__ void fovea_stats(const FoveaStage& fs, int Lz, int Lx
   const int tid = threadIdx.x, part = tid >> 8, t = tid & 255;
   const int lo = part ? Lz : 0, n = part ? Lx : Lz;
   const int c = t & 7, stripe = t >> 3;
-  float* rp = red + part * 32;
+  float* rm = red + part * 32;        // [group][channel] maxima
+  float* rs = red + 64 + part * 32;   // [group][channel] sums
+  const int cnt = n > stripe ? (n - stripe + 31) / 32 : 0;   // this thread's slots stripe, stripe + 32, ...
+  const bool regs = cnt <= FOVEA_KV;                         // (n <= 256: every thread)
+  float v[FOVEA_KV];
   float mx = -INFINITY;
-  for (int k = stripe; k < n; k += 32) mx = fmaxf(mx, va[(lo + k) * 8 + c] * sm);
+  if (regs) {
+#pragma unroll
+    for (int j = 0; j < FOVEA_KV; ++j) v[j] = j < cnt ? va[(lo + stripe + 32 * j) * 8 + c] : 0.f;
+#pragma unroll
+    for (int j = 0; j < FOVEA_KV; ++j)
+      if (j < cnt) mx = fmaxf(mx, v[j] * sm);
+  } else {
+    for (int k = stripe; k < n; k += 32) mx = fmaxf(mx, va[(lo + k) * 8 + c] * sm);
+  }
   mx = fmaxf(mx, dpp<DPP_ROR8>(mx));
   mx = xmax16(mx);
   mx = xmax32(mx);
-  if ((t & 63) < 8) rp[(t >> 6) * 8 + c] = mx;
+  if ((t & 63) < 8) rm[(t >> 6) * 8 + c] = mx;
   __syncthreads();
-  if (t < 8) st[part * 16 + t] = fmaxf(fmaxf(rp[t], rp[8 + t]), fmaxf(rp[16 + t], rp[24 + t]));
-  __syncthreads();
-  const float cm = st[part * 16 + c];
+  const float cm = fmaxf(fmaxf(rm[c], rm[8 + c]), fmaxf(rm[16 + c], rm[24 + c]));
   float sum = 0.f;
-  for (int k = stripe; k < n; k += 32) sum += __expf(__builtin_fmaf(va[(lo + k) * 8 + c], sm, -cm));
+  if (regs) {
+#pragma unroll
+    for (int j = 0; j < FOVEA_KV; ++j)
+      if (j < cnt) sum += __expf(__builtin_fmaf(v[j], sm, -cm));
+  } else {
+    for (int k = stripe; k < n; k += 32) sum += __expf(__builtin_fmaf(va[(lo + k) * 8 + c], sm, -cm));
+  }
   sum += dpp<DPP_ROR8>(sum);
   sum = xsum16(sum, sum);
   sum = xsum32(sum, sum);
+  if ((t & 63) < 8) rs[(t >> 6) * 8 + c] = sum;
   __syncthreads();
-  if ((t & 63) < 8) rp[(t >> 6) * 8 + c] = sum;
-  __syncthreads();
-  if (t < 8) st[part * 16 + 8 + t] = (rp[t] + rp[8 + t]) + (rp[16 + t] + rp[24 + t]);
+  if (t < 8) {
+    st[part * 16 + t] = cm;
+    st[part * 16 + 8 + t] = (rs[t] + rs[8 + t]) + (rs[16 + t] + rs[24 + t]);
+  }
   __syncthreads();
 }
 // s8[c] of one slot (lane c < 8 of the caller): fovea mask * a8 + c8 (the former fovea kernel's expression)
@@ -233,6 +278,9 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
                                                  bf16_t* olo, float oscale, float* of, int rows, int rows_per_seq,
                                                  const int* gather, int in_rows_per_seq, float* xcopy,
                                                  const RowReduce rr) {
+  RSTAMP_DECL;
+  RSTAMP_RT(RR ? 0 : 3, 4);
+  RSTAMP(RR ? 0 : 3, 0);
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
   const LnAffine af = load_affine(w, b, lane);
@@ -247,10 +295,15 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
     if (!xcopy) store_f32(const_cast<float*>(x) + src * C768, xv, lane);
   }
   if (xcopy) store_f32(xcopy + (int64_t)r * C768, xv, lane);
+  RSTAMP(RR ? 0 : 3, 1);   // (the row and its slabs landed: the combine consumed them)
   const Row12 y = ln_row(xv, af);
+  RSTAMP(RR ? 0 : 3, 2);
   if (olo) store_split(ob + (int64_t)r * C768, olo + (int64_t)r * C768, y, oscale, lane);
   else if (ob) store_bf16(ob + (int64_t)r * C768, y, lane);
   if (of) store_f32(of + (int64_t)r * C768, y, lane);
+  RSTAMP_DRAIN();
+  RSTAMP(RR ? 0 : 3, 3);
+  RSTAMP_RT(RR ? 0 : 3, 5);
 }
 
 void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float out_scale,
@@ -405,7 +458,10 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
   __shared__ float fold[FOLD_N];
   __shared__ __attribute__((aligned(16))) float W0[8 * C768];   // conv0_0 (LN_A affine folded in)
   extern __shared__ __attribute__((aligned(16))) float va[];   // [L][8] (dynamic: sized by the launch)
-  __shared__ float red[64], st[32];
+  __shared__ float red[128], st[32];
+  RSTAMP_DECL;
+  RSTAMP_RT(2, 4);
+  RSTAMP(2, 0);
   const int L = a.Lz + a.Lx, lane = threadIdx.x & 63, b = blockIdx.y;
   // the previous a8's fovea statistics: as the previous LN1 wrote them (32 floats), else reduced here
   const bool pre = a.fstat_p != nullptr;
@@ -440,12 +496,14 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
 #pragma unroll
   for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[threadIdx.x + TOK_THREADS * k] = wst[k];
   if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
+  RSTAMP(2, 1);   // (wave 0's weight share landed: stored to the LDS)
   if (pre) {
     if (threadIdx.x < 32) st[threadIdx.x] = stv;
     __syncthreads();
   } else {
     fovea_stats(fsg, a.Lz, a.Lx, a.smooth_p, va, red, st);   // ends with a barrier
   }
+  RSTAMP(2, 2);
 #pragma unroll
   for (int rr = 0; rr < R; ++rr) {
   const int s = sv[rr], pos = posv[rr];
@@ -464,6 +522,9 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
     a.c8[row * 8 + lane] = ac.y;
   }
   }
+  RSTAMP_DRAIN();
+  RSTAMP(2, 3);
+  RSTAMP_RT(2, 5);
 }
 
 // slots per wave of the deep prompt / LN1 kernels: 2 from 8 sequences up (the weight fill and fovea statistics of a
@@ -563,7 +624,10 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
   __shared__ __attribute__((aligned(16))) float W1t[8 * C768];
   __shared__ __attribute__((aligned(16))) float cst[3 * C768];   // conv1x1 bias, norm1 weight, norm1 bias
   extern __shared__ __attribute__((aligned(16))) float va[];   // [L][8] (dynamic: sized by the launch)
-  __shared__ float red[64], st[32];
+  __shared__ float red[128], st[32];
+  RSTAMP_DECL;
+  RSTAMP_RT(1, 4);
+  RSTAMP(1, 0);
   const int lane = threadIdx.x & 63, b = blockIdx.y, L = a.Lz + a.Lx;
   const FoveaStage fsg = fovea_stage(a.a8 + (int64_t)b * L * 8, L);
   int tv[R], slotv[R];
@@ -606,13 +670,18 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
     const int e = threadIdx.x + TOK_THREADS * k;
     if (e < 3 * C768) cst[e] = cs[k];
   }
+  RSTAMP(1, 1);   // (wave 0's weight share landed: stored to the LDS)
   fovea_stats(fsg, a.Lz, a.Lx, a.smooth, va, red, st);   // ends with a barrier
+  RSTAMP(1, 2);
   if (a.fstat && blockIdx.x == 0 && threadIdx.x < 32) a.fstat[b * 32 + threadIdx.x] = st[threadIdx.x];
 #pragma unroll
   for (int rr = 0; rr < R; ++rr) {
   if (tv[rr] >= a.rows_per_seq) break;   // wave-uniform; later rows of the wave lie further out
   ln_prompt_row<MODE>(xvv[rr], qv[rr], avv[rr], cvv[rr], slotv[rr] < a.Lz ? 0 : 1, st, W1t, cst, a, rv[rr], lane);
   }
+  RSTAMP_DRAIN();
+  RSTAMP(1, 3);
+  RSTAMP_RT(1, 5);
 }
 
 void prompt_expand_ln(const LnPromptArgs& a, hipStream_t s) {
