@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
   RSTAMP_DECL;
   RSTAMP_RT(RR ? 0 : 3, 4);
   RSTAMP(RR ? 0 : 3, 0);
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
   const LnAffine af = load_affine(w, b, lane);
   int64_t src = r;
@@ -306,15 +306,25 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* x, const float* w,
   RSTAMP_RT(RR ? 0 : 3, 5);
 }
 
+// rows per workgroup: 4, or 1 for the few rows of one or two sequences -- each workgroup's row, split-K slabs and
+// affine then come into a CU of their own instead of four rows' worth into one (the launch is per-CU intake bound
+// there: a row with four fc2 slabs is 15 KB)
+static int rows_per_block(int rows) {
+  static const int few = getenv("MMT_ROW_FEW") ? atoi(getenv("MMT_ROW_FEW")) : 1024;
+  return rows <= few ? 1 : 4;
+}
+
 void layernorm(const float* x, const float* w, const float* b, bf16_t* out_bf16, bf16_t* out_lo, float out_scale,
                float* out_f32, int rows, int rows_per_seq, const int* gather, int in_rows_per_seq, float* xcopy,
                hipStream_t s, const RowReduce& rr) {
+  const int rpb = rows_per_block(rows);
+  const dim3 grid((rows + rpb - 1) / rpb), block(64 * rpb);
   if (rr.ws)
-    hipLaunchKernelGGL(ln_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_scale,
-                       out_f32, rows, rows_per_seq, gather, in_rows_per_seq, xcopy, rr);
+    hipLaunchKernelGGL(ln_kernel<true>, grid, block, 0, s, x, w, b, out_bf16, out_lo, out_scale, out_f32, rows,
+                       rows_per_seq, gather, in_rows_per_seq, xcopy, rr);
   else
-    hipLaunchKernelGGL(ln_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, s, x, w, b, out_bf16, out_lo, out_scale,
-                       out_f32, rows, rows_per_seq, gather, in_rows_per_seq, xcopy, rr);
+    hipLaunchKernelGGL(ln_kernel<false>, grid, block, 0, s, x, w, b, out_bf16, out_lo, out_scale, out_f32, rows,
+                       rows_per_seq, gather, in_rows_per_seq, xcopy, rr);
 }
 
 // ------------------------------------------------------------------ prompt block, part 1
@@ -407,6 +417,9 @@ __global__ __launch_bounds__(256) void prompt_reduce_kernel(const PromptArgs a) 
 // a8 / c8 -- is issued before the block's weight fill, statistics and barriers.
 constexpr int TOK_THREADS = 512;   // 8 waves per block share one LDS copy of the weights
 constexpr int TOK_ROWS = TOK_THREADS / 64;
+// the blocks of a deep-prompt / LN1 launch walk the 1 536 float4 of their 8 x 768 weight fill from one of eight
+// offsets, so they do not all request the same lines in the same order (one sequence +0.2 %, r06_b1_row_stamps.txt)
+#define WFILL_IDX(i) (((i) + (int)((blockIdx.x + 5 * blockIdx.y) % 8) * 192) % (8 * C768 / 4))
 
 // One slot of a deep prompt block (the wave's x row, already current; live = the slot has a row): returns, valid in
 // lanes 0-7, a8 = conv0_0(LN_A(x)) + b00 (LN_A's affine folded into W0 / b00 by pack_weights) and c8 from the previous
@@ -453,6 +466,8 @@ __device__ __forceinline__ float2 deep_slot(const Row12& x, bool live, int part_
 }
 
 // R: slots per wave (the block's weight fill and fovea statistics shared by R x 8 slots; 2 at large batches)
+// (two-slot 128-thread blocks for one sequence -- four times the blocks, each with its 24-KB weight fill -- measured
+// 4.1 -> 6.7 us per block and one sequence -2.5 %, profiles/r06_b1_row_stamps.txt)
 template <bool RR, int R>
 __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const PromptArgs a) {
   __shared__ float fold[FOLD_N];
@@ -490,11 +505,11 @@ __global__ __launch_bounds__(TOK_THREADS) void prompt_reduce_deep_kernel(const P
   constexpr int WV = 8 * C768 / 4 / TOK_THREADS;
   float4 wst[WV];
 #pragma unroll
-  for (int k = 0; k < WV; ++k) wst[k] = reinterpret_cast<const float4*>(a.w00)[threadIdx.x + TOK_THREADS * k];
+  for (int k = 0; k < WV; ++k) wst[k] = reinterpret_cast<const float4*>(a.w00)[WFILL_IDX(threadIdx.x + TOK_THREADS * k)];
   const float fo = threadIdx.x < FOLD_N ? a.fold[threadIdx.x] : 0.f;
   const float ba = lane < 8 ? a.b00[lane] : 0.f;
 #pragma unroll
-  for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[threadIdx.x + TOK_THREADS * k] = wst[k];
+  for (int k = 0; k < WV; ++k) reinterpret_cast<float4*>(W0)[WFILL_IDX(threadIdx.x + TOK_THREADS * k)] = wst[k];
   if (threadIdx.x < FOLD_N) fold[threadIdx.x] = fo;
   RSTAMP(2, 1);   // (wave 0's weight share landed: stored to the LDS)
   if (pre) {
@@ -656,7 +671,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
   constexpr int WE = 8 * C768 / 4 / TOK_THREADS;   // 3 float4 of conv1x1 (channel-major, a.w1 = W1t) per thread
   float4 wst[WE];
 #pragma unroll
-  for (int k = 0; k < WE; ++k) wst[k] = reinterpret_cast<const float4*>(a.w1)[threadIdx.x + TOK_THREADS * k];
+  for (int k = 0; k < WE; ++k) wst[k] = reinterpret_cast<const float4*>(a.w1)[WFILL_IDX(threadIdx.x + TOK_THREADS * k)];
   float cs[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -664,7 +679,7 @@ __global__ __launch_bounds__(TOK_THREADS) __attribute__((amdgpu_waves_per_eu(LNP
     cs[k] = e < C768 ? a.b1[e] : e < 2 * C768 ? a.w[e - C768] : e < 3 * C768 ? a.b[e - 2 * C768] : 0.f;
   }
 #pragma unroll
-  for (int k = 0; k < WE; ++k) reinterpret_cast<float4*>(W1t)[threadIdx.x + TOK_THREADS * k] = wst[k];
+  for (int k = 0; k < WE; ++k) reinterpret_cast<float4*>(W1t)[WFILL_IDX(threadIdx.x + TOK_THREADS * k)] = wst[k];
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     const int e = threadIdx.x + TOK_THREADS * k;
@@ -857,7 +872,7 @@ __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int row
                                                          bf16_t* feat, bf16_t* feat_lo, float fscale, float* dbg,
                                                          const RowReduce rr) {
   const int L = Lz + Lx;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= B * L) return;
   const int bs = r / L, s = r - bs * L;
   const LnAffine af = load_affine(w, b, lane);
@@ -880,9 +895,9 @@ __global__ __launch_bounds__(256) void final_norm_kernel(const float* X, int row
 void final_norm_recover(const float* X, int rows_per_seq, const int* slot2pos, const float* w, const float* b,
                         int B, int Lz, int Lx, bf16_t* feat, bf16_t* feat_lo, float feat_scale, float* feat_f32_dbg,
                         hipStream_t s, const RowReduce& rr) {
-  const int rows = B * (Lz + Lx);
-  hipLaunchKernelGGL(final_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, X, rows_per_seq, slot2pos, w, b, B,
-                     Lz, Lx, feat, feat_lo, feat_scale, feat_f32_dbg, rr);
+  const int rows = B * (Lz + Lx), rpb = rows_per_block(rows);
+  hipLaunchKernelGGL(final_norm_kernel, dim3((rows + rpb - 1) / rpb), dim3(64 * rpb), 0, s, X, rows_per_seq, slot2pos,
+                     w, b, B, Lz, Lx, feat, feat_lo, feat_scale, feat_f32_dbg, rr);
 }
 
 }  // namespace mmt
