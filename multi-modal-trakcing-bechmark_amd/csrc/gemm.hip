@@ -1705,6 +1705,226 @@ static bool launch256s_epi(const GemmArgs& a, int epi, hipStream_t s, bool t320 
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// f16x3 128 x 256 tile in the staggered two-group structure of gemm256s_kernel (round 6), for the N = 768 fp32-output
+// GEMMs (proj, fc2, patch): 3 column tiles of 256 and one row block of 128 per tile, so the launch has a tile for about
+// every CU where the 256-row kernel leaves half of them idle and the 1-barrier-per-K-tile 128 x 128 / 128 x 192
+// kernels issue MFMAs only ~1/3 of the time.  A 32-deep K-tile is three half-tiles (A rows 0..127, W rows 0..127,
+// W rows 128..255; hi then lo plane, 16 KB each) in a 3-stage LDS ring (144 KB), multiplied in two phases: A x W0
+// into acc[0], A x W1 into acc[1] (per wave 64 x 32 of each 128 x 128 quadrant: 4 x 2 fragment pairs x 3 products =
+// 24 MFMAs per phase).  Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's MFMAs overlap the
+// other's fragment reads and load issue.  K-tile kt + 2's loads go out at the start of K-tile kt into the stage K-tile
+// kt - 1 left (both groups are past their last read of it: group 0 passed the barrier where group 1 finished reading
+// kt - 1, group 1 the one where group 0 did), and each wave waits for its own loads of K-tile kt + 1 before the barrier
+// that precedes the first read of them.  Every fragment read completes (lgkmcnt 0) before the group's next barrier.
+// Each output accumulates over the same K order, three products per 32-deep step in the same order, as every other
+// f16x3 tile: the same bits as gemm_kernel / gemm256s_kernel (test_gemm_f16x3_w256).
+#ifndef W256_LGKM
+#define W256_LGKM 0
+#endif
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm128w_kernel(const GemmArgs args) {
+  static_assert(EPI == EPI_RESID_F32 || EPI == EPI_F32 || EPI == EPI_POS_F32, "fp32-output epilogues");
+  constexpr int PW0 = 8192, PW1 = 16384, STG = 24576;   // elements: A (hi, lo) at 0, W0 (hi, lo), W1 (hi, lo)
+  __shared__ __attribute__((aligned(16))) bf16_t smem[3 * STG];   // the epilogue's [128][256] fp32 tile reuses it
+  GEMM_STAMP_DECL;
+  const GemmGroup& g = args.g[blockIdx.z];
+  const int M = args.M, K = args.K;
+  const int tiles_m = (M + 127) / 128, tiles_n = args.N / 256, ntiles = tiles_m * tiles_n;
+  const int b = blockIdx.x, x = b & 7, j = b >> 3;
+  const int q = ntiles >> 3, r8 = ntiles & 7;
+  const int id = (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + j;
+  int tm, tn;
+  tile_of(id, tiles_m, tiles_n, args.gm, tm, tn);
+  const int m0 = tm * 128, n0 = tn * 256;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  GEMM_STAMP(0);
+  // the lane's bias chunks, requested before the operand loads (the prologue's counted wait retires them)
+  const rsrc_t rB = make_rsrc(g.bias, g.bias ? (int64_t)args.N * 4 : 0);
+  float4 bq[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) bq[h][jj] = epi_bias(rB, n0 + h * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4);
+
+  // half-tile loads: a wave-instruction fills 16 rows x 64 B (swzk<32> image, source chunk pre-swizzled); rows past M
+  // fall outside the A resources and read zeros
+  const int chunk = ((lane & 3) ^ ((lane >> 4) & 2)) * 16;
+  const int lrow = wave * 16 + (lane >> 2);
+  const rsrc_t rA = make_rsrc(g.A + (int64_t)m0 * g.lda, (int64_t)(M - m0) * g.lda * 2);
+  const rsrc_t rAl = make_rsrc(g.A_lo + (int64_t)m0 * g.lda, (int64_t)(M - m0) * g.lda * 2);
+  const rsrc_t rW = make_rsrc(g.W + (int64_t)n0 * g.ldw, (int64_t)256 * g.ldw * 2);
+  const rsrc_t rWl = make_rsrc(g.W_lo + (int64_t)n0 * g.ldw, (int64_t)256 * g.ldw * 2);
+  const uint32_t va = (uint32_t)(lrow * g.lda * 2 + chunk), vw = (uint32_t)(lrow * g.ldw * 2 + chunk);
+  const uint32_t vw1 = vw + (uint32_t)(128u * g.ldw * 2);
+  const int nk = K / 32;
+  // half-tile issue: A and W0 of a K-tile together (four wave-instructions), W1 alone (two)
+  auto issue_aw0 = [&](int kt) {
+    bf16_t* const d = smem + (kt % 3) * STG + wave * 512;
+    const int soff = kt * 64;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lptr_t)d, 16, va, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rAl, (lptr_t)(d + 4096), 16, va, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lptr_t)(d + PW0), 16, vw, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rWl, (lptr_t)(d + PW0 + 4096), 16, vw, soff, 0, 0);
+  };
+  auto issue_w1 = [&](int kt) {
+    bf16_t* const d = smem + (kt % 3) * STG + wave * 512;
+    const int soff = kt * 64;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lptr_t)(d + PW1), 16, vw1, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rWl, (lptr_t)(d + PW1 + 4096), 16, vw1, soff, 0, 0);
+  };
+  f32x4 acc[2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[a][i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 Ah[4], Al[4], Bh[2], Bl[2];
+  const int c = lane >> 4;
+  auto read_a = [&](const bf16_t* S) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 64 + i * 16 + (lane & 15);
+      Ah[i] = *reinterpret_cast<const bf16x8*>(S + swzk<32>(row, c));
+      Al[i] = *reinterpret_cast<const bf16x8*>(S + 4096 + swzk<32>(row, c));
+    }
+  };
+  auto read_b = [&](const bf16_t* S) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = wc * 32 + jj * 16 + (lane & 15);
+      Bh[jj] = *reinterpret_cast<const bf16x8*>(S + swzk<32>(row, c));
+      Bl[jj] = *reinterpret_cast<const bf16x8*>(S + 4096 + swzk<32>(row, c));
+    }
+  };
+  auto mma = [&](f32x4 (&C)[4][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bh[jj], Ah[i], C[i][jj]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bl[jj], Ah[i], C[i][jj]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) C[i][jj] = mfma16<true>(Bh[jj], Al[i], C[i][jj]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // Each half-tile slot is refilled as soon as both groups are past their last read of it: A / W0 of K-tile kt + 3 at
+  // phase 1 of K-tile kt (the slots of A / W0 (kt), last read in phase 0), W1 of kt + 2 at phase 0 of kt (the slot of
+  // W1 (kt - 1)); so every half-tile is requested five phases before its first read.  A wave waits for its own loads of
+  // a half-tile before the barrier that precedes the first read of it by either group: group 1 (one barrier behind)
+  // before its pre-MFMA barrier, group 0 before its post-MFMA one.  Counts: the wave-instructions issued after the
+  // awaited half-tile (12 in steady state).
+  issue_aw0(0);
+  issue_w1(0);
+  if (nk > 1) {
+    issue_aw0(1);
+    issue_w1(1);
+  }
+  if (nk > 2) issue_aw0(2);
+  vm_wait_rt<12>((nk > 1 ? 6 : 0) + (nk > 2 ? 4 : 0) + 2);   // A / W0 of K-tile 0 landed
+  __builtin_amdgcn_s_barrier();
+  GEMM_STAMP(1);
+  if (wr) __builtin_amdgcn_s_barrier();   // stagger: waves 4-7 one barrier behind
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16_t* S = smem + (kt % 3) * STG;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk, n3 = kt + 3 < nk;
+    // phase 0: A x W0
+    if (n2) issue_w1(kt + 2);
+    read_b(S + PW0);
+    read_a(S);
+    if (W256_LGKM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int c0 = (n1 ? 6 : 0) + (n2 ? 6 : 0);   // issued after W1 (kt)
+    if (wr) vm_wait_rt<12>(c0);
+    __builtin_amdgcn_s_barrier();
+    mma(acc[0]);
+    if (!wr) vm_wait_rt<12>(c0);
+    __builtin_amdgcn_s_barrier();
+    // phase 1: A x W1
+    if (n3) issue_aw0(kt + 3);
+    read_b(S + PW1);
+    if (W256_LGKM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int c1 = 2 + (n2 ? 6 : 0) + (n3 ? 4 : 0);   // issued after A / W0 (kt + 1)
+    if (wr && n1) vm_wait_rt<12>(c1);
+    __builtin_amdgcn_s_barrier();
+    mma(acc[1]);
+    if (!wr && n1) vm_wait_rt<12>(c1);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (!wr) __builtin_amdgcn_s_barrier();  // balance the stagger
+  GEMM_STAMP(2);
+
+  // epilogue: the residual / position chunks requested first, acc * inv + bias staged through the LDS ([128][256]
+  // fp32, 16-B chunks XOR-swizzled by row), then every lane stores whole 16-B row chunks of R + value (store4v's
+  // arithmetic: the same bits)
+  using LF = LdsTile<EPI_F32, 256>;
+  char* const lds = reinterpret_cast<char*>(smem);
+  const int tid = threadIdx.x;
+  u32x4 rv[epi_has_r(EPI) ? 16 : 1];
+  if constexpr (epi_has_r(EPI)) {
+    const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int idx = tid + k * 512, r = idx >> 6, cc = idx & 63, m = m0 + r;
+      const int row = EPI == EPI_POS_F32 ? m % args.pos_rows : m;
+      const uint32_t o = m < M ? (uint32_t)(((int64_t)row * g.ldr + n0 + 4 * cc) * 4) : kBufOob;
+      rv[k] = __builtin_amdgcn_raw_buffer_load_b128(rR, o, 0, 0);
+    }
+  }
+  __syncthreads();   // every wave's last fragment reads are done
+#pragma unroll
+  for (int qd = 0; qd < 2; ++qd)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const f32x4& a = acc[qd][i][jj];
+        const float4 bv = bq[qd][jj];
+        const float v[4] = {a[0] * g.inv + bv.x, a[1] * g.inv + bv.y, a[2] * g.inv + bv.z, a[3] * g.inv + bv.w};
+        LF::put(lds, wr * 64 + i * 16 + (lane & 15), qd * 128 + wc * 32 + jj * 16 + (lane >> 4) * 4, v);
+      }
+  __syncthreads();
+  const int rows = max(0, min(128, M - m0));
+  const rsrc_t rC = make_rsrc(static_cast<float*>(g.C) + (int64_t)m0 * g.ldc, (int64_t)rows * g.ldc * 4);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int idx = tid + k * 512, r = idx >> 6, cc = idx & 63;
+    f32x4 v = *reinterpret_cast<const f32x4*>(lds + r * 256 * 4 + ((cc ^ (r & LF::MASK)) << 4));
+    if constexpr (epi_has_r(EPI)) v = __builtin_bit_cast(f32x4, rv[k]) + v;
+    const uint32_t go = r < rows ? (uint32_t)(((int64_t)r * g.ldc + n0 + 4 * cc) * 4) : kBufOob;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rC, go, 0, 0);
+  }
+  GEMM_STAMP(3);
+}
+
+static int super_rows(int tiles_m, int K);
+
+template <int EPI>
+static void launch128w(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  const int tiles_m = (a.M + 127) / 128;
+  a.gm = super_rows(tiles_m, a.K);
+  hipLaunchKernelGGL((gemm128w_kernel<EPI>), dim3(tiles_m * (a.N / 256), 1, a.groups), dim3(512), 0, s, a);
+}
+
+static bool launch128w_epi(const GemmArgs& a, int epi, hipStream_t s) {
+  if (a.N % 256 || a.K % 32 || a.K < 32 || a.amode != A_DENSE) return false;
+  switch (epi) {
+    case EPI_RESID_F32: return launch128w<EPI_RESID_F32>(a, s), true;
+    case EPI_F32: return launch128w<EPI_F32>(a, s), true;
+    case EPI_POS_F32: return launch128w<EPI_POS_F32>(a, s), true;
+    default: return false;
+  }
+}
+
 // super-tile height (tile rows walked together, column-major inside): 8 rows x all columns keeps a short-K
 // GEMM's weight slab shared per XCD; a long-K GEMM (fc2: K = 3072; the head conv: K = 6912) re-fetches its
 // large A row blocks once per column tile unless the row's column tiles run close together (gm = 4: head
@@ -1880,6 +2100,17 @@ static void gemm_dispatch(const GemmArgs& a, int epi, hipStream_t s) {
       const int r256 = (conc * ((a.M + 255) / 256) * (a.N / 256) + slots - 1) / slots;
       const int r320 = (conc * ((a.M + 319) / 320) * (a.N / 256) + slots - 1) / slots;
       use320 = t320 == 2 || 5 * r320 < 4 * r256;
+    }
+    // 128 x 256 two-group tiles (gemm128w_kernel) for the fp32-output N = 768 GEMMs where the 256-row kernel's tiles
+    // would leave most CUs idle.  MMT_W256: 0 never, 1 the rule, 2 always (tuning); mmt_gemm_force_config(128) pins it
+    static const int w256 = getenv("MMT_W256") ? atoi(getenv("MMT_W256")) : 1;
+    if (g_force_cfg == 128 && launch128w_epi(a, epi, s)) return;
+    if (w256 && g_force_cfg < 0 && epi == EPI_RESID_F32 && a.groups == 1 && a.N % 256 == 0 && a.N < 2048) {
+      // the rule: its tiles fill at least 90 % of one round of the one-workgroup-per-CU slots, counting the concurrent
+      // stream part, where 128 x 128 tiles would take two rounds or more
+      const int conc = a.conc > 1 ? a.conc : 1, slots = num_cus();
+      const int tw = conc * ((a.M + 127) / 128) * (a.N / 256), t128 = conc * ((a.M + 127) / 128) * (a.N / 128);
+      if ((w256 == 2 || (tw <= slots && 10 * tw >= 9 * slots && t128 > slots)) && launch128w_epi(a, epi, s)) return;
     }
     const bool forced = g_force_cfg == 320 || g_force_cfg == 256;   // tests: pin the tile (any tile count)
     if (forced) use320 = g_force_cfg == 320 && (epi == EPI_BF16 || epi == EPI_GELU_BF16);

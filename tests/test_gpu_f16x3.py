@@ -7,8 +7,8 @@ mmt_op_attention_f16x3 (include/mmtrack.h) on the path's shapes:
 
 * M = 10240 (32 sequences x 320 tokens), N = 2304 / 3072, K = 768: the 256 x 256 eight-phase kernel
   gemm256s_kernel<EPI> (qkv EPI 0, fc1 EPI 1);
-* N = 768, K = 768 (proj, EPI 2) and K = 3072 (fc2, EPI 2): the 128 x 128 f16x3 gemm_kernel (32- and 64-deep
-  K-tiles); EPI 4 (patch embed);
+* N = 768, K = 768 (proj, EPI 2) and K = 3072 (fc2, EPI 2): the 128 x 128 / 128 x 192 f16x3 gemm_kernel (32- and
+  64-deep K-tiles) and, where its tiles fill one round, the 128 x 256 two-group gemm128w_kernel; EPI 4 (patch embed);
 * one sequence's few-tile shapes (M = 320 / 153): the 64 x 64 kernels and the split-K path;
 * attention at B * heads >= 128: attn_kernel<8, true>; one sequence: the key-split attn_kernel<4, true, 1, true>.
 
@@ -67,7 +67,7 @@ def _gemm(lib, Ah, Al, Wh, Wl, bias, C, Cl, inv, out_scale, epi, R=None, M=None)
     (10240, 3072, 768, 1),    # fc1, 32 sequences: gemm256s_kernel<1>
     (7808, 3072, 768, 1),     # fc1 after CE (244 tokens), M % 256 != 0
     (4896, 2304, 768, 0),     # qkv after the last CE (153 tokens)
-    (10240, 768, 768, 2),     # proj: 128 x 128, 32-deep K-tiles
+    (10240, 768, 768, 2),     # proj, 32 x 320 rows in one launch: the 128 x 256 two-group tile (240 tiles, one round)
     (4896, 768, 3072, 2),     # fc2 after the last CE: 128 x 128, 64-deep K-tiles
     (7808, 768, 3072, 2),     # fc2 (244 tokens): 128 x 192 tiles (one round of them against two of 128 x 128)
     (6080, 768, 768, 2),      # proj (190 tokens): 128 x 192, the residual chunks loaded in the drain
@@ -183,6 +183,63 @@ def test_gemm_f16x3_256s_residual(lib, M, N, K):
     print(f"f16x3 gemm 256x256 residual M={M} N={N} K={K}: max|err| {err:.3e} (tol {tol:.3e})")
     assert torch.isfinite(C).all()
     assert err <= tol
+
+
+@pytest.mark.parametrize("M,N,K,epi", [
+    (5120, 768, 768, 2),      # proj, one stream half of 16 x 320 tokens (the default rule's shape)
+    (3904, 768, 3072, 2),     # fc2, a half of 16 x 244 tokens
+    (3040, 768, 3072, 2),     # fc2, a half of 16 x 190 tokens: M % 128 = 96
+    (700, 768, 128, 2),       # forced: K = 128 (four K-tiles: the ring's tail), M % 128 = 60
+    (130, 768, 64, 2),        # forced: K = 64 (two K-tiles: the prologue's second load, no steady step), M = 128 + 2
+    (4096, 768, 768, 4),      # forced: fp32 output without a residual (patch-embed shape)
+    (2048, 768, 768, 6),      # forced: the position epilogue (row m % pos_rows; the op entry fixes pos_rows = 1)
+])
+def test_gemm_f16x3_w256(lib, M, N, K, epi):
+    """The 128 x 256 two-group tile (gemm128w_kernel<EPI>: three half-tiles per 32-deep K-tile in a 3-stage ring, two
+    MFMA phases, waves 4-7 one barrier behind) against fp64 and bit for bit against the 256 x 256 eight-phase tile,
+    which accumulates every output over the same K order (attn.py proj, timm Mlp fc2 + the block's residual adds,
+    attn_blocks.py:93-104; patch_embed.py:20 for the fp32 / position epilogues)."""
+    g = torch.Generator(device="cuda").manual_seed(M + 5 * N + K + epi)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g) * (0.5 / math.sqrt(K))
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    sa, sw = range_scale(A), range_scale(W)
+    Ah, Al, A64 = split(A, sa)
+    Wh, Wl, W64 = split(W, sw)
+    ref = A64 @ W64.t() + bias.double()
+    pos_rows = 1   # mmt_op_gemm_f16x3's position epilogue: every row adds R's row 0
+    R = torch.randn(M if epi == 2 else pos_rows, N, device="cuda", generator=g)
+    outs = []
+    try:
+        for cfg in (128, 256):
+            lib.mmt_gemm_force_config(cfg)
+            if epi == 2:
+                C = R.clone()
+                _gemm(lib, Ah, Al, Wh, Wl, bias, C, None, 1.0 / (sa * sw), 1.0, epi, R=C)   # in place
+            else:
+                C = torch.full((M, N), float("nan"), device="cuda")
+                rc = lib.mmt_op_gemm_f16x3(Ah.data_ptr(), Al.data_ptr(), K, Wh.data_ptr(), Wl.data_ptr(), K,
+                                           bias.data_ptr(), C.data_ptr(), None, N,
+                                           R.data_ptr() if epi == 6 else None, N if epi == 6 else 0,
+                                           M, N, K, epi, 1.0 / (sa * sw), 1.0, 0, 0, _stream())
+                assert rc == 0
+                torch.cuda.synchronize()
+            outs.append(C)
+    finally:
+        lib.mmt_gemm_force_config(-1)
+    C, C2 = outs
+    if epi == 2:
+        y = R.double() + ref
+    elif epi == 6:
+        y = ref + R.double()[torch.arange(M, device="cuda") % pos_rows]
+    else:
+        y = ref
+    err = float((C.double() - y).abs().max())
+    tol = 1e-5 * float(ref.abs().max()) + 4e-7 * float(y.abs().max())
+    print(f"f16x3 gemm 128x256 M={M} N={N} K={K} epi={epi}: max|err| {err:.3e} (tol {tol:.3e})")
+    assert torch.isfinite(C).all()
+    assert err <= tol
+    assert torch.equal(C.view(torch.int32), C2.view(torch.int32))
 
 
 @pytest.mark.parametrize("B,N", [(32, 320), (16, 320), (16, 244), (16, 153), (16, 720), (12, 190), (1, 320),

@@ -14,8 +14,12 @@ from mmtrack_amd import _lib  # noqa: E402
 lib = _lib.load()
 SHAPES = {"fc2_half": (5120, 768, 3072, 2), "proj_half": (5120, 768, 768, 2), "fc2_153": (2448, 768, 3072, 2),
           "qkv_half": (5120, 2304, 768, 0), "fc1_half": (5120, 3072, 768, 1), "qkv_b1": (320, 2304, 768, 0),
-          "fc1_b1": (320, 3072, 768, 1), "fc1_b8": (2560, 3072, 768, 1), "qkv_b8": (2560, 2304, 768, 0)}
+          "fc1_b1": (320, 3072, 768, 1), "fc1_b8": (2560, 3072, 768, 1), "qkv_b8": (2560, 2304, 768, 0),
+          "fc2_full": (10240, 768, 3072, 2), "proj_full": (10240, 768, 768, 2), "fc2_244": (7808, 768, 3072, 2)}
+# MMT_FORCE: pin the tile (mmt_gemm_force_config: 128 = the 128 x 256 two-group kernel, 256 = 256 x 256)
 s = torch.cuda.current_stream().cuda_stream
+if os.environ.get("MMT_FORCE"):
+    lib.mmt_gemm_force_config(int(os.environ["MMT_FORCE"]))
 st = torch.zeros(65536 + 256 * 2 * 288, dtype=torch.int64, device="cuda")
 for name in os.environ.get("SHAPES", ",".join(SHAPES)).split(","):
     M, N, K, epi = SHAPES[name]
