@@ -1716,12 +1716,11 @@ static bool launch256s_epi(const GemmArgs& a, int epi, hipStream_t s, bool t320 
 // other's fragment reads and load issue.  K-tile kt + 2's loads go out at the start of K-tile kt into the stage K-tile
 // kt - 1 left (both groups are past their last read of it: group 0 passed the barrier where group 1 finished reading
 // kt - 1, group 1 the one where group 0 did), and each wave waits for its own loads of K-tile kt + 1 before the barrier
-// that precedes the first read of them.  Every fragment read completes (lgkmcnt 0) before the group's next barrier.
+// that precedes the first read of them.  Fragment reads are not drained before a barrier (the MFMA after it waits for
+// them): a slot's refill is issued after a later barrier and lands hundreds of cycles after any read issued before it
+// (drained, the K loop ran 10 % slower; the eight-phase kernel relies on the same order).
 // Each output accumulates over the same K order, three products per 32-deep step in the same order, as every other
 // f16x3 tile: the same bits as gemm_kernel / gemm256s_kernel (test_gemm_f16x3_w256).
-#ifndef W256_LGKM
-#define W256_LGKM 0
-#endif
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm128w_kernel(const GemmArgs args) {
   static_assert(EPI == EPI_RESID_F32 || EPI == EPI_F32 || EPI == EPI_POS_F32, "fp32-output epilogues");
@@ -1841,7 +1840,6 @@ __global__ __launch_bounds__(512) void gemm128w_kernel(const GemmArgs args) {
     if (n2) issue_w1(kt + 2);
     read_b(S + PW0);
     read_a(S);
-    if (W256_LGKM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int c0 = (n1 ? 6 : 0) + (n2 ? 6 : 0);   // issued after W1 (kt)
     if (wr) vm_wait_rt<12>(c0);
     __builtin_amdgcn_s_barrier();
@@ -1851,7 +1849,6 @@ __global__ __launch_bounds__(512) void gemm128w_kernel(const GemmArgs args) {
     // phase 1: A x W1
     if (n3) issue_aw0(kt + 3);
     read_b(S + PW1);
-    if (W256_LGKM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int c1 = 2 + (n2 ? 6 : 0) + (n3 ? 4 : 0);   // issued after A / W0 (kt + 1)
     if (wr && n1) vm_wait_rt<12>(c1);
     __builtin_amdgcn_s_barrier();
@@ -1870,6 +1867,7 @@ __global__ __launch_bounds__(512) void gemm128w_kernel(const GemmArgs args) {
   const int tid = threadIdx.x;
   u32x4 rv[epi_has_r(EPI) ? 16 : 1];
   if constexpr (epi_has_r(EPI)) {
+    // (requested at kernel entry instead, they moved ~5k cycles from the epilogue into the prologue: level)
     const rsrc_t rR = epi_resid_rsrc<EPI>(g, args, M);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
