@@ -29,7 +29,7 @@ def epi_of(name):
     if not m:
         return None
     args = [a.strip() for a in m.group(2).split(",")]
-    if m.group(1) in ("gemm256s_kernel", "gemm256_kernel"):
+    if m.group(1) in ("gemm256s_kernel", "gemm256_kernel", "gemm128w_kernel"):
         return int(args[0])
     if m.group(1) == "gemm_kernel":
         return int(args[4])

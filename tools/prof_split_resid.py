@@ -8,10 +8,13 @@ import csv
 import statistics
 import sys
 
-NAME = "gemm_kernel<128, 128, 4, 2, 2, 0, true, 2, 64>"
+NAMES = ("gemm_kernel<128, 128, 4, 2, 2, 0, true, 2, 64>", "gemm128w_kernel<2>")   # (the 128 x 256 tile: the 320-token layers)
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000 for r in rows if NAME in r["Kernel_Name"]]
-if not d or len(d) % 2:
-    raise SystemExit(f"expected proj / fc2 pairs of {NAME}, found {len(d)} launches")
-print(f"{len(d)} launches of {NAME}: proj {statistics.mean(d[0::2]):.2f} us, fc2 {statistics.mean(d[1::2]):.2f} us "
-      f"(mean per launch, {len(d) // 2} each)")
+for NAME in NAMES:
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000 for r in rows if NAME in r["Kernel_Name"]]
+    if not d:
+        continue
+    if len(d) % 2:
+        raise SystemExit(f"expected proj / fc2 pairs of {NAME}, found {len(d)} launches")
+    print(f"{len(d)} launches of {NAME}: proj {statistics.mean(d[0::2]):.2f} us, fc2 {statistics.mean(d[1::2]):.2f} us "
+          f"(mean per launch, {len(d) // 2} each)")
