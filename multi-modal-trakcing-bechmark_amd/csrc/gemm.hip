@@ -1707,18 +1707,16 @@ static bool launch256s_epi(const GemmArgs& a, int epi, hipStream_t s, bool t320 
 
 // ---------------------------------------------------------------------------------------------------
 // f16x3 128 x 256 tile in the staggered two-group structure of gemm256s_kernel (round 6), for the N = 768 fp32-output
-// GEMMs (proj, fc2, patch): 3 column tiles of 256 and one row block of 128 per tile, so the launch has a tile for about
-// every CU where the 256-row kernel leaves half of them idle and the 1-barrier-per-K-tile 128 x 128 / 128 x 192
-// kernels issue MFMAs only ~1/3 of the time.  A 32-deep K-tile is three half-tiles (A rows 0..127, W rows 0..127,
-// W rows 128..255; hi then lo plane, 16 KB each) in a 3-stage LDS ring (144 KB), multiplied in two phases: A x W0
-// into acc[0], A x W1 into acc[1] (per wave 64 x 32 of each 128 x 128 quadrant: 4 x 2 fragment pairs x 3 products =
-// 24 MFMAs per phase).  Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's MFMAs overlap the
-// other's fragment reads and load issue.  K-tile kt + 2's loads go out at the start of K-tile kt into the stage K-tile
-// kt - 1 left (both groups are past their last read of it: group 0 passed the barrier where group 1 finished reading
-// kt - 1, group 1 the one where group 0 did), and each wave waits for its own loads of K-tile kt + 1 before the barrier
-// that precedes the first read of them.  Fragment reads are not drained before a barrier (the MFMA after it waits for
-// them): a slot's refill is issued after a later barrier and lands hundreds of cycles after any read issued before it
-// (drained, the K loop ran 10 % slower; the eight-phase kernel relies on the same order).
+// GEMMs (proj, fc2): 3 column tiles of 256 and one row block of 128 per tile -- where its tiles fill one round of the
+// one-workgroup-per-CU slots and 128 x 128 tiles would take two (the 256-row kernel would leave half the CUs idle).
+// A 32-deep K-tile is three half-tiles (A rows 0..127, W rows 0..127, W rows 128..255; hi then lo plane, 16 KB each)
+// in a 3-stage LDS ring (144 KB), multiplied in two phases: A x W0 into acc[0], A x W1 into acc[1] (per wave 64 x 32
+// of each 128 x 128 quadrant: 4 x 2 fragment pairs x 3 products = 24 MFMAs per phase; A's fragments are read once per
+// K-tile).  Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's MFMAs overlap the other's fragment
+// reads and load issue; the half-tile slots are refilled five phases ahead of their first read (the loop below).
+// Fragment reads are not drained before a barrier (the MFMA after it waits for them): a slot's refill is issued after
+// a later barrier and lands hundreds of cycles after any read issued before it (drained, the K loop ran 10 % slower;
+// the eight-phase kernel relies on the same order).  Per-block stamps: ~1 000 cycles per phase against 768 of MFMAs.
 // Each output accumulates over the same K order, three products per 32-deep step in the same order, as every other
 // f16x3 tile: the same bits as gemm_kernel / gemm256s_kernel (test_gemm_f16x3_w256).
 template <int EPI>
