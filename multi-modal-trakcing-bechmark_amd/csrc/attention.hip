@@ -181,13 +181,32 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
     if (kb0 < N) fetch(kb0);
   }
   int stage = 0;
+#ifdef ATTN_STAMPS
+  // tuning build (abx variant, never the product): wave 0's cycles per loop part, summed over the key tiles and printed
+  // by the first workgroups -- wait (tile landed + barrier + next issue), S issue, softmax (incl. the S results), PV issue
+  unsigned long long st_w = 0, st_s = 0, st_x = 0, st_p = 0, st_t0 = __builtin_amdgcn_s_memtime(), st_q = 0, st_e = 0;
+  int st_n = 0;
+#define ATTN_ST(v)                                            \
+  do {                                                        \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    v += t_ - st_q;                                           \
+    st_q = t_;                                                \
+  } while (0)
+#else
+#define ATTN_ST(v) do { } while (0)
+#endif
   for (int kb = kb0; kb < N; kb += KSTEP) {
+#ifdef ATTN_STAMPS
+    st_q = __builtin_amdgcn_s_memtime();
+    ++st_n;
+#endif
     if constexpr (DMA) {
       // this tile's pieces landed (the only loads in flight) and every wave is past the previous tile, whose
       // stage then takes the next tile
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (kb + KSTEP < N) issue(kb + KSTEP, stage ^ 1);
+      ATTN_ST(st_w);
     } else {
       tile_sync();
 #pragma unroll
@@ -231,6 +250,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
       // (f16x3: S = (K s)(Q s)^T / s^2 / 8 -- qk_inv, a power of two, is folded into the exponent's scale below:
       // the same bits as scaling the scores, 16 multiplies fewer per tile)
     }
+    ATTN_ST(st_s);
     bf16x8 pf[RB][2], pl[RB][2];
     const bool tail = kb + KB > N;   // only the last key tile has keys past N (wave-uniform)
 #pragma unroll
@@ -307,6 +327,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
         }
     }
 
+    ATTN_ST(st_x);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       // V^T fragment of keys {32u + 4g + 0..3} and {32u + 16 + 4g + 0..3} (the P element order) at
@@ -334,7 +355,14 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
         }
       }
     }
+    ATTN_ST(st_p);
   }
+#ifdef ATTN_STAMPS
+  st_e = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0 && blockIdx.x < 24)
+    printf("attn_stamps block %d waves %d N %d tiles %d: total %llu wait %llu s %llu softmax %llu pv %llu\n", (int)blockIdx.x,
+           WAVES, N, st_n, st_e - st_t0, st_w, st_s, st_x, st_p);
+#endif
 
   if constexpr (KSPLIT) {
     // merge the waves' partial softmax states in wave order: m = max m_w, l = sum l_w e^(m_w - m),
