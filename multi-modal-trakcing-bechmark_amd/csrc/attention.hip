@@ -183,8 +183,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
   int stage = 0;
 #ifdef ATTN_STAMPS
   // tuning build (abx variant, never the product): wave 0's cycles per loop part, summed over the key tiles and printed
-  // by the first workgroups -- wait (tile landed + barrier + next issue), S issue, softmax (incl. the S results), PV issue
-  unsigned long long st_w = 0, st_s = 0, st_x = 0, st_p = 0, st_t0 = __builtin_amdgcn_s_memtime(), st_q = 0, st_e = 0;
+  // by the first workgroups -- landed (this tile's DMA waited for), wait (the barrier + the next tile's issue), S issue,
+  // softmax (incl. the S results), PV issue
+  unsigned long long st_l = 0, st_w = 0, st_s = 0, st_x = 0, st_p = 0, st_t0 = __builtin_amdgcn_s_memtime(), st_q = 0, st_e = 0;
   int st_n = 0;
 #define ATTN_ST(v)                                            \
   do {                                                        \
@@ -204,6 +205,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
       // this tile's pieces landed (the only loads in flight) and every wave is past the previous tile, whose
       // stage then takes the next tile
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      ATTN_ST(st_l);
       __builtin_amdgcn_s_barrier();
       if (kb + KSTEP < N) issue(kb + KSTEP, stage ^ 1);
       ATTN_ST(st_w);
@@ -360,8 +362,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(WAVE
 #ifdef ATTN_STAMPS
   st_e = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0 && blockIdx.x < 24)
-    printf("attn_stamps block %d waves %d N %d tiles %d: total %llu wait %llu s %llu softmax %llu pv %llu\n", (int)blockIdx.x,
-           WAVES, N, st_n, st_e - st_t0, st_w, st_s, st_x, st_p);
+    printf("attn_stamps block %d waves %d N %d tiles %d: total %llu wait %llu s %llu softmax %llu pv %llu landed %llu\n",
+           (int)blockIdx.x, WAVES, N, st_n, st_e - st_t0, st_w, st_s, st_x, st_p, st_l);
 #endif
 
   if constexpr (KSPLIT) {

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6 (second session), run 13: phase stamps of the 32-sequence attention kernel (attn_kernel<8, true>, ATTN_STAMPS
+# Round 6 (second session), run 13 (second pass: the wait split into the tile's landing and the barrier): phase stamps of the 32-sequence attention kernel (attn_kernel<8, true>, ATTN_STAMPS
 # build abx/libattnst.so): wave 0's cycles per key-tile loop part at N = 320 / 244 / 190 / 153, 16 and 32 sequences
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/r6_s2_run13
@@ -14,7 +14,7 @@ for f in ("gpurun_out/r6_s2_run13/stamps32.txt", "gpurun_out/r6_s2_run13/stamps1
         if l.startswith("## "):
             cur = l.strip()
             rows[cur] = []
-        m = re.search(r"tiles (\d+): total (\d+) wait (\d+) s (\d+) softmax (\d+) pv (\d+)", l)
+        m = re.search(r"tiles (\d+): total (\d+) wait (\d+) s (\d+) softmax (\d+) pv (\d+) landed (\d+)", l)
         if m and cur:
             rows[cur].append([int(x) for x in m.groups()])
     for k, v in rows.items():
@@ -22,6 +22,7 @@ for f in ("gpurun_out/r6_s2_run13/stamps32.txt", "gpurun_out/r6_s2_run13/stamps1
             continue
         med = [statistics.median(c) for c in zip(*v)]
         t = med[0]
-        print(f"{k}: {len(v)} blocks, tiles {t:.0f}, per tile cycles: total {med[1] / t:.0f}, wait {med[2] / t:.0f}, "
-              f"S {med[3] / t:.0f}, softmax {med[4] / t:.0f}, PV {med[5] / t:.0f}")
+        print(f"{k}: {len(v)} blocks, tiles {t:.0f}, per tile cycles: total {med[1] / t:.0f}, "
+              f"S {med[3] / t:.0f}, softmax {med[4] / t:.0f}, PV {med[5] / t:.0f}, tile landed {med[6] / t:.0f}, "
+              f"barrier + next issue {med[2] / t:.0f}")
 P
